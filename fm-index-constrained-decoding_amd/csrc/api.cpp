@@ -1,0 +1,706 @@
+// api.cpp -- the extern "C" boundary (include/fmidx.h) over the device index.
+//
+// Host responsibilities only: argument checking, construction orchestration
+// (SA-IS suffix sorting for host-built indexes), persistence, and staging
+// of host arguments for the synchronous SWIG-equivalent calls.  Every query
+// computes on the GPU through the launchers in query.hip.
+#include "fmidx_internal.h"
+#include "sais.h"
+#include "../../include/fmidx.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace fmidx {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+void Index::release() {
+  void* ptrs[] = {wm, D, C, bwt, bm, sa, text, ws};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  wm = nullptr;
+  D = nullptr;
+  C = nullptr;
+  bwt = nullptr;
+  bm = nullptr;
+  sa = nullptr;
+  text = nullptr;
+  ws = nullptr;
+  ws_bytes = 0;
+  built = false;
+  view = DevView{};
+}
+
+}  // namespace fmidx
+
+using fmidx::set_error;
+
+struct fm_index {
+  fmidx::Index idx;
+  std::mutex mu;            // serialises host-API staging buffers / workspace
+  uint64_t* scratch = nullptr;  // small device scratch for scalar results
+};
+
+namespace {
+
+// Makes the handle's device current for the duration of a call.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+#define FM_CHECK_HANDLE(h)                       \
+  do {                                           \
+    if (!(h)) {                                  \
+      set_error("null handle");                  \
+      return -1;                                 \
+    }                                            \
+  } while (0)
+
+#define FM_CHECK_BUILT(h)                        \
+  do {                                           \
+    FM_CHECK_HANDLE(h);                          \
+    if (!(h)->idx.built) {                       \
+      set_error("index not initialized");        \
+      return -1;                                 \
+    }                                            \
+  } while (0)
+
+#define FM_GUARD(h)                               \
+  DeviceGuard guard_((h)->idx.device);            \
+  if (!guard_.ok) {                               \
+    set_error("hipSetDevice(%d) failed", (h)->idx.device); \
+    return -1;                                    \
+  }
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int alloc(size_t count) {
+    if (count == 0) count = 1;
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+    return 0;
+  }
+};
+
+int grow_ws(fm_index* h, size_t bytes) {
+  auto& x = h->idx;
+  if (x.ws_bytes >= bytes) return 0;
+  if (x.ws) FM_HIP(hipFree(x.ws));
+  x.ws = nullptr;
+  x.ws_bytes = 0;
+  FM_HIP(hipMalloc(&x.ws, bytes));
+  x.ws_bytes = bytes;
+  return 0;
+}
+
+// Build from a host text T' (+ sentinel already appended) on the host, then
+// the device structures.
+int build_from_text(fm_index* h, std::vector<uint32_t>& text) {
+  auto& x = h->idx;
+  const uint64_t n = text.size();
+  uint32_t maxs = 0;
+  for (uint32_t v : text) maxs = std::max(maxs, v);
+  std::vector<uint64_t> sa64(n);
+  try {
+    if (n < (1ull << 31)) {
+      std::vector<int32_t> sa;
+      fmidx::suffix_array<int32_t>(text.data(), (int64_t)n, maxs + 1, sa);
+      for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
+    } else {
+      std::vector<int64_t> sa;
+      fmidx::suffix_array<int64_t>(text.data(), (int64_t)n, maxs + 1, sa);
+      for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
+    }
+  } catch (const std::exception& e) {
+    set_error("suffix sorting failed: %s", e.what());
+    return -1;
+  }
+  std::vector<uint32_t> bwt(n);
+  for (uint64_t i = 0; i < n; ++i) bwt[i] = text[sa64[i] == 0 ? n - 1 : sa64[i] - 1];
+  x.release();
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
+  FM_HIP(hipMemcpyAsync(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(x.sa, sa64.data(), n * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(x.text, text.data(), n * 4, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
+}
+
+int initialize_symbols(fm_index* h, const uint64_t* data, uint64_t n) {
+  if (n + 1 > (1ull << 40)) {
+    set_error("text too long for the host builder");
+    return -1;
+  }
+  std::vector<uint32_t> text(n + 1);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t v = data[i];
+    if (v == 0) {
+      set_error("text contains 0 symbol at position %llu (reserved for the sentinel)",
+                (unsigned long long)i);
+      return -1;
+    }
+    if (v >= (1ull << fmidx::kMaxLevels)) {
+      set_error("symbol %llu at position %llu exceeds 2^%d", (unsigned long long)v,
+                (unsigned long long)i, fmidx::kMaxLevels);
+      return -1;
+    }
+    text[i] = (uint32_t)v;
+  }
+  text[n] = 0;
+  return build_from_text(h, text);
+}
+
+// Clamped width of a distinct_count query (fm_index.cpp:127-133); 0 = empty.
+uint64_t distinct_width(uint64_t lo, uint64_t hi, uint64_t n) {
+  if (lo == hi) return 0;
+  if (hi > n) hi = n;
+  if (lo >= hi) return 0;
+  return hi - lo;
+}
+
+// Host-staged batched interval_symbols: syms/counts per range in CSR form.
+int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint64_t m,
+                  std::vector<uint64_t>& syms, std::vector<uint64_t>& counts,
+                  std::vector<uint64_t>& offsets) {
+  auto& x = h->idx;
+  std::vector<uint64_t> cap_off(m + 1, 0);
+  for (uint64_t i = 0; i < m; ++i)
+    cap_off[i + 1] = cap_off[i] + std::min<uint64_t>(distinct_width(lows[i], highs[i], x.n), x.sigma);
+  const uint64_t total = cap_off[m];
+  DevBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_k;
+  if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(total) ||
+      d_cnt.alloc(total) || d_k.alloc(m))
+    return -1;
+  FM_HIP(hipMemcpyAsync(d_lo.p, lows, m * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(d_hi.p, highs, m * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(d_off.p, cap_off.data(), (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
+  if (grow_ws(h, fmidx::distinct_ws_bytes(total))) return -1;
+  if (fmidx::launch_distinct(x.view, d_lo.p, d_hi.p, m, d_off.p, d_syms.p, d_cnt.p, d_k.p, x.ws,
+                             total, x.stream))
+    return -1;
+  std::vector<uint64_t> k(m), s(total), c(total);
+  FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, x.stream));
+  if (total) {
+    FM_HIP(hipMemcpyAsync(s.data(), d_syms.p, total * 8, hipMemcpyDeviceToHost, x.stream));
+    FM_HIP(hipMemcpyAsync(c.data(), d_cnt.p, total * 8, hipMemcpyDeviceToHost, x.stream));
+  }
+  FM_HIP(hipStreamSynchronize(x.stream));
+  offsets.assign(m + 1, 0);
+  syms.clear();
+  counts.clear();
+  for (uint64_t i = 0; i < m; ++i) {
+    if (k[i] == ~0ull) {
+      set_error("distinct_count capacity overflow on range %llu", (unsigned long long)i);
+      return -1;
+    }
+    for (uint64_t j = 0; j < k[i]; ++j) {
+      syms.push_back(s[cap_off[i] + j]);
+      counts.push_back(c[cap_off[i] + j]);
+    }
+    offsets[i + 1] = offsets[i] + k[i];
+  }
+  return 0;
+}
+
+constexpr char kMagic[8] = {'F', 'M', 'I', 'D', 'X', 'A', 'M', 'D'};
+
+}  // namespace
+
+extern "C" {
+
+const char* fm_last_error(void) { return fmidx::g_err.c_str(); }
+
+int fm_device_info(int device, char* buf, size_t cap) {
+  hipDeviceProp_t p;
+  FM_HIP(hipGetDeviceProperties(&p, device));
+  std::snprintf(buf, cap, "%s cu=%d hbm=%zuMB", p.gcnArchName, p.multiProcessorCount,
+                (size_t)(p.totalGlobalMem >> 20));
+  return 0;
+}
+
+int fm_create(fm_index** out, int device) {
+  if (!out) {
+    set_error("null out");
+    return -1;
+  }
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    set_error("no HIP device available (the FM-index engine has no CPU query path)");
+    return -1;
+  }
+  if (device < 0 || device >= count) {
+    set_error("device %d out of range (%d devices)", device, count);
+    return -1;
+  }
+  auto* h = new fm_index();
+  h->idx.device = device;
+  DeviceGuard g(device);
+  if (!g.ok || hipStreamCreateWithFlags(&h->idx.stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&h->scratch), 64 * 8) != hipSuccess) {
+    set_error("device %d initialisation failed", device);
+    delete h;
+    return -1;
+  }
+  *out = h;
+  return 0;
+}
+
+void fm_destroy(fm_index* h) {
+  if (!h) return;
+  {
+    DeviceGuard g(h->idx.device);
+    (void)hipDeviceSynchronize();
+    h->idx.release();
+    if (h->scratch) (void)hipFree(h->scratch);
+    if (h->idx.stream) (void)hipStreamDestroy(h->idx.stream);
+  }
+  delete h;
+}
+
+int fm_initialize(fm_index* h, const uint64_t* data, uint64_t n) {
+  FM_CHECK_HANDLE(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!data && n) {
+    set_error("null data");
+    return -1;
+  }
+  return initialize_symbols(h, data, n);
+}
+
+int fm_initialize_from_file(fm_index* h, const char* path, int width) {
+  FM_CHECK_HANDLE(h);
+  if (width != 1 && width != 2 && width != 4 && width != 8) {
+    set_error("unsupported width %d", width);
+    return -1;
+  }
+  std::ifstream f(path, std::ios::binary);
+  if (!f) {
+    set_error("cannot open %s", path ? path : "(null)");
+    return -1;
+  }
+  std::vector<unsigned char> raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  const uint64_t n = raw.size() / (uint64_t)width;
+  std::vector<uint64_t> data(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t v = 0;
+    for (int b = width - 1; b >= 0; --b) v = (v << 8) | raw[i * width + b];
+    data[i] = v;
+  }
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  return initialize_symbols(h, data.data(), n);
+}
+
+int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n,
+                                  const uint64_t* d_sa, const uint32_t* d_text, void* stream) {
+  FM_CHECK_HANDLE(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto& x = h->idx;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  FM_HIP(hipStreamSynchronize(s));
+  x.release();
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
+  FM_HIP(hipMemcpyAsync(x.bwt, d_bwt, n * 4, hipMemcpyDeviceToDevice, x.stream));
+  if (d_sa) {
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
+    FM_HIP(hipMemcpyAsync(x.sa, d_sa, n * 8, hipMemcpyDeviceToDevice, x.stream));
+  }
+  if (d_text) {
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
+    FM_HIP(hipMemcpyAsync(x.text, d_text, n * 4, hipMemcpyDeviceToDevice, x.stream));
+  }
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
+}
+
+int fm_size(const fm_index* h, uint64_t* out) {
+  FM_CHECK_BUILT(h);
+  *out = h->idx.n;
+  return 0;
+}
+
+int fm_sigma(const fm_index* h, uint64_t* out) {
+  FM_CHECK_BUILT(h);
+  *out = h->idx.sigma;
+  return 0;
+}
+
+int fm_backward_search_step(fm_index* h, uint64_t symbol, uint64_t low, uint64_t high,
+                            uint64_t out[2]) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto& x = h->idx;
+  if (fmidx::launch_step_raw(x.view, symbol, low, high, h->scratch, x.stream)) return -1;
+  FM_HIP(hipMemcpyAsync(out, h->scratch, 16, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return 0;
+}
+
+int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, uint64_t out[2]) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto& x = h->idx;
+  DevBuf<uint64_t> q;
+  if (q.alloc(len)) return -1;
+  if (len) FM_HIP(hipMemcpyAsync(q.p, query, len * 8, hipMemcpyHostToDevice, x.stream));
+  if (fmidx::launch_raw_multi(x.view, q.p, len, h->scratch, x.stream)) return -1;
+  FM_HIP(hipMemcpyAsync(out, h->scratch, 16, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return 0;
+}
+
+int fm_distinct_count_multi(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint64_t m,
+                            uint64_t* out, uint64_t cap, uint64_t* offsets) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  std::vector<uint64_t> s, c, off;
+  if (host_distinct(h, lows, highs, m, s, c, off)) return -1;
+  std::memcpy(offsets, off.data(), (m + 1) * 8);
+  if (2 * s.size() > cap) {
+    set_error("output capacity %llu < %llu", (unsigned long long)cap,
+              (unsigned long long)(2 * s.size()));
+    return -2;
+  }
+  for (size_t i = 0; i < s.size(); ++i) {
+    out[2 * i] = s[i];
+    out[2 * i + 1] = c[i];
+  }
+  return 0;
+}
+
+int fm_distinct_count(fm_index* h, uint64_t low, uint64_t high, uint64_t* out, uint64_t cap,
+                      uint64_t* k) {
+  uint64_t off[2];
+  FM_CHECK_BUILT(h);
+  // two-call protocol: with too small a buffer report the size and fail
+  std::vector<uint64_t> tmp;
+  const uint64_t need = 2 * std::min<uint64_t>(distinct_width(low, high, h->idx.n), h->idx.sigma);
+  tmp.resize(std::max<uint64_t>(need, 1));
+  const int rc = fm_distinct_count_multi(h, &low, &high, 1, tmp.data(), tmp.size(), off);
+  if (rc) return rc;
+  *k = off[1];
+  if (2 * off[1] > cap) {
+    set_error("output capacity %llu < %llu", (unsigned long long)cap,
+              (unsigned long long)(2 * off[1]));
+    return -2;
+  }
+  std::memcpy(out, tmp.data(), 2 * off[1] * 8);
+  return 0;
+}
+
+int fm_distinct(fm_index* h, uint64_t low, uint64_t high, uint64_t* syms, uint64_t cap, uint64_t* k) {
+  FM_CHECK_BUILT(h);
+  const uint64_t need = 2 * std::min<uint64_t>(distinct_width(low, high, h->idx.n), h->idx.sigma);
+  std::vector<uint64_t> tmp(std::max<uint64_t>(need, 1));
+  uint64_t kk = 0;
+  const int rc = fm_distinct_count(h, low, high, tmp.data(), tmp.size(), &kk);
+  if (rc) return rc;
+  *k = kk;
+  if (kk > cap) {
+    set_error("output capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)kk);
+    return -2;
+  }
+  for (uint64_t i = 0; i < kk; ++i) syms[i] = tmp[2 * i];
+  return 0;
+}
+
+int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offsets, uint64_t m,
+                       int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in,
+                       uint64_t* lo_out, uint64_t* hi_out) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto& x = h->idx;
+  if (m == 0) return 0;
+  const uint64_t ntok = (uint64_t)offsets[m];
+  DevBuf<int64_t> d_tok, d_off;
+  DevBuf<uint64_t> d_li, d_hi, d_lo2, d_hi2;
+  if (d_tok.alloc(ntok) || d_off.alloc(m + 1) || d_lo2.alloc(m) || d_hi2.alloc(m)) return -1;
+  if (ntok) FM_HIP(hipMemcpyAsync(d_tok.p, tokens, ntok * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(d_off.p, offsets, (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
+  if (lo_in && hi_in) {
+    if (d_li.alloc(m) || d_hi.alloc(m)) return -1;
+    FM_HIP(hipMemcpyAsync(d_li.p, lo_in, m * 8, hipMemcpyHostToDevice, x.stream));
+    FM_HIP(hipMemcpyAsync(d_hi.p, hi_in, m * 8, hipMemcpyHostToDevice, x.stream));
+  }
+  if (fmidx::launch_search(x.view, d_tok.p, d_off.p, m, shift, d_li.p, d_hi.p, d_lo2.p, d_hi2.p,
+                           x.stream))
+    return -1;
+  FM_HIP(hipMemcpyAsync(lo_out, d_lo2.p, m * 8, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipMemcpyAsync(hi_out, d_hi2.p, m * 8, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return 0;
+}
+
+int fm_locate(fm_index* h, uint64_t row, uint64_t* out) {
+  FM_CHECK_BUILT(h);
+  auto& x = h->idx;
+  if (row >= x.n) {  // fm_index.cpp:170
+    *out = ~0ull;
+    return 0;
+  }
+  if (!x.sa) {
+    set_error("index built without a suffix array: locate unavailable");
+    return -1;
+  }
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  FM_HIP(hipMemcpyAsync(out, x.sa + row, 8, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipStreamSynchronize(x.stream));
+  return 0;
+}
+
+int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, uint64_t cap,
+                    uint64_t* len) {
+  FM_CHECK_BUILT(h);
+  auto& x = h->idx;
+  *len = 0;
+  if (end <= begin) return 0;                // fm_index.cpp:177
+  if (end > x.n) end = x.n;                  // :178
+  if (end <= begin) {
+    // the reference loops (end-begin-1) times in unsigned arithmetic here
+    set_error("extract_text: begin %llu >= clamped end %llu (unbounded in the reference)",
+              (unsigned long long)begin, (unsigned long long)end);
+    return -3;
+  }
+  if (!x.text) {
+    set_error("index built without text: extract_text unavailable");
+    return -1;
+  }
+  const uint64_t L = end - begin;
+  *len = L;
+  const uint64_t w = std::min(L, cap);
+  if (w == 0) return 0;
+  // The LF walk from isa[end-1] emits T'[end-2], T'[end-3], ... cyclically:
+  // out[j] = T'[(end - 2 - j) mod n].  Read those rows of T' from HBM.
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  const uint64_t n = x.n;
+  std::vector<uint32_t> seg;
+  uint64_t j = 0;
+  uint64_t pos = (end + n - 2) % n;          // position of out[0]
+  while (j < w) {
+    const uint64_t run = std::min(w - j, pos + 1);  // pos, pos-1, ..., pos-run+1
+    seg.resize(run);
+    FM_HIP(hipMemcpyAsync(seg.data(), x.text + (pos + 1 - run), run * 4, hipMemcpyDeviceToHost,
+                          x.stream));
+    FM_HIP(hipStreamSynchronize(x.stream));
+    for (uint64_t t = 0; t < run; ++t) out[j + t] = seg[run - 1 - t];
+    j += run;
+    pos = n - 1;
+  }
+  return 0;
+}
+
+int fm_save(fm_index* h, const char* path) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto& x = h->idx;
+  const uint64_t n = x.n;
+  std::vector<uint32_t> bwt(n), text;
+  std::vector<uint64_t> sa;
+  FM_HIP(hipMemcpy(bwt.data(), x.bwt, n * 4, hipMemcpyDeviceToHost));
+  uint32_t flags = 0;
+  if (x.sa) {
+    sa.resize(n);
+    FM_HIP(hipMemcpy(sa.data(), x.sa, n * 8, hipMemcpyDeviceToHost));
+    flags |= 1;
+  }
+  if (x.text) {
+    text.resize(n);
+    FM_HIP(hipMemcpy(text.data(), x.text, n * 4, hipMemcpyDeviceToHost));
+    flags |= 2;
+  }
+  std::ofstream f(path, std::ios::binary | std::ios::trunc);
+  if (!f) {
+    set_error("cannot write %s", path);
+    return -1;
+  }
+  const uint32_t version = 1;
+  f.write(kMagic, 8);
+  f.write(reinterpret_cast<const char*>(&version), 4);
+  f.write(reinterpret_cast<const char*>(&flags), 4);
+  f.write(reinterpret_cast<const char*>(&n), 8);
+  f.write(reinterpret_cast<const char*>(bwt.data()), n * 4);
+  if (flags & 1) f.write(reinterpret_cast<const char*>(sa.data()), n * 8);
+  if (flags & 2) f.write(reinterpret_cast<const char*>(text.data()), n * 4);
+  if (!f) {
+    set_error("write failed: %s", path);
+    return -1;
+  }
+  return 0;
+}
+
+int fm_load(fm_index** out, const char* path, int device) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) {
+    set_error("cannot open %s", path ? path : "(null)");
+    return -1;
+  }
+  char magic[8];
+  uint32_t version = 0, flags = 0;
+  uint64_t n = 0;
+  f.read(magic, 8);
+  f.read(reinterpret_cast<char*>(&version), 4);
+  f.read(reinterpret_cast<char*>(&flags), 4);
+  f.read(reinterpret_cast<char*>(&n), 8);
+  if (!f || std::memcmp(magic, kMagic, 8) != 0 || version != 1 || n == 0) {
+    set_error("%s is not an fmidx index file", path);
+    return -1;
+  }
+  std::vector<uint32_t> bwt(n), text;
+  std::vector<uint64_t> sa;
+  f.read(reinterpret_cast<char*>(bwt.data()), n * 4);
+  if (flags & 1) {
+    sa.resize(n);
+    f.read(reinterpret_cast<char*>(sa.data()), n * 8);
+  }
+  if (flags & 2) {
+    text.resize(n);
+    f.read(reinterpret_cast<char*>(text.data()), n * 4);
+  }
+  if (!f) {
+    set_error("truncated index file %s", path);
+    return -1;
+  }
+  fm_index* h = nullptr;
+  if (fm_create(&h, device)) return -1;
+  {
+    DeviceGuard g(device);
+    auto& x = h->idx;
+    auto fail = [&]() {
+      fm_destroy(h);
+      return -1;
+    };
+    if (hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4) != hipSuccess) return fail();
+    if (hipMemcpy(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
+    if (flags & 1) {
+      if (hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8) != hipSuccess) return fail();
+      if (hipMemcpy(x.sa, sa.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess) return fail();
+    }
+    if (flags & 2) {
+      if (hipMalloc(reinterpret_cast<void**>(&x.text), n * 4) != hipSuccess) return fail();
+      if (hipMemcpy(x.text, text.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
+    }
+    if (fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream)) return fail();
+  }
+  *out = h;
+  return 0;
+}
+
+// ---- batched device entry points ------------------------------------------
+
+int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, const uint64_t* d_lo,
+                     const uint64_t* d_hi, uint64_t* d_lo_out, uint64_t* d_hi_out, uint64_t m,
+                     void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, INT64_MIN, d_lo, d_hi, d_lo_out,
+                               d_hi_out, m, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_backward_search_batch(fm_index* h, const int64_t* d_tokens, const int64_t* d_offsets,
+                             uint64_t m, int64_t shift, const uint64_t* d_lo_in,
+                             const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
+                             void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_search(h->idx.view, d_tokens, d_offsets, m, shift, d_lo_in, d_hi_in,
+                              d_lo_out, d_hi_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_allowed_mask_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
+                          uint8_t* d_mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
+                          void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_mask(h->idx.view, d_lo, d_hi, m, d_mask, ld, vocab, shift, packed,
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                         uint64_t* d_lo, uint64_t* d_hi, uint64_t m, uint8_t* d_mask, uint64_t ld,
+                         uint64_t vocab, int packed, void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo, d_hi, m, s))
+    return -1;
+  return fmidx::launch_mask(h->idx.view, d_lo, d_hi, m, d_mask, ld, vocab, shift, packed, s);
+}
+
+int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
+                            const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
+                            uint64_t* d_counts, uint64_t* d_k, void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (grow_ws(h, fmidx::distinct_ws_bytes(total_cap))) return -1;
+  return fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k,
+                                h->idx.ws, total_cap, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
+             uint64_t* bitmap_bytes, uint64_t* bitmap_block) {
+  FM_CHECK_BUILT(h);
+  const auto& x = h->idx;
+  if (levels) *levels = x.L;
+  if (wm_bytes) *wm_bytes = x.wm_bytes;
+  if (bwt_bytes) *bwt_bytes = x.n * 4;
+  if (bitmap_bytes) *bitmap_bytes = x.bm_bytes;
+  if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;
+  return 0;
+}
+
+int fm_device_bwt(const fm_index* h, const uint32_t** out) {
+  FM_CHECK_BUILT(h);
+  *out = h->idx.bwt;
+  return 0;
+}
+
+int fm_synchronize(fm_index* h) {
+  FM_CHECK_HANDLE(h);
+  FM_GUARD(h);
+  FM_HIP(hipDeviceSynchronize());
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,410 @@
+// build.hip -- device-side construction of the HBM index from a BWT.
+//
+// Replaces the structure-building half of sdsl ``construct`` for
+// ``csa_wt_int<>`` (reference cpp_modules_linux/fm_index.cpp:37,44): given the
+// BWT (uint32 symbols, one sentinel 0), build
+//   * the wavelet matrix (L levels of 64-B rank blocks) by L rounds of
+//     ballot-pack + block scan + stable partition,
+//   * C / D tables from the final wavelet order (no histogram atomics),
+//   * the range-presence bitmap hierarchy.
+// Every pass is a coalesced stream over n symbols.
+#include "fmidx_internal.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+namespace fmidx {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Exclusive scan of a per-thread uint64 over a 256-thread block.
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* total, uint64_t* lds /*[kWaves]*/) {
+  const uint32_t lane = lane_id();
+  const uint32_t wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) lds[wave] = x;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    const uint64_t t = lds[w];
+    if ((uint32_t)w < wave) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+__global__ void __launch_bounds__(kThreads) k_chunk_sums(const uint64_t* __restrict__ in, uint64_t n,
+                                                        uint64_t* __restrict__ sums) {
+  __shared__ uint64_t lds[kWaves];
+  const uint64_t base = (uint64_t)blockIdx.x * (kThreads * 4) + threadIdx.x * 4;
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + k < n) s += in[base + k];
+  uint64_t tot;
+  block_exclusive_scan(s, &tot, lds);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kThreads) k_chunk_scan(const uint64_t* __restrict__ in, uint64_t n,
+                                                        const uint64_t* __restrict__ offs,
+                                                        uint64_t* __restrict__ out,
+                                                        uint64_t* __restrict__ total) {
+  __shared__ uint64_t lds[kWaves];
+  const uint64_t base = (uint64_t)blockIdx.x * (kThreads * 4) + threadIdx.x * 4;
+  uint64_t v[4];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = (base + k < n) ? in[base + k] : 0;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t ex = block_exclusive_scan(s, &tot, lds) + (offs ? offs[blockIdx.x] : 0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (base + k < n) out[base + k] = ex;
+    ex += v[k];
+  }
+  if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == kThreads - 1) *total = ex;
+}
+
+// ---- wavelet matrix ------------------------------------------------------
+// One wave per 448-symbol block: 7 ballots -> 7 payload words (lanes 1..7 store).
+__global__ void __launch_bounds__(kThreads) k_pack(const uint32_t* __restrict__ cur, uint64_t n,
+                                                  uint32_t bitpos, uint64_t* __restrict__ lvl,
+                                                  uint64_t* __restrict__ blkcnt, uint64_t nblk) {
+  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (b >= nblk) return;
+  const uint32_t lane = lane_id();
+  const uint64_t base = b * kBlockBits;
+  uint64_t mine = 0, ones = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const uint64_t i = base + (uint64_t)k * 64 + lane;
+    const int bit = (i < n) ? (int)((cur[i] >> bitpos) & 1u) : 0;
+    const uint64_t word = __ballot(bit);
+    ones += (uint64_t)__popcll(word);
+    if (lane == (uint32_t)(k + 1)) mine = word;
+  }
+  if (lane >= 1 && lane <= 7) lvl[b * kBlockWords + lane] = mine;
+  if (lane == 0) blkcnt[b] = ones;
+}
+
+// Stable partition of the level (zeros first) and the block's absolute count.
+__global__ void __launch_bounds__(kThreads) k_partition(const uint32_t* __restrict__ cur,
+                                                       uint32_t* __restrict__ nxt, uint64_t n,
+                                                       uint32_t bitpos, uint64_t* __restrict__ lvl,
+                                                       const uint64_t* __restrict__ cum,
+                                                       uint64_t zeros, uint64_t nblk) {
+  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (b >= nblk) return;
+  const uint32_t lane = lane_id();
+  const uint64_t base = b * kBlockBits;
+  uint64_t ones = cum[b];
+  if (lane == 0) lvl[b * kBlockWords] = ones;
+  const uint64_t below_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const uint64_t i = base + (uint64_t)k * 64 + lane;
+    const bool valid = i < n;
+    const uint32_t v = valid ? cur[i] : 0u;
+    const int bit = valid ? (int)((v >> bitpos) & 1u) : 0;
+    const uint64_t word = __ballot(bit);
+    const uint64_t mine = ones + (uint64_t)__popcll(word & below_mask);
+    if (valid) {
+      const uint64_t dest = bit ? zeros + mine : i - mine;
+      nxt[dest] = v;
+    }
+    ones += (uint64_t)__popcll(word);
+  }
+}
+
+__global__ void k_max_sym(const uint32_t* __restrict__ a, uint64_t n, uint32_t* __restrict__ out) {
+  uint32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, a[i]);
+  for (int d = 32; d > 0; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+  if (lane_id() == 0) atomicMax(out, m);
+}
+
+__global__ void k_count_zero(const uint32_t* __restrict__ a, uint64_t n, unsigned long long* out) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    c += (a[i] == 0u);
+  if (c) atomicAdd(out, c);
+}
+
+// Symbol runs of the final wavelet order: S[c] = first row, E[c] = one past.
+__global__ void k_bounds(const uint32_t* __restrict__ fin, uint64_t n, uint64_t* __restrict__ S,
+                         uint64_t* __restrict__ E) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = fin[i];
+  if (i == 0 || fin[i - 1] != c) S[c] = i;
+  if (i + 1 == n || fin[i + 1] != c) E[c] = i + 1;
+}
+
+__global__ void k_counts(const uint64_t* __restrict__ S, const uint64_t* __restrict__ E, uint64_t K,
+                         uint64_t* __restrict__ cnt, unsigned long long* __restrict__ sigma) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K) return;
+  const uint64_t k = E[c] - S[c];
+  cnt[c] = k;
+  if (k) atomicAdd(sigma, 1ull);
+}
+
+__global__ void k_dtable(const uint64_t* __restrict__ C, const uint64_t* __restrict__ S, uint64_t K,
+                         int64_t* __restrict__ D) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K) return;
+  D[c] = (int64_t)C[c] - (int64_t)S[c];
+}
+
+// ---- range bitmaps -------------------------------------------------------
+// Base level: one workgroup per aligned run of B0 rows; LDS bitmap, then store.
+__global__ void __launch_bounds__(kThreads) k_bm_base(const uint32_t* __restrict__ bwt,
+                                                     uint32_t log2b0, uint32_t words,
+                                                     uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t bits[];
+  for (uint32_t w = threadIdx.x; w < words; w += kThreads) bits[w] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x << log2b0;
+  const uint32_t cnt = 1u << log2b0;
+  const uint4* src = reinterpret_cast<const uint4*>(bwt + base);
+  for (uint32_t j = threadIdx.x; j < cnt / 4; j += kThreads) {
+    const uint4 q = src[j];
+    atomicOr(&bits[q.x >> 5], 1u << (q.x & 31));
+    atomicOr(&bits[q.y >> 5], 1u << (q.y & 31));
+    atomicOr(&bits[q.z >> 5], 1u << (q.z & 31));
+    atomicOr(&bits[q.w >> 5], 1u << (q.w & 31));
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(out + (uint64_t)blockIdx.x * words);
+  const uint4* s4 = reinterpret_cast<const uint4*>(bits);
+  for (uint32_t w = threadIdx.x; w < words / 4; w += kThreads) dst[w] = s4[w];
+}
+
+__global__ void __launch_bounds__(kThreads) k_bm_up(const uint32_t* __restrict__ child,
+                                                   uint32_t words, uint32_t* __restrict__ out) {
+  const uint64_t p = blockIdx.x;
+  const uint4* c = reinterpret_cast<const uint4*>(child + p * 4 * words);
+  uint4* o = reinterpret_cast<uint4*>(out + p * words);
+  const uint32_t w4 = words / 4;
+  for (uint32_t w = threadIdx.x; w < w4; w += kThreads) {
+    uint4 a = c[w], b = c[w4 + w], d = c[2 * w4 + w], e = c[3 * w4 + w];
+    a.x |= b.x | d.x | e.x;
+    a.y |= b.y | d.y | e.y;
+    a.z |= b.z | d.z | e.z;
+    a.w |= b.w | d.w | e.w;
+    o[w] = a;
+  }
+}
+
+template <typename T>
+int dmalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  return 0;
+}
+
+}  // namespace
+
+int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s,
+                       uint64_t* d_total) {
+  if (n == 0) {
+    if (d_total) FM_HIP(hipMemsetAsync(d_total, 0, sizeof(uint64_t), s));
+    return 0;
+  }
+  const uint64_t per = kThreads * 4;
+  const uint64_t chunks = (n + per - 1) / per;
+  uint64_t* offs = nullptr;
+  if (chunks > 1) {
+    uint64_t* sums = nullptr;
+    if (dmalloc(&sums, chunks) || dmalloc(&offs, chunks)) return -1;
+    k_chunk_sums<<<(unsigned)chunks, kThreads, 0, s>>>(d_in, n, sums);
+    if (exclusive_scan_u64(sums, offs, chunks, s, nullptr)) return -1;
+    FM_HIP(hipStreamSynchronize(s));
+    FM_HIP(hipFree(sums));
+  }
+  k_chunk_scan<<<(unsigned)chunks, kThreads, 0, s>>>(d_in, n, offs, d_out, d_total);
+  FM_HIP(hipGetLastError());
+  if (offs) {
+    FM_HIP(hipStreamSynchronize(s));
+    FM_HIP(hipFree(offs));
+  }
+  return 0;
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return (uint32_t)std::strtoul(v, nullptr, 10);
+}
+
+// h->bwt must already hold the BWT (device, owned by h).
+int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
+  if (n == 0) {
+    set_error("empty BWT");
+    return -1;
+  }
+  const unsigned grid_stream = 2048;
+  // -- alphabet
+  uint32_t* d_max = nullptr;
+  unsigned long long* d_z = nullptr;
+  if (dmalloc(&d_max, 1) || dmalloc(&d_z, 1)) return -1;
+  FM_HIP(hipMemsetAsync(d_max, 0, 4, s));
+  FM_HIP(hipMemsetAsync(d_z, 0, 8, s));
+  k_max_sym<<<grid_stream, kThreads, 0, s>>>(d_bwt, n, d_max);
+  k_count_zero<<<grid_stream, kThreads, 0, s>>>(d_bwt, n, d_z);
+  uint32_t max_sym = 0;
+  unsigned long long nzero = 0;
+  FM_HIP(hipMemcpyAsync(&max_sym, d_max, 4, hipMemcpyDeviceToHost, s));
+  FM_HIP(hipMemcpyAsync(&nzero, d_z, 8, hipMemcpyDeviceToHost, s));
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(d_max));
+  FM_HIP(hipFree(d_z));
+  if (nzero != 1) {
+    set_error("BWT must contain exactly one sentinel 0 (found %llu)", nzero);
+    return -1;
+  }
+  uint32_t L = 1;
+  while (L < 32 && (max_sym >> L) != 0) ++L;
+  if (L > (uint32_t)kMaxLevels) {
+    set_error("symbol %u too large (max %d bits)", max_sym, kMaxLevels);
+    return -1;
+  }
+  const uint64_t K = 1ull << L;
+  const uint64_t nblk = n / kBlockBits + 1;
+
+  // -- wavelet matrix
+  uint64_t* wm = nullptr;
+  uint32_t *cur = nullptr, *nxt = nullptr;
+  uint64_t *blkcnt = nullptr, *cum = nullptr, *d_tot = nullptr;
+  if (dmalloc(&wm, (size_t)L * nblk * kBlockWords) || dmalloc(&cur, n) || dmalloc(&nxt, n) ||
+      dmalloc(&blkcnt, nblk) || dmalloc(&cum, nblk) || dmalloc(&d_tot, 1))
+    return -1;
+  FM_HIP(hipMemcpyAsync(cur, d_bwt, n * 4, hipMemcpyDeviceToDevice, s));
+  const unsigned gblk = (unsigned)((nblk + kWaves - 1) / kWaves);
+  uint64_t zeros[kMaxLevels] = {0};
+  for (uint32_t lev = 0; lev < L; ++lev) {
+    const uint32_t bitpos = L - 1 - lev;
+    uint64_t* lvl = wm + (uint64_t)lev * nblk * kBlockWords;
+    k_pack<<<gblk, kThreads, 0, s>>>(cur, n, bitpos, lvl, blkcnt, nblk);
+    FM_HIP(hipGetLastError());
+    if (exclusive_scan_u64(blkcnt, cum, nblk, s, d_tot)) return -1;
+    uint64_t ones = 0;
+    FM_HIP(hipMemcpyAsync(&ones, d_tot, 8, hipMemcpyDeviceToHost, s));
+    FM_HIP(hipStreamSynchronize(s));
+    zeros[lev] = n - ones;
+    k_partition<<<gblk, kThreads, 0, s>>>(cur, nxt, n, bitpos, lvl, cum, zeros[lev], nblk);
+    FM_HIP(hipGetLastError());
+    std::swap(cur, nxt);
+  }
+  // -- C / D from the final order
+  uint64_t *S = nullptr, *E = nullptr, *cnt = nullptr, *C = nullptr;
+  int64_t* D = nullptr;
+  unsigned long long* d_sigma = nullptr;
+  if (dmalloc(&S, K) || dmalloc(&E, K) || dmalloc(&cnt, K + 1) || dmalloc(&C, K + 1) ||
+      dmalloc(&D, K) || dmalloc(&d_sigma, 1))
+    return -1;
+  FM_HIP(hipMemsetAsync(S, 0, K * 8, s));
+  FM_HIP(hipMemsetAsync(E, 0, K * 8, s));
+  FM_HIP(hipMemsetAsync(cnt, 0, (K + 1) * 8, s));
+  FM_HIP(hipMemsetAsync(d_sigma, 0, 8, s));
+  k_bounds<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(cur, n, S, E);
+  k_counts<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(S, E, K, cnt, d_sigma);
+  if (exclusive_scan_u64(cnt, C, K + 1, s, nullptr)) return -1;
+  k_dtable<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(C, S, K, D);
+  FM_HIP(hipGetLastError());
+  unsigned long long sigma = 0;
+  FM_HIP(hipMemcpyAsync(&sigma, d_sigma, 8, hipMemcpyDeviceToHost, s));
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(S));
+  FM_HIP(hipFree(E));
+  FM_HIP(hipFree(cnt));
+  FM_HIP(hipFree(d_sigma));
+  FM_HIP(hipFree(cur));
+  FM_HIP(hipFree(nxt));
+  FM_HIP(hipFree(blkcnt));
+  FM_HIP(hipFree(cum));
+  FM_HIP(hipFree(d_tot));
+
+  // -- range bitmaps
+  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", 13);
+  const uint32_t words = (uint32_t)(((uint64_t)max_sym + 1 + 127) / 128 * 4);
+  const uint64_t nb0 = n >> log2b0;
+  uint32_t bm_levels = 0;
+  uint64_t bm_off[kMaxBmLevels] = {0}, bm_count[kMaxBmLevels] = {0};
+  uint64_t total_words = 0;
+  // bitmaps only pay off for vocabulary-sized alphabets (LDS holds one bitmap)
+  const bool bm_ok = (uint64_t)words * 4 <= 64 * 1024;
+  for (uint64_t c = bm_ok ? nb0 : 0; c > 0 && bm_levels < (uint32_t)kMaxBmLevels; c >>= 2) {
+    bm_off[bm_levels] = total_words;
+    bm_count[bm_levels] = c;
+    total_words += c * words;
+    ++bm_levels;
+  }
+  uint32_t* bm = nullptr;
+  if (dmalloc(&bm, total_words)) return -1;
+  if (bm_levels > 0) {
+    k_bm_base<<<(unsigned)nb0, kThreads, words * 4, s>>>(d_bwt, log2b0, words, bm + bm_off[0]);
+    FM_HIP(hipGetLastError());
+    for (uint32_t j = 1; j < bm_levels; ++j) {
+      k_bm_up<<<(unsigned)bm_count[j], kThreads, 0, s>>>(bm + bm_off[j - 1], words, bm + bm_off[j]);
+      FM_HIP(hipGetLastError());
+    }
+  }
+  FM_HIP(hipStreamSynchronize(s));
+
+  h->n = n;
+  h->L = L;
+  h->max_sym = max_sym;
+  h->sigma = sigma;
+  h->wm = wm;
+  h->C = C;
+  h->D = D;
+  h->bm = bm;
+  h->wm_bytes = (uint64_t)L * nblk * 64;
+  h->bm_bytes = total_words * 4;
+  DevView& v = h->view;
+  v = DevView{};
+  v.n = n;
+  v.nblk = nblk;
+  v.wm = wm;
+  v.D = D;
+  v.C = C;
+  v.bwt = d_bwt;
+  v.bm = bm;
+  for (uint32_t j = 0; j < bm_levels; ++j) {
+    v.bm_off[j] = bm_off[j];
+    v.bm_count[j] = bm_count[j];
+  }
+  for (uint32_t lev = 0; lev < L; ++lev) v.zeros[lev] = zeros[lev];
+  v.L = L;
+  v.max_sym = max_sym;
+  v.bm_words = words;
+  v.bm_levels = bm_levels;
+  v.bm_log2 = log2b0;
+  h->built = true;
+  return 0;
+}
+
+}  // namespace fmidx

@@ -1,0 +1,336 @@
+"""``FMIndex`` -- the SWIG surface of ``cpp_modules.fm_index`` on the MI355X engine.
+
+Reference: ``cpp_modules_linux/fm_index.hpp:20-45`` / ``fm_index.cpp:27-209``
+(SWIG module ``fm_index.i``).  Same method names, argument meaning, return
+shapes (tuples, as SWIG returns for ``std::vector``) and error behaviour
+(``OverflowError`` for negative / oversize unsigned arguments, ``TypeError``
+for non-integers).  Every query runs on the GPU holding the index; the
+batched ``*_batch`` / ``allowed_mask`` / ``decode_step`` methods take torch
+tensors resident on that GPU and are stream-ordered on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import byref, c_uint64, c_void_p
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ._lib import FMIndexError, check, lib
+
+U64_MAX = (1 << 64) - 1
+
+
+def _u64(v, method: str, argno: int, typ: str = "size_type") -> int:
+    if isinstance(v, (bool,)) or not isinstance(v, (int, np.integer)):
+        raise TypeError(f"in method 'FMIndex_{method}', argument {argno} of type '{typ}'")
+    v = int(v)
+    if v < 0 or v > U64_MAX:
+        raise OverflowError(f"in method 'FMIndex_{method}', argument {argno} of type '{typ}'")
+    return v
+
+
+def _u64_vec(values, method: str, argno: int) -> np.ndarray:
+    if isinstance(values, np.ndarray):
+        arr = values
+    else:
+        values = list(values)
+        for v in values:
+            if isinstance(v, bool) or not isinstance(v, (int, np.integer)):
+                raise TypeError(f"in method 'FMIndex_{method}', argument {argno} of type "
+                                "'std::vector< unsigned long,std::allocator< unsigned long > >'")
+        arr = np.asarray(values, dtype=object) if values else np.zeros(0, dtype=np.int64)
+    if arr.size:
+        mn = int(arr.min())
+        mx = int(arr.max())
+        if mn < 0 or mx > U64_MAX:
+            raise OverflowError(f"in method 'FMIndex_{method}', argument {argno} of type "
+                                "'std::vector< unsigned long,std::allocator< unsigned long > >'")
+    return np.ascontiguousarray(arr.astype(np.uint64))
+
+
+def _ptr(a: np.ndarray, ctype=c_uint64):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def _default_device() -> int:
+    env = os.environ.get("FMIDX_DEVICE")
+    if env is not None:
+        return int(env)
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_device())
+    except Exception:  # pragma: no cover - torch is optional for the SWIG surface
+        pass
+    return 0
+
+
+def _stream_of(t) -> int:
+    import torch
+
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+class FMIndex:
+    """Drop-in for the SWIG proxy class ``cpp_modules.fm_index.FMIndex``."""
+
+    def __init__(self, device: Optional[int] = None):
+        self._h = c_void_p()
+        self._device = _default_device() if device is None else int(device)
+        check(lib().fm_create(byref(self._h), self._device), "FMIndex()")
+
+    # -- lifecycle ----------------------------------------------------------
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().fm_destroy(h)
+            except Exception:
+                pass
+            self._h = c_void_p()
+
+    @property
+    def device(self) -> int:
+        return self._device
+
+    # -- construction (fm_index.cpp:33-48) ----------------------------------
+    def initialize(self, data) -> None:
+        arr = _u64_vec(data, "initialize", 2)
+        check(lib().fm_initialize(self._h, _ptr(arr), arr.size), "initialize")
+
+    def initialize_from_file(self, file: str, width: int) -> None:
+        if not isinstance(file, str):
+            raise TypeError("in method 'FMIndex_initialize_from_file', argument 2 of type 'std::string const'")
+        check(lib().fm_initialize_from_file(self._h, file.encode(), int(width)), "initialize_from_file")
+
+    def initialize_from_bwt_device(self, bwt, sa=None, text=None) -> None:
+        """Device build from a uint32/int32 BWT tensor already in HBM."""
+        import torch
+
+        assert bwt.is_cuda and bwt.dtype in (torch.int32,) and bwt.is_contiguous()
+        stream = _stream_of(bwt)
+        check(lib().fm_initialize_from_bwt_device(
+            self._h, c_void_p(bwt.data_ptr()), bwt.numel(),
+            c_void_p(sa.data_ptr()) if sa is not None else None,
+            c_void_p(text.data_ptr()) if text is not None else None,
+            c_void_p(stream)), "initialize_from_bwt_device")
+
+    # -- SWIG surface --------------------------------------------------------
+    def size(self) -> int:
+        out = c_uint64()
+        check(lib().fm_size(self._h, byref(out)), "size")
+        return int(out.value)
+
+    def sigma(self) -> int:
+        out = c_uint64()
+        check(lib().fm_sigma(self._h, byref(out)), "sigma")
+        return int(out.value)
+
+    def backward_search_step(self, symbol, low, high) -> Tuple[int, int]:
+        """fm_index.cpp:67-97."""
+        s = _u64(symbol, "backward_search_step", 2, "char_type")
+        lo = _u64(low, "backward_search_step", 3)
+        hi = _u64(high, "backward_search_step", 4)
+        out = (c_uint64 * 2)()
+        check(lib().fm_backward_search_step(self._h, s, lo, hi, out), "backward_search_step")
+        return (int(out[0]), int(out[1]))
+
+    def backward_search_multi(self, query) -> Tuple[int, int]:
+        """fm_index.cpp:55-65."""
+        q = _u64_vec(query, "backward_search_multi", 2)
+        out = (c_uint64 * 2)()
+        check(lib().fm_backward_search_multi(self._h, _ptr(q), q.size, out), "backward_search_multi")
+        return (int(out[0]), int(out[1]))
+
+    def _width(self, low: int, high: int) -> int:
+        n = self.size()
+        if low == high:
+            return 0
+        high = min(high, n)
+        return max(0, high - low)
+
+    def distinct(self, low, high) -> Tuple[int, ...]:
+        """fm_index.cpp:99-117."""
+        lo = _u64(low, "distinct", 2)
+        hi = _u64(high, "distinct", 3)
+        cap = max(1, min(self._width(lo, hi), self.sigma()))
+        buf = np.zeros(cap, dtype=np.uint64)
+        k = c_uint64()
+        check(lib().fm_distinct(self._h, lo, hi, _ptr(buf), cap, byref(k)), "distinct")
+        return tuple(int(x) for x in buf[: k.value])
+
+    def distinct_count(self, low, high) -> Tuple[int, ...]:
+        """fm_index.cpp:119-144: interleaved (symbol, count), ascending."""
+        lo = _u64(low, "distinct_count", 2)
+        hi = _u64(high, "distinct_count", 3)
+        cap = 2 * max(1, min(self._width(lo, hi), self.sigma()))
+        buf = np.zeros(cap, dtype=np.uint64)
+        k = c_uint64()
+        check(lib().fm_distinct_count(self._h, lo, hi, _ptr(buf), cap, byref(k)), "distinct_count")
+        return tuple(int(x) for x in buf[: 2 * k.value])
+
+    def _distinct_count_multi_arrays(self, lows: np.ndarray, highs: np.ndarray):
+        m = lows.size
+        n = self.size()
+        sigma = self.sigma()
+        hc = np.minimum(highs, np.uint64(n))
+        width = np.where((lows == highs) | (lows >= hc), 0, hc - lows)
+        cap = int(2 * np.minimum(width, np.uint64(sigma)).astype(np.uint64).sum())
+        out = np.zeros(max(1, cap), dtype=np.uint64)
+        offs = np.zeros(m + 1, dtype=np.uint64)
+        check(lib().fm_distinct_count_multi(self._h, _ptr(lows), _ptr(highs), m, _ptr(out),
+                                            max(1, cap), _ptr(offs)), "distinct_count_multi")
+        return out, offs
+
+    def distinct_count_multi(self, lows, highs):
+        """fm_index.cpp:146-166: one batched GPU launch for all ranges."""
+        lo = _u64_vec(lows, "distinct_count_multi", 2)
+        hi = _u64_vec(highs, "distinct_count_multi", 3)
+        if lo.size != hi.size:
+            raise ValueError("lows and highs differ in length")
+        out, offs = self._distinct_count_multi_arrays(lo, hi)
+        flat = out.tolist()
+        o = offs.tolist()
+        return tuple(tuple(flat[2 * o[i]: 2 * o[i + 1]]) for i in range(lo.size))
+
+    def locate(self, row) -> int:
+        """fm_index.cpp:168-172."""
+        r = _u64(row, "locate", 2)
+        out = c_uint64()
+        check(lib().fm_locate(self._h, r, byref(out)), "locate")
+        return int(out.value)
+
+    def extract_text(self, begin, end) -> Tuple[int, ...]:
+        """fm_index.cpp:174-194."""
+        b = _u64(begin, "extract_text", 2)
+        e = _u64(end, "extract_text", 3)
+        if e <= b:
+            return tuple()
+        n = self.size()
+        cap = max(1, min(e, n) - b) if min(e, n) > b else 1
+        buf = np.zeros(cap, dtype=np.uint64)
+        ln = c_uint64()
+        check(lib().fm_extract_text(self._h, b, e, _ptr(buf), cap, byref(ln)), "extract_text")
+        return tuple(int(x) for x in buf[: ln.value])
+
+    def save(self, path: str) -> None:
+        check(lib().fm_save(self._h, str(path).encode()), "save")
+
+    # -- engine extensions ---------------------------------------------------
+    def stats(self) -> dict:
+        vals = [c_uint64() for _ in range(5)]
+        check(lib().fm_stats(self._h, *[byref(v) for v in vals]), "stats")
+        keys = ["levels", "wm_bytes", "bwt_bytes", "bitmap_bytes", "bitmap_block"]
+        return {k: int(v.value) for k, v in zip(keys, vals)}
+
+    def get_range_batch(self, patterns: Sequence[Sequence[int]], shift: int = 0,
+                        starts: Optional[Tuple[Sequence[int], Sequence[int]]] = None):
+        """get_range (index.py:103-114) for many patterns in one GPU launch.
+        Returns (lows, highs) as uint64 numpy arrays."""
+        m = len(patterns)
+        lens = np.fromiter((len(p) for p in patterns), dtype=np.int64, count=m)
+        offs = np.zeros(m + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        toks = np.fromiter((int(t) for p in patterns for t in p), dtype=np.int64, count=int(offs[-1]))
+        lo_out = np.zeros(max(1, m), dtype=np.uint64)
+        hi_out = np.zeros(max(1, m), dtype=np.uint64)
+        if m == 0:
+            return lo_out[:0], hi_out[:0]
+        li = hi_in = None
+        if starts is not None:
+            li = np.ascontiguousarray(np.asarray(starts[0], dtype=np.uint64))
+            hi_in = np.ascontiguousarray(np.asarray(starts[1], dtype=np.uint64))
+        check(lib().fm_get_range_batch(
+            self._h, _ptr(toks, ctypes.c_int64), _ptr(offs, ctypes.c_int64), m, int(shift),
+            _ptr(li) if li is not None else None, _ptr(hi_in) if hi_in is not None else None,
+            _ptr(lo_out), _ptr(hi_out)), "get_range_batch")
+        return lo_out, hi_out
+
+    # torch-tensor batched hot path (device pointers, current stream)
+    def lf_step_batch(self, tokens, lo, hi, shift: int, lo_out=None, hi_out=None):
+        lo_out = lo if lo_out is None else lo_out
+        hi_out = hi if hi_out is None else hi_out
+        check(lib().fm_lf_step_batch(self._h, c_void_p(tokens.data_ptr()), int(shift),
+                                     c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
+                                     c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()),
+                                     lo.numel(), c_void_p(_stream_of(lo))), "lf_step_batch")
+        return lo_out, hi_out
+
+    def backward_search_batch(self, tokens, offsets, shift: int, lo_out, hi_out, lo_in=None, hi_in=None):
+        check(lib().fm_backward_search_batch(
+            self._h, c_void_p(tokens.data_ptr()), c_void_p(offsets.data_ptr()), lo_out.numel(), int(shift),
+            c_void_p(lo_in.data_ptr()) if lo_in is not None else None,
+            c_void_p(hi_in.data_ptr()) if hi_in is not None else None,
+            c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()),
+            c_void_p(_stream_of(lo_out))), "backward_search_batch")
+        return lo_out, hi_out
+
+    def allowed_mask(self, lo, hi, vocab: int, shift: int, out=None, packed: bool = False):
+        """bool/uint8 [m, vocab] (or int32 [m, ceil(vocab/32)] when packed)."""
+        import torch
+
+        m = lo.numel()
+        if out is None:
+            if packed:
+                out = torch.empty((m, (vocab + 31) // 32), dtype=torch.int32, device=lo.device)
+            else:
+                out = torch.empty((m, vocab), dtype=torch.uint8, device=lo.device)
+        ld = out.stride(0) * out.element_size()
+        check(lib().fm_allowed_mask_batch(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), m,
+                                          c_void_p(out.data_ptr()), ld, int(vocab), int(shift),
+                                          1 if packed else 0, c_void_p(_stream_of(lo))), "allowed_mask")
+        return out
+
+    def decode_step(self, tokens, lo, hi, mask, vocab: int, shift: int, reset_below: int = -(1 << 63),
+                    packed: bool = False):
+        ld = mask.stride(0) * mask.element_size()
+        check(lib().fm_decode_step_batch(self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below),
+                                         c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), lo.numel(),
+                                         c_void_p(mask.data_ptr()), ld, int(vocab), 1 if packed else 0,
+                                         c_void_p(_stream_of(lo))), "decode_step")
+        return mask
+
+    def distinct_count_batch(self, lo, hi):
+        """Device interval_symbols for m ranges -> (syms, counts, k, cap_off)."""
+        import torch
+
+        n = self.size()
+        sigma = self.sigma()
+        hc = torch.clamp(hi, max=n)
+        width = torch.where((lo == hi) | (lo >= hc), torch.zeros_like(lo), hc - lo)
+        cap = torch.clamp(width, max=sigma)
+        cap_off = torch.zeros(lo.numel() + 1, dtype=torch.int64, device=lo.device)
+        torch.cumsum(cap, 0, out=cap_off[1:])
+        total = int(cap_off[-1].item())
+        syms = torch.empty(max(1, total), dtype=torch.int64, device=lo.device)
+        counts = torch.empty(max(1, total), dtype=torch.int64, device=lo.device)
+        k = torch.empty(lo.numel(), dtype=torch.int64, device=lo.device)
+        check(lib().fm_distinct_count_batch(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
+                                            lo.numel(), c_void_p(cap_off.data_ptr()), total,
+                                            c_void_p(syms.data_ptr()), c_void_p(counts.data_ptr()),
+                                            c_void_p(k.data_ptr()), c_void_p(_stream_of(lo))),
+              "distinct_count_batch")
+        return syms, counts, k, cap_off
+
+    def device_bwt_ptr(self) -> int:
+        p = c_void_p()
+        check(lib().fm_device_bwt(self._h, byref(p)), "device_bwt")
+        return int(p.value or 0)
+
+    def synchronize(self) -> None:
+        check(lib().fm_synchronize(self._h), "synchronize")
+
+
+def load_FMIndex(path: str, device: Optional[int] = None) -> FMIndex:
+    """fm_index.cpp:201-209 (own binary format)."""
+    obj = FMIndex.__new__(FMIndex)
+    obj._h = c_void_p()
+    obj._device = _default_device() if device is None else int(device)
+    check(lib().fm_load(byref(obj._h), str(path).encode(), obj._device), "load_FMIndex")
+    return obj
+
+
+__all__ = ["FMIndex", "load_FMIndex", "FMIndexError"]

@@ -1,0 +1,160 @@
+"""``FMIndex`` -- the ``index.py`` surface on the MI355X engine.
+
+Reference: ``index.py:20-207``.  Same attributes (``beginnings``,
+``occurring``, ``occurring_distinct``, ``occurring_counts``, ``labels``),
+methods and return shapes, same corpus encoding (each doc reversed, ids +
+``SHIFT``, concatenated without separators) so ranges, counts and distinct
+sets are identical to the reference's.  Differences are performance-only:
+``get_range`` runs the whole pattern in one GPU launch (the reference makes
+one SWIG call per token, ``index.py:109-112``) and
+``get_distinct_count_multi`` is one launch for all rows (``fm_index.cpp:146``
+spawns a thread per row).  ``.oth`` metadata is written as JSON, not pickle.
+"""
+from __future__ import annotations
+
+import bisect
+import json
+from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .fm_index import FMIndex as _FMIndex
+from .fm_index import load_FMIndex
+
+SHIFT = 10                      # index.py:16
+
+
+def encode_corpus(sequences: Iterable[Sequence[int]]):
+    """index.py:47-56 -> (T' as uint64 array, beginnings, occurring set)."""
+    beginnings = [0]
+    occurring = set()
+    parts = []
+    for seq in sequences:
+        a = np.asarray(list(seq) if not isinstance(seq, np.ndarray) else seq, dtype=np.int64)
+        beginnings.append(beginnings[-1] + int(a.size))
+        occurring |= set(a.tolist())
+        parts.append(a[::-1] + SHIFT)
+    data = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+    if data.size and int(data.min()) < 0:
+        raise OverflowError("token id below -SHIFT cannot be encoded")
+    return data.astype(np.uint64), beginnings, occurring
+
+
+class FMIndex(_FMIndex):
+    """Drop-in for ``index.FMIndex`` (index.py:20)."""
+
+    beginnings: List[int]
+    occurring: List[int]
+    occurring_distinct: List[int]
+    occurring_counts: List[int]
+    labels: Optional[List[str]]
+
+    def __init__(self, device: Optional[int] = None):
+        super().__init__(device)
+        self.beginnings = [0]
+        self.occurring = set()
+        self.occurring_distinct = []
+        self.occurring_counts = []
+        self.labels = None
+
+    def initialize(self, sequences: Iterable[List[int]], in_memory: bool = False) -> None:  # type: ignore[override]
+        """index.py:39-67.  ``in_memory`` is accepted for API parity; both
+        paths encode in memory (the reference's temp-file path feeds the same
+        symbols through ``initialize_from_file(tmp, 4)``)."""
+        data, beginnings, occurring = encode_corpus(sequences)
+        self.beginnings = beginnings
+        self.occurring = list(occurring)
+        super().initialize(data)
+        self.occurring_distinct, self.occurring_counts = self.get_distinct_count(0, len(self))
+
+    # -- docs --------------------------------------------------------------
+    def get_doc(self, doc_index: int) -> List[int]:
+        doc = self.extract_text(self.beginnings[doc_index], self.beginnings[doc_index + 1])
+        return [x - SHIFT for x in doc]
+
+    def get_doc_index(self, token_index: int) -> int:
+        return bisect.bisect_right(self.beginnings, token_index) - 1
+
+    def get_doc_length(self, doc_index: int) -> int:
+        return self.beginnings[doc_index + 1] - self.beginnings[doc_index]
+
+    def get_token_index_from_row(self, row: int) -> int:
+        return self.locate(row)
+
+    def get_doc_index_from_row(self, row: int) -> int:
+        return self.get_doc_index(self.locate(row))
+
+    # -- search ------------------------------------------------------------
+    def get_range(self, sequence: List[int]) -> Tuple[int, int]:
+        """index.py:103-114 in one launch; (0, size()) for an empty pattern."""
+        seq = list(sequence)
+        if seq and min(seq) + SHIFT < 0:
+            raise OverflowError("in method 'FMIndex_backward_search_step', argument 2 of type 'char_type'")
+        lo, hi = self.get_range_batch([seq], SHIFT)
+        return int(lo[0]), int(hi[0])
+
+    def get_ranges(self, sequences: Sequence[Sequence[int]]) -> List[Tuple[int, int]]:
+        """Batched ``get_range`` for many patterns (one launch)."""
+        lo, hi = self.get_range_batch(sequences, SHIFT)
+        return list(zip(lo.tolist(), hi.tolist()))
+
+    def get_count(self, sequence: List[int]) -> int:
+        start, end = self.get_range(sequence)
+        return end - start
+
+    def get_doc_indices(self, sequence: List[int]) -> Iterator[int]:
+        start, end = self.get_range(sequence)
+        for row in range(start, end):
+            yield self.get_doc_index_from_row(row)
+
+    def get_continuations(self, sequence: List[int]) -> List[int]:
+        start, end = self.get_range(sequence)
+        return self.get_distinct(start, end)
+
+    def get_distinct(self, low: int, high: int) -> List[int]:
+        return [c - SHIFT for c in self.distinct(low, high) if c > 0]
+
+    def get_distinct_count(self, low: int, high: int) -> Tuple[List[int], List[int]]:
+        data = self.distinct_count(low, high)
+        syms = data[0::2]
+        cnts = data[1::2]
+        keep = [i for i, d in enumerate(syms) if d > 0]          # drop the sentinel (index.py:156)
+        return [syms[i] - SHIFT for i in keep], [cnts[i] for i in keep]
+
+    def get_distinct_count_multi(self, lows: List[int], highs: List[int]) -> List[Tuple[List[int], List[int]]]:
+        ret = []
+        for data in self.distinct_count_multi(lows, highs):
+            syms = data[0::2]
+            cnts = data[1::2]
+            keep = [i for i, d in enumerate(syms) if d > 0]
+            ret.append(([syms[i] - SHIFT for i in keep], [cnts[i] for i in keep]))
+        return ret
+
+    def __len__(self) -> int:
+        return self.beginnings[-1]
+
+    @property
+    def n_docs(self) -> int:
+        return len(self.beginnings) - 1
+
+    # -- persistence ---------------------------------------------------------
+    def save(self, path: str) -> None:  # type: ignore[override]
+        with open(path + ".oth", "w") as f:
+            json.dump({"beginnings": self.beginnings, "occurring": sorted(int(x) for x in self.occurring),
+                       "labels": self.labels}, f)
+        return super().save(path + ".fmi")
+
+    @classmethod
+    def load(cls, path: str, device: Optional[int] = None) -> "FMIndex":
+        index = load_FMIndex(path + ".fmi", device)
+        index.__class__ = cls
+        with open(path + ".oth") as f:
+            meta = json.load(f)
+        index.beginnings = [int(x) for x in meta["beginnings"]]
+        index.occurring = [int(x) for x in meta["occurring"]]
+        index.labels = meta.get("labels")
+        index.occurring_distinct, index.occurring_counts = index.get_distinct_count(0, len(index))
+        return index
+
+
+__all__ = ["FMIndex", "SHIFT", "encode_corpus"]

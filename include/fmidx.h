@@ -1,0 +1,190 @@
+/*
+ * fmidx.h -- C-ABI of the MI355X-native FM-index engine (libfmidx.so).
+ *
+ * This is the drop-in boundary that replaces the SWIG module
+ * ``cpp_modules.fm_index`` (reference: cpp_modules_linux/fm_index.{hpp,cpp,i}).
+ * Every SWIG method of class ``FMIndex`` has an ``fm_*`` equivalent on an
+ * opaque handle; in addition the batched hot-path entry points take DEVICE
+ * pointers and a ``hipStream_t`` (passed as ``void*``) so a logits processor
+ * can build a (rows x vocab) allowed-token mask with no host round trip.
+ *
+ * Conventions
+ *  - Every function returns an int status: 0 = ok, < 0 = error; the message
+ *    of the last error on the calling thread is in fm_last_error().
+ *  - Symbols are the reference's ``char_type`` (unsigned long, fm_index.hpp:22):
+ *    token id + SHIFT (index.py:16); the batched entry points instead take
+ *    int64 token ids plus a ``shift`` so they can read ``input_ids`` directly.
+ *  - Ranges are half-open [low, high) unless a comment says "inclusive"
+ *    (fm_index.cpp:67 takes an inclusive high, and returns a half-open one).
+ *  - Host-pointer functions are synchronous.  Device-pointer functions are
+ *    stream-ordered on ``stream`` (NULL = the legacy default stream) and never
+ *    allocate or synchronise, so they can be captured into a hipGraph, except
+ *    where noted (workspace growth on first use).
+ *  - There is no CPU query path: every query executes on the GPU that holds
+ *    the index.  Construction (suffix sorting) runs on the host or, for the
+ *    device-build entry points, on the GPU.
+ */
+#ifndef FMIDX_H_
+#define FMIDX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fm_index fm_index;
+
+/* ---- lifecycle / errors ------------------------------------------------ */
+
+/* Last error message of the calling thread ("" if none). */
+const char* fm_last_error(void);
+
+/* Library / device info: writes a short string (arch, CU count). */
+int fm_device_info(int device, char* buf, size_t cap);
+
+/* FMIndex::FMIndex()  -- fm_index.cpp:27-29.  Binds the handle to ``device``. */
+int fm_create(fm_index** out, int device);
+
+/* FMIndex::~FMIndex() -- fm_index.cpp:31 (frees host and device memory). */
+void fm_destroy(fm_index* h);
+
+/* ---- construction ------------------------------------------------------ */
+
+/* FMIndex::initialize(const vector<char_type>&) -- fm_index.cpp:33-41.
+ * ``data`` is T' (already reversed / shifted by index.py:47-53) WITHOUT the
+ * sentinel; a 0 symbol is an error (sdsl construct rejects it).  Builds the
+ * suffix array on the host (SA-IS), then the BWT, wavelet matrix, C table,
+ * range bitmaps and SA/text arrays on the device. */
+int fm_initialize(fm_index* h, const uint64_t* data, uint64_t n);
+
+/* FMIndex::initialize_from_file(string, int width) -- fm_index.cpp:43-48:
+ * ``width``-byte little-endian unsigned integers (index.py:63 writes '<l'). */
+int fm_initialize_from_file(fm_index* h, const char* path, int width);
+
+/* Device build from a finished BWT already resident in HBM (no host copy):
+ * ``d_bwt`` holds n uint32 symbols with exactly one 0 (the sentinel row).
+ * Optional ``d_sa`` (n uint64, may be NULL) enables fm_locate and
+ * ``d_text`` (n uint32 = T' with sentinel, may be NULL) enables extract.
+ * The buffers are copied; the caller keeps ownership. */
+int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n,
+                                  const uint64_t* d_sa, const uint32_t* d_text,
+                                  void* stream);
+
+/* ---- SWIG surface (host pointers, synchronous) ------------------------- */
+
+/* FMIndex::size() -- fm_index.cpp:50-52: corpus tokens + 1 sentinel. */
+int fm_size(const fm_index* h, uint64_t* out);
+
+/* Number of distinct symbols in the BWT (sdsl wavelet_tree.sigma). */
+int fm_sigma(const fm_index* h, uint64_t* out);
+
+/* FMIndex::backward_search_step(symbol, low, high_inclusive) -- fm_index.cpp:67-97.
+ * out[0..1] = half-open (low', high'), (0,0) when empty; high clamped to n-1. */
+int fm_backward_search_step(fm_index* h, uint64_t symbol, uint64_t low, uint64_t high,
+                            uint64_t out[2]);
+
+/* FMIndex::backward_search_multi(query) -- fm_index.cpp:55-65: raw sdsl
+ * backward_search chained from (0, n-1) with no early exit; out = (l, r+1). */
+int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, uint64_t out[2]);
+
+/* FMIndex::distinct(low, high) -- fm_index.cpp:99-117: ascending distinct
+ * symbols of BWT[low, high).  Writes at most ``cap`` and the true count to *k. */
+int fm_distinct(fm_index* h, uint64_t low, uint64_t high, uint64_t* syms, uint64_t cap,
+                uint64_t* k);
+
+/* FMIndex::distinct_count(low, high) -- fm_index.cpp:119-144: interleaved
+ * [s0, c0, s1, c1, ...]; ``cap`` counts uint64 slots; *k = number of symbols. */
+int fm_distinct_count(fm_index* h, uint64_t low, uint64_t high, uint64_t* out, uint64_t cap,
+                      uint64_t* k);
+
+/* FMIndex::distinct_count_multi(lows, highs) -- fm_index.cpp:146-166, one GPU
+ * launch for all m ranges instead of one std::async per range.  Results of
+ * range i are interleaved pairs at out[2*offsets[i] .. 2*offsets[i+1]);
+ * ``offsets`` (m+1 entries) is written by the call; ``cap`` counts uint64
+ * slots of ``out``.  Returns -2 (and offsets filled) if cap is too small. */
+int fm_distinct_count_multi(fm_index* h, const uint64_t* lows, const uint64_t* highs,
+                            uint64_t m, uint64_t* out, uint64_t cap, uint64_t* offsets);
+
+/* Batched get_range (index.py:103-114) for host CSR patterns of token ids:
+ * pattern i = tokens[offsets[i] .. offsets[i+1]); symbol = token + shift.
+ * Starts at (0, n) (or (lo_in[i], hi_in[i]) when lo_in != NULL) and stops at
+ * the first empty step with (0, 0). */
+int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offsets, uint64_t m,
+                       int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in,
+                       uint64_t* lo_out, uint64_t* hi_out);
+
+/* FMIndex::locate(row) -- fm_index.cpp:168-172: SA[row]; UINT64_MAX if row >= n. */
+int fm_locate(fm_index* h, uint64_t row, uint64_t* out);
+
+/* FMIndex::extract_text(begin, end) -- fm_index.cpp:174-194 (LF walk from
+ * isa[end-1], cyclic).  Writes min(len, cap) symbols; *len = true length. */
+int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, uint64_t cap,
+                    uint64_t* len);
+
+/* FMIndex::save(path) / load_FMIndex(path) -- fm_index.cpp:196-209.  Own
+ * little-endian binary format (sdsl's serialization is not reproduced). */
+int fm_save(fm_index* h, const char* path);
+int fm_load(fm_index** out, const char* path, int device);
+
+/* ---- batched hot path (device pointers, stream-ordered) ---------------- */
+
+/* One LF step per row for the incremental decode: state (lo[i], hi[i]) is a
+ * half-open range with (0,0) meaning "empty"; symbol = tokens[i] + shift.
+ * Equivalent to one iteration of index.py:109-112 (get_range's loop body),
+ * i.e. backward_search_step(sym, lo, hi-1) with its (0,0) mapping; an empty
+ * input state stays (0,0).  lo_out/hi_out may alias lo/hi. */
+int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift,
+                     const uint64_t* d_lo, const uint64_t* d_hi,
+                     uint64_t* d_lo_out, uint64_t* d_hi_out, uint64_t m, void* stream);
+
+/* Device get_range for CSR patterns (same semantics as fm_get_range_batch). */
+int fm_backward_search_batch(fm_index* h, const int64_t* d_tokens, const int64_t* d_offsets,
+                             uint64_t m, int64_t shift, const uint64_t* d_lo_in,
+                             const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
+                             void* stream);
+
+/* Allowed-next-token mask: mask[i*ld + t] = 1 iff symbol t+shift occurs in
+ * BWT[lo[i], hi[i]) (t in [0, vocab)), else 0.  This is the boolean core of
+ * every document_constrained_generation_* processor (the distinct list of
+ * index.py:161-174 scattered into a vocab row).  ``packed`` != 0 writes a
+ * bit mask instead (uint32 words, ld counts bytes and must be >= 4*ceil(vocab/32)). */
+int fm_allowed_mask_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
+                          uint8_t* d_mask, uint64_t ld, uint64_t vocab, int64_t shift,
+                          int packed, void* stream);
+
+/* Fused decode step: LF step (as fm_lf_step_batch, updating d_lo/d_hi in
+ * place) followed by the allowed mask of the new ranges.  A row whose token
+ * is < reset_below (e.g. -1) is reset to the full range (0, n) instead of
+ * stepping (a fresh sequence with an empty pattern). */
+int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                         uint64_t* d_lo, uint64_t* d_hi, uint64_t m, uint8_t* d_mask, uint64_t ld,
+                         uint64_t vocab, int packed, void* stream);
+
+/* Device distinct_count for m ranges: ascending symbols + counts per row in
+ * CSR slots d_cap_off[i] .. d_cap_off[i+1] (capacity, caller-computed as
+ * min(hi-lo, sigma) prefix sums; total_cap = d_cap_off[m] known on the host);
+ * the number written per row goes to d_k (UINT64_MAX = capacity overflow).
+ * Grows the handle's workspace on first use (not graph-capturable then). */
+int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
+                            const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
+                            uint64_t* d_counts, uint64_t* d_k, void* stream);
+
+/* ---- introspection (bench / roofline accounting) ----------------------- */
+
+/* Wavelet levels L, bytes of each device structure. */
+int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
+             uint64_t* bitmap_bytes, uint64_t* bitmap_block);
+
+/* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces. */
+int fm_device_bwt(const fm_index* h, const uint32_t** out);
+
+/* Synchronise the handle's device (hipDeviceSynchronize on its device). */
+int fm_synchronize(fm_index* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FMIDX_H_ */

@@ -1,0 +1,78 @@
+"""C-ABI surface (CPU): the library loads, exports every symbol declared in
+include/fmidx.h, the ctypes table matches the header, and -- with no GPU --
+creating an index fails loudly instead of falling back to a CPU path."""
+import os
+import re
+
+import pytest
+
+from conftest import REPO, gpu_available
+
+HEADER = os.path.join(REPO, "include", "fmidx.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for required in ["fm_create", "fm_destroy", "fm_initialize", "fm_initialize_from_file", "fm_size",
+                     "fm_backward_search_step", "fm_backward_search_multi", "fm_distinct",
+                     "fm_distinct_count", "fm_distinct_count_multi", "fm_locate", "fm_extract_text",
+                     "fm_save", "fm_load", "fm_lf_step_batch", "fm_allowed_mask_batch",
+                     "fm_distinct_count_batch", "fm_decode_step_batch"]:
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from fmidx._lib import SIGNATURES, lib
+
+    dll = lib()
+    names = declared_functions()
+    for name in names:
+        assert hasattr(dll, name), name
+    assert sorted(SIGNATURES) == names
+
+
+def test_nm_exports_match_header():
+    import subprocess
+
+    from fmidx._lib import LIB_PATH
+
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True).stdout
+    exported = sorted(set(re.findall(r" T (fm_[a-z0-9_]+)", out)))
+    assert exported == declared_functions()
+
+
+@pytest.mark.skipif(gpu_available(), reason="only meaningful without a GPU")
+def test_no_cpu_fallback_without_gpu():
+    from fmidx._lib import FMIndexError
+    from fmidx.fm_index import FMIndex
+
+    with pytest.raises(FMIndexError):
+        FMIndex(device=0)
+
+
+def test_swig_argument_errors_before_device():
+    from fmidx.fm_index import _u64, _u64_vec
+
+    with pytest.raises(OverflowError):
+        _u64(-1, "backward_search_step", 2)
+    with pytest.raises(TypeError):
+        _u64(1.5, "backward_search_step", 2)
+    with pytest.raises(OverflowError):
+        _u64_vec([1, -2], "initialize", 2)
+    assert _u64_vec([1, 2, 3], "initialize", 2).tolist() == [1, 2, 3]
+
+
+def test_encode_corpus_matches_reference_encoding():
+    from fmidx.index import encode_corpus
+    from oracle.fm_oracle import encode_corpus as oracle_encode
+
+    docs = [[1, 2, 3], [], [5], [0, 9, 9]]
+    data, beg, occ = encode_corpus(docs)
+    d2, b2, o2 = oracle_encode(docs)
+    assert data.tolist() == d2 and beg == b2 and occ == o2

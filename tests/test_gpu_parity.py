@@ -1,0 +1,318 @@
+"""GPU parity: the HIP engine (through libfmidx.so's C-ABI) against the oracle
+and the golden vectors from the reference's own index.py.  Integer results
+must be bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.fm_oracle import NaiveFMIndex, OracleIndex, UINT64_MAX, allowed_mask
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def ours_index(docs, bm_log2=None):
+    from fmidx.index import FMIndex
+
+    old = os.environ.get("FMIDX_BM_LOG2")
+    if bm_log2 is not None:
+        os.environ["FMIDX_BM_LOG2"] = str(bm_log2)
+    try:
+        idx = FMIndex(device=0)
+        idx.initialize(docs, in_memory=True)
+    finally:
+        if bm_log2 is not None:
+            if old is None:
+                del os.environ["FMIDX_BM_LOG2"]
+            else:
+                os.environ["FMIDX_BM_LOG2"] = old
+    return idx
+
+
+def markov_docs(seed, n_docs, vocab, max_len, sticky=0.7):
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(n_docs):
+        ln = int(rng.integers(1, max_len + 1))
+        tok = int(rng.integers(0, vocab))
+        d = []
+        for _ in range(ln):
+            d.append(tok)
+            tok = (tok * 31 + 7) % vocab if rng.random() < sticky else int(rng.integers(0, vocab))
+        docs.append(d)
+    return docs
+
+
+# ---------------------------------------------------------------- golden
+def test_golden_index_cases(dev, golden_index_cases):
+    from fmidx.index import FMIndex
+
+    checked = 0
+    for case in golden_index_cases:
+        if "docs" not in case:
+            continue
+        idx = FMIndex(device=0)
+        idx.initialize(case["docs"], in_memory=case["in_memory"])
+        name = case["name"]
+        assert idx.size() == case["n"], name
+        assert len(idx) == case["len"]
+        assert idx.beginnings == case["beginnings"]
+        assert sorted(idx.occurring) == case["occurring"]
+        assert idx.occurring_distinct == case["occurring_distinct"], name
+        assert idx.occurring_counts == case["occurring_counts"], name
+        pats = [p for p, *_ in case["get_range"]]
+        got = idx.get_ranges(pats)
+        for (p, lo, hi, cnt), g in zip(case["get_range"], got):
+            if p and min(p) + 10 < 0:
+                continue
+            assert g == (lo, hi), (name, p)
+            assert idx.get_range(p) == (lo, hi)
+            assert idx.get_count(p) == cnt
+        for a, b, d, c, raw, dist in case["distinct_count"]:
+            assert list(idx.distinct_count(a, b)) == raw, (name, a, b)
+            assert idx.get_distinct_count(a, b) == (d, c)
+            assert idx.get_distinct(a, b) == dist
+        multi = idx.get_distinct_count_multi(case["multi"]["lows"], case["multi"]["highs"])
+        assert [[list(a), list(b)] for a, b in multi] == case["multi"]["out"]
+        for s, lo, hi, out in case["backward_search_step"]:
+            assert list(idx.backward_search_step(s, lo, hi)) == out, (name, s, lo, hi)
+        for q, out in case["backward_search_multi"]:
+            assert list(idx.backward_search_multi(q)) == out
+        for r, out in case["locate"]:
+            assert idx.locate(r) == out
+        for a, b, out in case["extract_text"]:
+            assert list(idx.extract_text(a, b)) == out, (name, a, b)
+        for d, doc in case["get_doc"]:
+            assert idx.get_doc(d) == doc
+        for r, d in case["doc_index_from_row"]:
+            assert idx.get_doc_index_from_row(r) == d
+        checked += 1
+    assert checked >= 9
+
+
+def test_swig_surface_errors(dev):
+    from fmidx._lib import FMIndexError
+    from fmidx.fm_index import FMIndex
+
+    fm = FMIndex(device=0)
+    fm.initialize([11, 12, 13, 12])
+    with pytest.raises(OverflowError):
+        fm.backward_search_step(-1, 0, 3)
+    with pytest.raises(TypeError):
+        fm.distinct_count(0.5, 3)
+    with pytest.raises(FMIndexError):
+        fm.extract_text(7, 9)           # unbounded loop in the reference
+    with pytest.raises(FMIndexError):
+        FMIndex(device=0).initialize([3, 0, 4])   # sdsl rejects a 0 symbol
+    assert fm.locate(99) == UINT64_MAX
+
+
+# ---------------------------------------------------------------- random corpora
+@pytest.mark.parametrize("seed,n_docs,vocab,max_len,bm", [
+    (1, 40, 30, 60, 6),
+    (2, 200, 500, 120, 6),
+    (3, 300, 128256, 80, 7),
+    (4, 120, 5, 200, 5),
+    (5, 400, 2000, 150, None),
+])
+def test_random_corpora_vs_oracle(dev, seed, n_docs, vocab, max_len, bm):
+    import torch
+
+    docs = markov_docs(seed, n_docs, vocab, max_len)
+    ours = ours_index(docs, bm_log2=bm)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    assert ours.size() == n
+    assert ours.occurring_distinct == ora.occurring_distinct
+    assert ours.occurring_counts == ora.occurring_counts
+    rng = np.random.default_rng(seed + 100)
+    F = [t for d in reversed(docs) for t in d]
+    pats = []
+    for _ in range(300):
+        s = int(rng.integers(0, len(F)))
+        pats.append(F[s: s + int(rng.integers(1, 12))])
+    for _ in range(100):
+        pats.append([int(x) for x in rng.integers(0, vocab + 5, size=int(rng.integers(1, 4)))])
+    pats.append([])
+    got = ours.get_ranges(pats)
+    want = [ora.get_range(p) for p in pats]
+    assert got == want
+    # ranges: pattern ranges + random + wide
+    lows, highs = [], []
+    for lo, hi in want:
+        lows.append(lo)
+        highs.append(hi)
+    for _ in range(100):
+        a = int(rng.integers(0, n + 1))
+        b = int(rng.integers(a, n + 1))
+        lows.append(a)
+        highs.append(b)
+    lows += [0, 0, n - 1, 5, 0]
+    highs += [n, n - 1, n, 3, n + 9]
+    assert ours.distinct_count_multi(lows, highs) == ora.distinct_count_multi(lows, highs)
+    # allowed masks: unpacked and packed, token space with SHIFT
+    lo_t = torch.tensor(lows, dtype=torch.int64, device=dev)
+    hi_t = torch.tensor(highs, dtype=torch.int64, device=dev)
+    V = min(vocab + 3, 128256)
+    mask = ours.allowed_mask(lo_t, hi_t, V, 10).cpu().numpy()
+    ref = allowed_mask(ora, lows, highs, V, 10)
+    assert np.array_equal(mask, ref)
+    packed = ours.allowed_mask(lo_t, hi_t, V, 10, packed=True).cpu().numpy().view(np.uint32)
+    unpacked = np.unpackbits(packed.view(np.uint8), axis=1, bitorder="little")[:, :V]
+    assert np.array_equal(unpacked, ref)
+    # device distinct_count with counts
+    syms, counts, k, cap_off = ours.distinct_count_batch(lo_t, hi_t)
+    syms, counts, k, cap_off = [x.cpu().numpy() for x in (syms, counts, k, cap_off)]
+    for i, (a, b) in enumerate(zip(lows, highs)):
+        exp = ora.distinct_count(a, b)
+        s0 = int(cap_off[i])
+        got_i = []
+        for j in range(int(k[i])):
+            got_i += [int(syms[s0 + j]), int(counts[s0 + j])]
+        assert tuple(got_i) == exp, (a, b)
+
+
+def test_incremental_lf_equals_full_research(dev):
+    """Carrying (lo, hi) across decode steps == re-running get_range on the
+    whole pattern every step (index.py:103-114), including early exit."""
+    import torch
+
+    docs = markov_docs(7, 150, 60, 100)
+    ours = ours_index(docs, bm_log2=6)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    F = [t for d in reversed(docs) for t in d]
+    rng = np.random.default_rng(9)
+    B, S = 64, 20
+    starts = rng.integers(0, len(F) - S - 1, size=B)
+    toks = np.zeros((S, B), dtype=np.int64)
+    for b in range(B):
+        for s in range(S):
+            toks[s, b] = F[starts[b] + s] if rng.random() < 0.85 else int(rng.integers(0, 70))
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.full((B,), ours.size(), dtype=torch.int64, device=dev)
+    for s in range(S):
+        t = torch.tensor(toks[s], device=dev)
+        ours.lf_step_batch(t, lo, hi, 10)
+        got = list(zip(lo.cpu().tolist(), hi.cpu().tolist()))
+        want = [ora.get_range(toks[: s + 1, b].tolist()) for b in range(B)]
+        assert got == want, s
+
+
+def test_decode_step_fused_and_reset(dev):
+    import torch
+
+    docs = markov_docs(11, 80, 40, 90)
+    ours = ours_index(docs, bm_log2=5)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    B, V = 16, 50
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.full((B,), n, dtype=torch.int64, device=dev)
+    state = [(0, n)] * B
+    rng = np.random.default_rng(3)
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    for step in range(12):
+        tk = rng.integers(0, 45, size=B)
+        tk[rng.random(B) < 0.2] = -1        # reset rows
+        ours.decode_step(torch.tensor(tk, device=dev), lo, hi, mask, V, 10, reset_below=0)
+        new = []
+        for b in range(B):
+            if tk[b] < 0:
+                new.append((0, n))
+            else:
+                l, h = state[b]
+                new.append((0, 0) if l >= h else ora.backward_search_step(int(tk[b]) + 10, l, h - 1))
+        state = new
+        assert list(zip(lo.cpu().tolist(), hi.cpu().tolist())) == state
+        ref = allowed_mask(ora, [s[0] for s in state], [s[1] for s in state], V, 10)
+        assert np.array_equal(mask.cpu().numpy(), ref)
+
+
+def test_device_build_matches_host_build(dev):
+    import torch
+
+    from fmidx.fm_index import FMIndex
+
+    docs = markov_docs(21, 100, 300, 100)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    bwt = torch.tensor(ora.bwt.astype(np.int32), device=dev)
+    sa = torch.tensor(ora.sa.astype(np.int64), device=dev)
+    text = torch.tensor(ora.text.astype(np.int32), device=dev)
+    fm = FMIndex(device=0)
+    fm.initialize_from_bwt_device(bwt, sa, text)
+    assert fm.size() == n
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        a = int(rng.integers(0, n))
+        b = int(rng.integers(a, n + 1))
+        assert fm.distinct_count(a, b) == ora.distinct_count(a, b)
+        s = int(rng.integers(10, 320))
+        assert fm.backward_search_step(s, a, b) == ora.backward_search_step(s, a, b)
+        assert fm.locate(a) == ora.locate(a)
+        if b > a:
+            assert fm.extract_text(a, b) == ora.extract_text(a, b)
+
+
+def test_save_load_roundtrip(dev, tmp_path):
+    from fmidx.index import FMIndex
+
+    docs = markov_docs(31, 30, 50, 40)
+    a = ours_index(docs)
+    a.labels = [f"doc{i}" for i in range(len(docs))]
+    a.save(str(tmp_path / "idx"))
+    b = FMIndex.load(str(tmp_path / "idx"), device=0)
+    assert b.size() == a.size() and b.beginnings == a.beginnings and b.labels == a.labels
+    assert b.occurring_distinct == a.occurring_distinct
+    for d in range(len(docs)):
+        assert b.get_doc(d) == a.get_doc(d)
+
+
+def test_properties_at_scale(dev):
+    """Size-independent properties on a ~1M-token index: counts sum to the
+    range width, mask popcount == number of distinct symbols, LF of every
+    distinct symbol has width == its count."""
+    import torch
+
+    from fmidx.index import FMIndex
+
+    rng = np.random.default_rng(77)
+    docs = [rng.integers(0, 20000, size=int(rng.integers(50, 1500))).tolist() for _ in range(1200)]
+    idx = FMIndex(device=0)
+    idx.initialize(docs, in_memory=True)
+    n = idx.size()
+    m = 64
+    a = rng.integers(0, n, size=m)
+    w = np.minimum(rng.integers(1, 400000, size=m), n - a)
+    b = a + w
+    lo_t = torch.tensor(a, dtype=torch.int64, device=dev)
+    hi_t = torch.tensor(b, dtype=torch.int64, device=dev)
+    syms, counts, k, off = idx.distinct_count_batch(lo_t, hi_t)
+    mask = idx.allowed_mask(lo_t, hi_t, 20010, 10)
+    k = k.cpu().numpy()
+    off = off.cpu().numpy()
+    syms = syms.cpu().numpy()
+    counts = counts.cpu().numpy()
+    pop = mask.sum(1).cpu().numpy()
+    for i in range(m):
+        s0 = off[i]
+        c = counts[s0: s0 + k[i]]
+        sy = syms[s0: s0 + k[i]]
+        assert int(c.sum()) == int(b[i] - a[i])
+        assert int(pop[i]) == int((sy >= 10).sum())
+        assert np.all(np.diff(sy) > 0)
+        for j in rng.choice(int(k[i]), size=min(5, int(k[i])), replace=False):
+            lo2, hi2 = idx.backward_search_step(int(sy[j]), int(a[i]), int(b[i]) - 1)
+            assert hi2 - lo2 == int(c[j])
