@@ -1,0 +1,388 @@
+#!/usr/bin/env python
+"""bench.py -- allowed-token masks/s of the FM-index decode step on MI355X.
+
+One step = one decode step of the hot path for B rows: the LF (backward-search)
+update of every row's (low, high) range by its new token, then the
+allowed-next-token mask bool[B, V] of the new ranges (SURVEY §8a A2-A8,
+incremental mode of §5 "long-context").  Inputs (index, decode trace,
+states) are resident in HBM before timing.
+
+Workload: seeded order-1 Markov corpus with Zipf(1.1) rows over
+V = 128256 (+SHIFT 10, 17 wavelet levels), lognormal docs (mean ~500),
+encoded exactly as index.py:47-53; suffix array built on the GPU.  Decode
+trace: B rows start from U{1..32}-token true corpus patterns; each step a row
+appends a true continuation (a random occurrence's next token, p = 0.9) or a
+uniform random id; a row whose range is empty restarts as a fresh sequence
+(empty pattern = full range); row 0 is an empty-pattern row, row 1 an
+eos-terminated (empty-range) row.
+
+Multi-GPU (--gpus N under torch.distributed.run): replicas -- every rank holds
+the full index and decodes its own B rows (weak scaling, no data-path
+collective); value = N*B*K / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "fm-index-constrained-decoding_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from fmidx.fm_index import FMIndex  # noqa: E402
+from fmidx.synth import bwt_from_sa, markov_corpus_gpu, suffix_array_gpu  # noqa: E402
+
+SHIFT = 10
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 measured stream)
+METRIC = "allowed-token masks/sec @ B=256, 128k vocab"
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------
+def build_index(n_tokens: int, vocab: int, seed: int, dev):
+    t0 = time.time()
+    text, beg = markov_corpus_gpu(n_tokens, vocab, seed, dev)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    sa = suffix_array_gpu(text)
+    torch.cuda.synchronize()
+    t2 = time.time()
+    bwt = bwt_from_sa(text, sa)
+    del sa
+    fm = FMIndex(device=dev.index)
+    fm.initialize_from_bwt_device(bwt)
+    torch.cuda.synchronize()
+    t3 = time.time()
+    log(f"corpus {t1 - t0:.1f}s  suffix array {t2 - t1:.1f}s  index {t3 - t2:.1f}s  n={bwt.numel()}")
+    return fm, text, bwt, {"corpus_s": t1 - t0, "sa_s": t2 - t1, "index_s": t3 - t2}
+
+
+def make_trace(fm, text, bwt, B: int, V: int, S: int, seed: int, dev):
+    """Decode trace (untimed): tokens[S, B] (-1 = restart as a fresh sequence)
+    and the states after every step (for byte accounting and the CPU leg)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 1)
+    n = bwt.numel()
+    # initial patterns: true corpus n-grams of F = reverse(T') (the text patterns match)
+    lens = torch.randint(1, 33, (B,), generator=g, device=dev)
+    q = torch.randint(0, n - 40, (B,), generator=g, device=dev)
+    offs = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    tot = int(offs[-1].item())
+    row_of = torch.repeat_interleave(torch.arange(B, device=dev), lens)
+    k = torch.arange(tot, device=dev) - offs[:-1][row_of]
+    fpos = q[row_of] + k                              # F position
+    toks = text[(n - 2) - fpos].to(torch.int64) - SHIFT
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.zeros(B, dtype=torch.int64, device=dev)
+    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    lo[0], hi[0] = 0, n          # empty-pattern row
+    lo[1], hi[1] = 0, 0          # eos-terminated row
+    init = (lo.clone(), hi.clone())
+    tokens = torch.empty((S, B), dtype=torch.int64, device=dev)
+    lo_hist = torch.empty((S, B), dtype=torch.int64, device=dev)
+    hi_hist = torch.empty((S, B), dtype=torch.int64, device=dev)
+    dummy = torch.empty((1, 1), dtype=torch.uint8, device=dev)
+    for s in range(S):
+        live = lo < hi
+        width = (hi - lo).clamp(min=1)
+        u = torch.rand(B, generator=g, device=dev, dtype=torch.float64)
+        j = (lo + (u * width.to(torch.float64)).to(torch.int64).clamp(max=n - 1)).clamp(max=n - 1)
+        true_tok = bwt[j].to(torch.int64) - SHIFT
+        rnd = torch.randint(0, V, (B,), generator=g, device=dev)
+        coin = torch.rand(B, generator=g, device=dev) < 0.9
+        tok = torch.where(coin & (true_tok >= 0), true_tok, rnd)
+        tok = torch.where(live, tok, torch.full_like(tok, -1))
+        tok[0] = -1
+        tok[1] = V + 1000             # unknown id: the eos row stays empty
+        tokens[s] = tok
+        fm.decode_step(tok, lo, hi, dummy, 0, SHIFT, reset_below=0)
+        lo_hist[s] = lo
+        hi_hist[s] = hi
+    torch.cuda.synchronize()
+    return tokens, init, lo_hist, hi_hist
+
+
+def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int):
+    """Bytes the mask algorithm must read per row: streamed BWT symbols (4 B)
+    + whole range bitmaps (mirrors plan_range in query.hip)."""
+    B0 = 1 << b0_log2
+    out = np.zeros(lo.size, dtype=np.int64)
+    for i, (l, h) in enumerate(zip(lo.tolist(), hi.tolist())):
+        h = min(h, n)
+        if l >= h:
+            continue
+        if bm_levels == 0 or h - l <= B0:
+            out[i] = 4 * (h - l)
+            continue
+        x = (l + B0 - 1) >> b0_log2
+        y = h >> b0_log2
+        if x >= y:
+            out[i] = 4 * (h - l)
+            continue
+        nb = 0
+        while x < y:
+            j = 0
+            while j + 1 < bm_levels:
+                span = 1 << (2 * (j + 1))
+                if (x & (span - 1)) or x + span > y:
+                    break
+                j += 1
+            nb += 1
+            x += 1 << (2 * j)
+        out[i] = 4 * (((((l + B0 - 1) >> b0_log2) << b0_log2) - l) + (h - ((h >> b0_log2) << b0_log2))) \
+            + nb * bm_bytes_each
+    return out
+
+
+# ---------------------------------------------------------------------------
+def cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, warmup, seconds, dev):
+    """The sdsl-faithful C++ restatement (oracle/cpu_ref.cpp) on the host
+    cores, replaying the same trace from step `warmup` until ~`seconds`."""
+    from oracle.cpu_ref import CpuRef
+
+    n = bwt.numel()
+    L = max(1, int(bwt.max().item()).bit_length())
+    wpl = (n + 63) // 64
+    words = np.zeros((L, wpl), dtype=np.uint64)
+    b64 = bwt.to(torch.int64)
+    pw = (torch.ones(1, dtype=torch.int64, device=dev) << torch.arange(64, device=dev, dtype=torch.int64))
+    for lev in range(L):
+        if lev == 0:
+            seq = b64
+        else:
+            _, order = torch.sort(b64 >> (L - lev), stable=True)
+            seq = b64[order]
+            del order
+        bits = ((seq >> (L - 1 - lev)) & 1)
+        pad = torch.zeros(wpl * 64, dtype=torch.int64, device=dev)
+        pad[:n] = bits
+        w = (pad.view(-1, 64) * pw).sum(1)
+        words[lev] = w.cpu().numpy().view(np.uint64)
+        del seq, bits, pad, w
+    cnt = torch.bincount(b64, minlength=(1 << L) + 1)
+    C = torch.zeros((1 << L) + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt[: 1 << L], 0, out=C[1:])
+    sigma = int((cnt > 0).sum().item())
+    C = C.cpu().numpy().view(np.uint64)
+    del b64, cnt
+    t0 = time.time()
+    ref = CpuRef(words, n, L, C, sigma)
+    log(f"cpu_ref build {time.time() - t0:.1f}s")
+    threads = int(os.environ.get("FMIDX_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    B = tokens.shape[1]
+    tok_np = tokens.cpu().numpy()
+    lo = lo_hist[warmup - 1].cpu().numpy().astype(np.uint64) if warmup > 0 else None
+    hi = hi_hist[warmup - 1].cpu().numpy().astype(np.uint64) if warmup > 0 else None
+    mask = np.zeros((B, V), dtype=np.uint8)
+    rows = 0
+    steps = 0
+    t0 = time.time()
+    s = warmup
+    while s < tok_np.shape[0]:
+        ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, lo, hi, mask, threads)
+        rows += B
+        steps += 1
+        s += 1
+        if time.time() - t0 >= seconds:
+            break
+    el = time.time() - t0
+    ok = bool(np.array_equal(lo, lo_hist[s - 1].cpu().numpy().astype(np.uint64)))
+    return {"value": rows / el, "unit": "masks/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} decode steps x {B} rows of the same trace (steps {warmup}..{s - 1}), "
+                      f"same n={n} index, sdsl-faithful wt_int + rank_support_v restatement, "
+                      f"{threads} threads, {el:.1f}s; final ranges match GPU: {ok}"}
+
+
+# ---------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--tokens", type=float, default=float(os.environ.get("FMIDX_BENCH_TOKENS", 3.0e8)))
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--vocab", type=int, default=128256)
+    ap.add_argument("--seed", type=int, default=20250905)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-steps", type=int, default=600)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    n_tokens = int(args.tokens)
+    B, V, K, W = args.batch, args.vocab, args.steps, args.warmup
+
+    fm, text, bwt, build_t = build_index(n_tokens, V, args.seed, dev)
+    n = bwt.numel()
+    st = fm.stats()
+    S = W + K
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
+    # the CPU leg replays the same trace past the GPU's steps (bounded by time)
+    S_trace = S + (args.cpu_steps if cpu_leg else 0)
+    tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
+    del text
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    lo = init[0].clone()
+    hi = init[1].clone()
+    dummy = torch.empty((1, 1), dtype=torch.uint8, device=dev)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    for s in range(W):
+        fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    t_start = torch.cuda.Event(enable_timing=True)
+    t_end = torch.cuda.Event(enable_timing=True)
+    wall0 = time.time()
+    t_start.record(stream)
+    for i in range(K):
+        s = W + i
+        ev[i][0].record(stream)
+        fm.decode_step(tokens[s], lo, hi, dummy, 0, SHIFT, reset_below=0)      # LF kernel (with restarts)
+        ev[i][1].record(stream)
+        fm.allowed_mask(lo, hi, V, SHIFT, out=mask)                               # mask kernel
+        ev[i][2].record(stream)
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    wall = time.time() - wall0
+    elapsed_ms = t_start.elapsed_time(t_end)
+    lf_ms = [e[0].elapsed_time(e[1]) for e in ev]
+    mask_ms = [e[1].elapsed_time(e[2]) for e in ev]
+    ok = bool(torch.equal(lo, lo_hist[S - 1]) and torch.equal(hi, hi_hist[S - 1]))
+
+    step_ms = elapsed_ms / K
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([step_ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_ms = float(t.item())
+    value = world * B * K / (step_ms * K / 1e3)
+
+    # ---- roofline accounting for the dominant (mask) kernel
+    lo_np = lo_hist[W:S].cpu().numpy()
+    hi_np = hi_hist[W:S].cpu().numpy()
+    max_sym = int(bwt.max().item())
+    words = ((max_sym + 1 + 127) // 128) * 4
+    b0 = st["bitmap_block"]
+    b0_log2 = b0.bit_length() - 1 if b0 else 0
+    nb0 = n >> b0_log2 if b0 else 0
+    bm_levels = 0
+    c = nb0
+    while c > 0:
+        bm_levels += 1
+        c >>= 2
+    read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4) for i in range(K)])
+    mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
+    mask_us = float(np.mean(mask_ms)) * 1e3
+    achieved = mask_bytes_per_launch / (mask_us * 1e-6) / 1e9
+    L = st["levels"]
+    # LF: two 64-B rank blocks per level per row that was live (restarts cost nothing)
+    prev_lo = np.concatenate([lo_hist[W - 1:W].cpu().numpy(), lo_np[:-1]]) if W > 0 else lo_np
+    prev_hi = np.concatenate([hi_hist[W - 1:W].cpu().numpy(), hi_np[:-1]]) if W > 0 else hi_np
+    tok_np = tokens[W:S].cpu().numpy()
+    live = (prev_lo < prev_hi) & (tok_np >= 0)
+    lf_bytes = 64 * 2 * L * live.sum(1)
+    lf_us = float(np.mean(lf_ms)) * 1e3
+    rank_gbs = float(lf_bytes.mean()) / (lf_us * 1e-6) / 1e9
+    widths = (hi_np - lo_np)
+    log(f"step {step_ms * 1e3:.1f}us (lf {lf_us:.1f}us, mask {mask_us:.1f}us, wall/step {wall / K * 1e6:.1f}us) "
+        f"mask bytes/launch {mask_bytes_per_launch / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
+        f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}")
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "masks/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": step_ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "uint64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
+                        f"of n={n} tokens (C2 scale), B={B} rows, V={V}, incremental ranges",
+            "corpus_tokens": n,
+            "global_batch": world * B,
+            "batch_per_gpu": B,
+            "vocab": V,
+            "wavelet_levels": L,
+            "parallelism": f"replicas{world}",
+            "mask": "uint8[B,V]",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "k_mask",
+            "alg_bytes_per_launch": mask_bytes_per_launch,
+            "avg_launch_us": mask_us,
+        },
+        "lf_kernel": {"avg_launch_us": lf_us, "rank_GBps": rank_gbs,
+                      "alg_bytes_per_launch": float(lf_bytes.mean())},
+        "index": {"build": build_t, **st},
+        "trace_check": ok,
+    }
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                t = json.load(f)
+            if t.get("corpus_tokens") == n and t.get("batch") == B:
+                result["roofline"]["traffic"] = t.get("k_mask_bytes_per_launch")
+        except Exception:
+            pass
+    if cpu_leg:
+        try:
+            result["cpu_baseline"] = cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, W, args.cpu_seconds, dev)
+        except Exception as e:  # the GPU line must still print
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

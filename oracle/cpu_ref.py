@@ -1,0 +1,102 @@
+"""ctypes wrapper of oracle/_build/libcpuref.so -- TEST INFRASTRUCTURE ONLY
+(the sdsl-faithful CPU restatement used as checker and as the bench's
+cpu_baseline).  See cpu_ref.cpp for what it restates."""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_int, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libcpuref.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle`")
+        d = ctypes.CDLL(LIB)
+        u64p = POINTER(c_uint64)
+        d.cr_build.restype = c_void_p
+        d.cr_build.argtypes = [u64p, c_uint64, c_uint32, u64p, c_uint64]
+        d.cr_free.argtypes = [c_void_p]
+        d.cr_backward_search_step.argtypes = [c_void_p, c_uint64, c_uint64, c_uint64, u64p]
+        d.cr_distinct_count.restype = c_uint64
+        d.cr_distinct_count.argtypes = [c_void_p, c_uint64, c_uint64, u64p, c_uint64]
+        d.cr_decode_step.argtypes = [c_void_p, POINTER(c_int64), c_int64, c_int64, u64p, u64p, c_uint64,
+                                     POINTER(ctypes.c_uint8), c_uint64, c_int]
+        d.cr_full_step.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), c_int64, c_uint64, u64p, u64p,
+                                   POINTER(ctypes.c_uint8), c_uint64, c_int]
+        _lib = d
+    return _lib
+
+
+def _p(a, t=c_uint64):
+    return a.ctypes.data_as(POINTER(t))
+
+
+def levels_numpy(bwt: np.ndarray, L: int) -> np.ndarray:
+    """wt_int level bit vectors: level l = BWT stably sorted by its top l bits."""
+    n = bwt.size
+    wpl = (n + 63) // 64
+    out = np.zeros((L, wpl), dtype=np.uint64)
+    b = bwt.astype(np.int64)
+    for lev in range(L):
+        seq = b if lev == 0 else b[np.argsort(b >> (L - lev), kind="stable")]
+        bits = ((seq >> (L - 1 - lev)) & 1).astype(np.uint8)
+        packed = np.packbits(bits, bitorder="little")
+        buf = np.zeros(wpl * 8, dtype=np.uint8)
+        buf[: packed.size] = packed
+        out[lev] = buf.view(np.uint64)
+    return out
+
+
+def c_array(bwt: np.ndarray, L: int) -> np.ndarray:
+    cnt = np.bincount(bwt.astype(np.int64), minlength=(1 << L) + 1).astype(np.uint64)
+    C = np.zeros((1 << L) + 1, dtype=np.uint64)
+    np.cumsum(cnt[: 1 << L], out=C[1:])
+    return C
+
+
+class CpuRef:
+    def __init__(self, level_words: np.ndarray, n: int, L: int, C: np.ndarray, sigma: int):
+        self.n = n
+        self.L = L
+        lw = np.ascontiguousarray(level_words, dtype=np.uint64)
+        Cc = np.ascontiguousarray(C, dtype=np.uint64)
+        self._h = lib().cr_build(_p(lw), n, L, _p(Cc), sigma)
+
+    @classmethod
+    def from_bwt(cls, bwt: np.ndarray) -> "CpuRef":
+        bwt = np.asarray(bwt)
+        L = max(1, int(bwt.max()).bit_length())
+        return cls(levels_numpy(bwt, L), bwt.size, L, c_array(bwt, L), int(np.unique(bwt).size))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().cr_free(self._h)
+            self._h = None
+
+    def backward_search_step(self, c, low, high):
+        out = np.zeros(2, dtype=np.uint64)
+        lib().cr_backward_search_step(self._h, c, low, high, _p(out))
+        return int(out[0]), int(out[1])
+
+    def distinct_count(self, low, high):
+        cap = 2 * max(1, min(max(0, min(high, self.n) - low), 1 << self.L))
+        out = np.zeros(cap, dtype=np.uint64)
+        k = lib().cr_distinct_count(self._h, low, high, _p(out), cap)
+        return tuple(int(x) for x in out[: 2 * k])
+
+    def decode_step(self, tok: np.ndarray, shift: int, reset_below: int, lo: np.ndarray, hi: np.ndarray,
+                    mask: np.ndarray, threads: int):
+        lib().cr_decode_step(self._h, _p(tok, c_int64), shift, reset_below, _p(lo), _p(hi), lo.size,
+                             _p(mask, ctypes.c_uint8), mask.shape[1], threads)
+
+    def full_step(self, tokens: np.ndarray, offsets: np.ndarray, shift: int, lo, hi, mask, threads: int):
+        lib().cr_full_step(self._h, _p(tokens, c_int64), _p(offsets, c_int64), shift, lo.size, _p(lo), _p(hi),
+                           _p(mask, ctypes.c_uint8), mask.shape[1], threads)
