@@ -231,7 +231,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n_tokens = int(args.tokens)
-    B, V, K, W = args.batch, args.vocab, args.steps, args.warmup
+    B, V, K, W = args.batch, args.vocab, args.steps, max(1, args.warmup)
 
     fm, text, bwt, build_t = build_index(n_tokens, V, args.seed, dev)
     n = bwt.numel()
@@ -256,32 +256,64 @@ def main():
     for s in range(W):
         fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
     torch.cuda.synchronize()
+    state_lo, state_hi = lo.clone(), hi.clone()
+
+    # Capture the K timed steps into one HIP graph (the C-ABI launches go onto
+    # torch's capture stream), plus per-kernel graphs for the roofline: K LF
+    # launches from the recorded states, and K mask launches on the recorded
+    # post-LF states.  Replays are timed with HIP events on the stream they run on.
+    lo_scr = torch.empty_like(lo)
+    hi_scr = torch.empty_like(hi)
+    g_step = torch.cuda.CUDAGraph()
+    g_lf = torch.cuda.CUDAGraph()
+    g_mask = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_step):
+        for i in range(K):
+            fm.decode_step(tokens[W + i], lo, hi, mask, V, SHIFT, reset_below=0)
+    with torch.cuda.graph(g_lf):
+        for i in range(K):
+            fm.lf_step_batch(tokens[W + i], lo_hist[W + i - 1], hi_hist[W + i - 1], SHIFT,
+                             lo_out=lo_scr, hi_out=hi_scr, reset_below=0)
+    with torch.cuda.graph(g_mask):
+        for i in range(K):
+            fm.allowed_mask(lo_hist[W + i], hi_hist[W + i], V, SHIFT, out=mask)
+
+    def timed(graph, reps=1, reset=False):
+        ts = []
+        for _ in range(reps):
+            if reset:
+                lo.copy_(state_lo)
+                hi.copy_(state_hi)
+            torch.cuda.synchronize()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            graph.replay()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return ts
+
+    timed(g_step, 2, reset=True)                  # warm the graph (caches, TLB)
+    lf_ms = [t / K for t in timed(g_lf, 5)]
+    mask_ms = [t / K for t in timed(g_mask, 5)]
+    lo.copy_(state_lo)
+    hi.copy_(state_hi)
+    torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    wall0 = time.time()
     t_start = torch.cuda.Event(enable_timing=True)
     t_end = torch.cuda.Event(enable_timing=True)
-    wall0 = time.time()
-    t_start.record(stream)
-    for i in range(K):
-        s = W + i
-        ev[i][0].record(stream)
-        fm.decode_step(tokens[s], lo, hi, dummy, 0, SHIFT, reset_below=0)      # LF kernel (with restarts)
-        ev[i][1].record(stream)
-        fm.allowed_mask(lo, hi, V, SHIFT, out=mask)                               # mask kernel
-        ev[i][2].record(stream)
-    t_end.record(stream)
+    t_start.record()
+    g_step.replay()
+    t_end.record()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     wall = time.time() - wall0
     elapsed_ms = t_start.elapsed_time(t_end)
-    lf_ms = [e[0].elapsed_time(e[1]) for e in ev]
-    mask_ms = [e[1].elapsed_time(e[2]) for e in ev]
     ok = bool(torch.equal(lo, lo_hist[S - 1]) and torch.equal(hi, hi_hist[S - 1]))
-
     step_ms = elapsed_ms / K
     if world > 1:
         import torch.distributed as dist
@@ -306,7 +338,7 @@ def main():
         c >>= 2
     read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4) for i in range(K)])
     mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
-    mask_us = float(np.mean(mask_ms)) * 1e3
+    mask_us = float(np.median(mask_ms)) * 1e3
     achieved = mask_bytes_per_launch / (mask_us * 1e-6) / 1e9
     L = st["levels"]
     # LF: two 64-B rank blocks per level per row that was live (restarts cost nothing)
@@ -315,10 +347,10 @@ def main():
     tok_np = tokens[W:S].cpu().numpy()
     live = (prev_lo < prev_hi) & (tok_np >= 0)
     lf_bytes = 64 * 2 * L * live.sum(1)
-    lf_us = float(np.mean(lf_ms)) * 1e3
+    lf_us = float(np.median(lf_ms)) * 1e3
     rank_gbs = float(lf_bytes.mean()) / (lf_us * 1e-6) / 1e9
     widths = (hi_np - lo_np)
-    log(f"step {step_ms * 1e3:.1f}us (lf {lf_us:.1f}us, mask {mask_us:.1f}us, wall/step {wall / K * 1e6:.1f}us) "
+    log(f"step {step_ms * 1e3:.1f}us (lf {lf_us:.1f}us, mask {mask_us:.1f}us, wall/step {wall / K * 1e6:.1f}us, graph) "
         f"mask bytes/launch {mask_bytes_per_launch / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
         f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}")
 

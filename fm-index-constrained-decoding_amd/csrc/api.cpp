@@ -628,12 +628,12 @@ int fm_load(fm_index** out, const char* path, int device) {
 
 // ---- batched device entry points ------------------------------------------
 
-int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, const uint64_t* d_lo,
-                     const uint64_t* d_hi, uint64_t* d_lo_out, uint64_t* d_hi_out, uint64_t m,
-                     void* stream) {
+int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                     const uint64_t* d_lo, const uint64_t* d_hi, uint64_t* d_lo_out,
+                     uint64_t* d_hi_out, uint64_t m, void* stream) {
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
-  return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, INT64_MIN, d_lo, d_hi, d_lo_out,
+  return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out,
                                d_hi_out, m, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -167,6 +167,44 @@ __device__ void plan_range(const DevView& v, uint64_t lo, uint64_t hi, Plan& p) 
 
 __device__ __forceinline__ int64_t floor_div32(int64_t x) { return x >= 0 ? x / 32 : -((-x + 31) / 32); }
 
+__device__ __forceinline__ void set_bit(uint32_t* win, uint32_t sym, int64_t base_bit, int64_t lim) {
+  const int64_t rel = (int64_t)sym - base_bit;
+  if (rel >= 0 && rel < lim) atomicOr(&win[rel >> 5], 1u << (rel & 31));
+}
+
+// OR the symbols of BWT[a, b) into the LDS window.  The 16-B aligned middle is
+// read as uint4 with kUnroll loads in flight per thread before any LDS atomic.
+constexpr int kUnroll = 4;
+__device__ void stream_symbols(const uint32_t* __restrict__ bwt, uint64_t a, uint64_t b, int64_t base_bit,
+                               int64_t lim, uint32_t* win) {
+  const uint64_t a4 = (a + 3) & ~3ull;
+  const uint64_t b4 = b & ~3ull;
+  if (a4 >= b4) {
+    for (uint64_t i = a + threadIdx.x; i < b; i += kMaskThreads) set_bit(win, bwt[i], base_bit, lim);
+    return;
+  }
+  if (threadIdx.x < a4 - a) set_bit(win, bwt[a + threadIdx.x], base_bit, lim);
+  if (threadIdx.x < b - b4) set_bit(win, bwt[b4 + threadIdx.x], base_bit, lim);
+  const uint4* src = reinterpret_cast<const uint4*>(bwt);
+  const uint64_t q0 = a4 / 4, q1 = b4 / 4;
+  for (uint64_t base = q0 + threadIdx.x; base < q1; base += (uint64_t)kMaskThreads * kUnroll) {
+    uint4 q[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t j = base + (uint64_t)u * kMaskThreads;
+      q[u] = (j < q1) ? src[j] : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (q[u].x == ~0u) continue;
+      set_bit(win, q[u].x, base_bit, lim);
+      set_bit(win, q[u].y, base_bit, lim);
+      set_bit(win, q[u].z, base_bit, lim);
+      set_bit(win, q[u].w, base_bit, lim);
+    }
+  }
+}
+
 template <bool PACKED>
 __global__ void __launch_bounds__(kMaskThreads) k_mask(DevView v, const uint64_t* __restrict__ lo_a,
                                                       const uint64_t* __restrict__ hi_a, uint64_t m,
@@ -198,10 +236,8 @@ __global__ void __launch_bounds__(kMaskThreads) k_mask(DevView v, const uint64_t
     for (int part = 0; part < 2; ++part) {
       const uint64_t a = part ? plan.a1 : plan.a0;
       const uint64_t b = part ? plan.b1 : plan.b0;
-      for (uint64_t i = a + threadIdx.x; i < b; i += kMaskThreads) {
-        const int64_t rel = (int64_t)v.bwt[i] - base_bit;
-        if (rel >= 0 && rel < lim) atomicOr(&win[rel >> 5], 1u << (rel & 31));
-      }
+      if (a >= b) continue;
+      stream_symbols(v.bwt, a, b, base_bit, lim, win);
     }
     __syncthreads();
     const uint32_t nb = plan.nb;

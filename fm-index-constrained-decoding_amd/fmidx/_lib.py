@@ -38,8 +38,8 @@ SIGNATURES = {
     "fm_extract_text": (c_int, [c_void_p, c_uint64, c_uint64, u64p, c_uint64, u64p]),
     "fm_save": (c_int, [c_void_p, c_char_p]),
     "fm_load": (c_int, [POINTER(c_void_p), c_char_p, c_int]),
-    "fm_lf_step_batch": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                 c_uint64, c_void_p]),
+    "fm_lf_step_batch": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_uint64, c_void_p]),
     "fm_backward_search_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int64, c_void_p,
                                          c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_allowed_mask_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64,

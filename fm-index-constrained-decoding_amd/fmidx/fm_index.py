@@ -250,10 +250,11 @@ class FMIndex:
         return lo_out, hi_out
 
     # torch-tensor batched hot path (device pointers, current stream)
-    def lf_step_batch(self, tokens, lo, hi, shift: int, lo_out=None, hi_out=None):
+    def lf_step_batch(self, tokens, lo, hi, shift: int, lo_out=None, hi_out=None,
+                      reset_below: int = -(1 << 63)):
         lo_out = lo if lo_out is None else lo_out
         hi_out = hi if hi_out is None else hi_out
-        check(lib().fm_lf_step_batch(self._h, c_void_p(tokens.data_ptr()), int(shift),
+        check(lib().fm_lf_step_batch(self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below),
                                      c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
                                      c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()),
                                      lo.numel(), c_void_p(_stream_of(lo))), "lf_step_batch")

@@ -98,17 +98,18 @@ def suffix_array_gpu(text: torch.Tensor, sym_bits: int = 17) -> torch.Tensor:
     k[:-2] |= t[2:]
     del t
     h = 3
-    idx = torch.arange(n, device=dev, dtype=torch.int64)
     while True:
         keys, sa = torch.sort(k)
         del k
         head = torch.ones(n, dtype=torch.bool, device=dev)
         head[1:] = keys[1:] != keys[:-1]
         del keys
-        ngroups = int(head.sum().item())
-        grp = torch.where(head, idx, torch.zeros_like(idx))
+        gid = torch.cumsum(head, 0)
+        ngroups = int(gid[-1].item())
+        heads = torch.nonzero(head).squeeze(1)      # group-head positions
         del head
-        grp = torch.cummax(grp, 0).values
+        grp = heads[gid - 1]
+        del gid, heads
         rank = torch.empty_like(grp)
         rank[sa] = grp
         del grp

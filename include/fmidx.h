@@ -134,8 +134,10 @@ int fm_load(fm_index** out, const char* path, int device);
  * half-open range with (0,0) meaning "empty"; symbol = tokens[i] + shift.
  * Equivalent to one iteration of index.py:109-112 (get_range's loop body),
  * i.e. backward_search_step(sym, lo, hi-1) with its (0,0) mapping; an empty
- * input state stays (0,0).  lo_out/hi_out may alias lo/hi. */
-int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift,
+ * input state stays (0,0).  A row whose token is < reset_below restarts at
+ * the full range (0, n) (a fresh sequence with an empty pattern); pass
+ * INT64_MIN for plain get_range semantics.  lo_out/hi_out may alias lo/hi. */
+int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
                      const uint64_t* d_lo, const uint64_t* d_hi,
                      uint64_t* d_lo_out, uint64_t* d_hi_out, uint64_t m, void* stream);
 
