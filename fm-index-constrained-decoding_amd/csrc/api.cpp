@@ -657,14 +657,13 @@ int fm_allowed_mask_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
 }
 
 int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
-                         uint64_t* d_lo, uint64_t* d_hi, uint64_t m, uint8_t* d_mask, uint64_t ld,
+                         const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out,
+                         uint64_t* d_hi_out, uint64_t m, uint8_t* d_mask, uint64_t ld,
                          uint64_t vocab, int packed, void* stream) {
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo, d_hi, m, s))
-    return -1;
-  return fmidx::launch_mask(h->idx.view, d_lo, d_hi, m, d_mask, ld, vocab, shift, packed, s);
+  return fmidx::launch_decode(h->idx.view, d_tokens, shift, reset_below, d_lo_in, d_hi_in, d_lo_out,
+                              d_hi_out, m, d_mask, ld, vocab, packed, reinterpret_cast<hipStream_t>(stream));
 }
 
 int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,

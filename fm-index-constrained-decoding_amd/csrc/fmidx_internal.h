@@ -179,6 +179,9 @@ int launch_step_raw(const DevView& v, uint64_t sym, uint64_t low, uint64_t high,
 int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                 uint8_t* mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
                 hipStream_t s);
+int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
+                  const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                  uint64_t m, uint8_t* mask, uint64_t ld, uint64_t vocab, int packed, hipStream_t s);
 int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
                     void* ws, uint64_t total_cap, hipStream_t s);

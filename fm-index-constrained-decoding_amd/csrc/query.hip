@@ -136,33 +136,70 @@ struct Plan {
   uint64_t off[kMaxPlan];    // word offsets of those bitmaps
 };
 
-// Canonical decomposition of [lo, hi): two streamed partial ends plus aligned
-// bitmap blocks of size B0*4^j, largest first.
-__device__ void plan_range(const DevView& v, uint64_t lo, uint64_t hi, Plan& p) {
-  p.a0 = lo;
-  p.b0 = hi;
-  p.a1 = p.b1 = 0;
-  p.nb = 0;
-  if (v.bm_levels == 0) return;
+// Canonical decomposition of [lo, hi) into two streamed partial ends plus the
+// maximal aligned bitmap blocks (B0*4^j rows at level j), computed by wave 0
+// with one lane per bitmap level: with a_j / b_j = x / y rounded up / down to
+// level-j alignment and `top` the highest level holding a whole block, level
+// j < top contributes [a_j, a_{j+1}) and [b_{j+1}, b_j), level top [a_top,
+// b_top) -- the same set the greedy left-to-right cover produces (<= 6 per level).
+__device__ void plan_range_wave(const DevView& v, uint64_t lo, uint64_t hi, Plan& p) {
+  const uint32_t lane = threadIdx.x;   // called by the 64 lanes of wave 0
   const uint32_t lg = v.bm_log2;
   const uint64_t B0 = 1ull << lg;
-  if (hi - lo <= B0) return;
-  uint64_t x = (lo + B0 - 1) >> lg;
-  const uint64_t y = hi >> lg;
-  if (x >= y) return;
-  p.b0 = x << lg;
-  p.a1 = y << lg;
-  p.b1 = hi;
-  while (x < y && p.nb < (uint32_t)kMaxPlan) {
-    uint32_t j = 0;
-    while (j + 1 < v.bm_levels) {
-      const uint64_t span = 1ull << (2 * (j + 1));
-      if ((x & (span - 1)) != 0 || x + span > y) break;
-      ++j;
-    }
-    p.off[p.nb++] = v.bm_off[j] + (x >> (2 * j)) * (uint64_t)v.bm_words;
-    x += 1ull << (2 * j);
+  bool split = v.bm_levels > 0 && hi - lo > B0;
+  uint64_t x = 0, y = 0;
+  if (split) {
+    x = (lo + B0 - 1) >> lg;
+    y = hi >> lg;
+    split = x < y;
   }
+  if (lane == 0) {
+    p.a0 = lo;
+    p.b0 = split ? (x << lg) : hi;
+    p.a1 = split ? (y << lg) : 0;
+    p.b1 = split ? hi : 0;
+    p.nb = 0;
+  }
+  if (!split) return;
+  const uint32_t J = v.bm_levels;
+  const uint32_t j = lane;
+  uint64_t aj = 0, bj = 0, aj1 = 0, bj1 = 0;
+  bool valid = false;
+  if (j < J) {
+    const uint64_t s0 = 1ull << (2 * j), s1 = 1ull << (2 * (j + 1));
+    aj = (x + s0 - 1) & ~(s0 - 1);
+    bj = y & ~(s0 - 1);
+    aj1 = (x + s1 - 1) & ~(s1 - 1);
+    bj1 = y & ~(s1 - 1);
+    valid = aj < bj;
+  }
+  const uint64_t vb = __ballot(valid);
+  const uint32_t top = 63u - (uint32_t)__clzll(vb);
+  uint32_t cnt = 0;
+  if (j < top)
+    cnt = (uint32_t)(((aj1 - aj) + (bj - bj1)) >> (2 * j));
+  else if (j == top)
+    cnt = (uint32_t)((bj - aj) >> (2 * j));
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += t;
+  }
+  const uint32_t start = incl - cnt;
+  if (cnt) {
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < j; ++i) off += (v.bm_count[0] >> (2 * i)) * (uint64_t)v.bm_words;
+    const uint64_t s0 = 1ull << (2 * j);
+    uint32_t k = start;
+    if (j < top) {
+      for (uint64_t pos = aj; pos < aj1; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+      for (uint64_t pos = bj1; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+    } else {
+      for (uint64_t pos = aj; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+    }
+  }
+  if (j == top) p.nb = start + cnt;
 }
 
 __device__ __forceinline__ int64_t floor_div32(int64_t x) { return x >= 0 ? x / 32 : -((-x + 31) / 32); }
@@ -174,7 +211,7 @@ __device__ __forceinline__ void set_bit(uint32_t* win, uint32_t sym, int64_t bas
 
 // OR the symbols of BWT[a, b) into the LDS window.  The 16-B aligned middle is
 // read as uint4 with kUnroll loads in flight per thread before any LDS atomic.
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 8;
 __device__ void stream_symbols(const uint32_t* __restrict__ bwt, uint64_t a, uint64_t b, int64_t base_bit,
                                int64_t lim, uint32_t* win) {
   const uint64_t a4 = (a + 3) & ~3ull;
@@ -191,8 +228,8 @@ __device__ void stream_symbols(const uint32_t* __restrict__ bwt, uint64_t a, uin
     uint4 q[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t j = base + (uint64_t)u * kMaskThreads;
-      q[u] = (j < q1) ? src[j] : make_uint4(~0u, ~0u, ~0u, ~0u);
+      const uint64_t jq = base + (uint64_t)u * kMaskThreads;
+      q[u] = (jq < q1) ? src[jq] : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
@@ -205,68 +242,108 @@ __device__ void stream_symbols(const uint32_t* __restrict__ bwt, uint64_t a, uin
   }
 }
 
-template <bool PACKED>
-__global__ void __launch_bounds__(kMaskThreads) k_mask(DevView v, const uint64_t* __restrict__ lo_a,
-                                                      const uint64_t* __restrict__ hi_a, uint64_t m,
-                                                      uint8_t* __restrict__ mask, uint64_t ld,
-                                                      uint64_t vocab, int64_t shift, uint32_t S,
-                                                      uint32_t SW) {
+// blockIdx -> (row, slice).  Blocks b and b+8 share an XCD under round-robin
+// dispatch, so the S slices of a row are given blockIdx values congruent mod 8:
+// their redundant reads of the row's rank blocks / BWT / bitmaps share one L2.
+// Speed only; any placement is correct.
+__device__ __forceinline__ void map_block(uint32_t b, uint32_t S, uint64_t& row, uint32_t& slice) {
+  const uint32_t per = 8u * S;
+  const uint32_t r = b % per;
+  row = (uint64_t)(b / per) * 8 + (r & 7u);
+  slice = r >> 3;
+}
+
+// One workgroup = one vocab slice of one row.  With DO_LF the row's LF step
+// (or restart) is computed first by thread 0 (redundantly per slice; slice 0
+// publishes the new state), otherwise [lo_in, hi_in) is the range to mask.
+template <bool PACKED, bool DO_LF>
+__global__ void __launch_bounds__(kMaskThreads) k_decode(DevView v, const int64_t* __restrict__ tok,
+                                                        int64_t shift, int64_t reset_below,
+                                                        const uint64_t* __restrict__ lo_in,
+                                                        const uint64_t* __restrict__ hi_in,
+                                                        uint64_t* __restrict__ lo_out,
+                                                        uint64_t* __restrict__ hi_out, uint64_t m,
+                                                        uint8_t* __restrict__ mask, uint64_t ld,
+                                                        uint64_t vocab, uint32_t S, uint32_t SW) {
   __shared__ Plan plan;
+  __shared__ uint64_t s_lohi[2];
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
-  const uint64_t row = blockIdx.x / S;
-  const uint32_t slice = blockIdx.x % S;
+  uint64_t row;
+  uint32_t slice;
+  map_block(blockIdx.x, S, row, slice);
   if (row >= m) return;
   const uint64_t t0 = (uint64_t)slice * SW;
   if (t0 >= vocab) return;
   const uint64_t t1 = min(vocab, t0 + SW);
+  if (threadIdx.x == 0) {
+    uint64_t l = lo_in[row], h = hi_in[row];
+    if (DO_LF) {
+      const int64_t t = tok[row];
+      if (t < reset_below) {
+        l = 0;
+        h = v.n;
+      } else {
+        lf_step(v, t + shift, l, h);
+      }
+      if (slice == 0) {
+        lo_out[row] = l;
+        hi_out[row] = h;
+      }
+    }
+    if (h > v.n) h = v.n;
+    s_lohi[0] = l;
+    s_lohi[1] = h;
+  }
   // LDS window over symbol space, 128-bit aligned: words [w_lo, w_lo + nwin)
   const int64_t w_lo = floor_div32((int64_t)t0 + shift) & ~(int64_t)3;
   const int64_t sym_end = (int64_t)t1 + shift + 64;
   const uint32_t nwin = (uint32_t)(((sym_end - w_lo * 32 + 31) / 32 + 3) & ~3ll);
   for (uint32_t w = threadIdx.x; w < nwin; w += kMaskThreads) win[w] = 0;
-  uint64_t lo = lo_a[row];
-  uint64_t hi = hi_a[row];
-  if (hi > v.n) hi = v.n;
+  __syncthreads();
+  const uint64_t lo = s_lohi[0], hi = s_lohi[1];
   const bool live = lo < hi;
-  if (live && threadIdx.x == 0) plan_range(v, lo, hi, plan);
+  if (live && threadIdx.x < 64) plan_range_wave(v, lo, hi, plan);
   __syncthreads();
   if (live) {
     const int64_t base_bit = w_lo * 32;
     const int64_t lim = (int64_t)nwin * 32;
-    for (int part = 0; part < 2; ++part) {
-      const uint64_t a = part ? plan.a1 : plan.a0;
-      const uint64_t b = part ? plan.b1 : plan.b0;
-      if (a >= b) continue;
-      stream_symbols(v.bwt, a, b, base_bit, lim, win);
-    }
-    __syncthreads();
+    if (plan.a0 < plan.b0) stream_symbols(v.bwt, plan.a0, plan.b0, base_bit, lim, win);
+    if (plan.a1 < plan.b1) stream_symbols(v.bwt, plan.a1, plan.b1, base_bit, lim, win);
     const uint32_t nb = plan.nb;
     if (nb) {
-      uint4* win4 = reinterpret_cast<uint4*>(win);
-      for (uint32_t w4 = threadIdx.x; w4 < nwin / 4; w4 += kMaskThreads) {
-        const int64_t gw = w_lo + 4 * (int64_t)w4;
-        if (gw < 0 || gw + 4 > (int64_t)v.bm_words) continue;
-        uint4 acc = win4[w4];
-        uint32_t q = 0;
-        for (; q + 4 <= nb; q += 4) {
-          const uint4 x0 = *reinterpret_cast<const uint4*>(v.bm + plan.off[q + 0] + gw);
-          const uint4 x1 = *reinterpret_cast<const uint4*>(v.bm + plan.off[q + 1] + gw);
-          const uint4 x2 = *reinterpret_cast<const uint4*>(v.bm + plan.off[q + 2] + gw);
-          const uint4 x3 = *reinterpret_cast<const uint4*>(v.bm + plan.off[q + 3] + gw);
-          acc.x |= x0.x | x1.x | x2.x | x3.x;
-          acc.y |= x0.y | x1.y | x2.y | x3.y;
-          acc.z |= x0.z | x1.z | x2.z | x3.z;
-          acc.w |= x0.w | x1.w | x2.w | x3.w;
+      // bitmap ORs: G thread groups split the bitmaps, each thread owns one
+      // uint4 of the window; groups merge with LDS atomics.
+      const uint32_t nw4 = nwin / 4;
+      const uint32_t G = max(1u, (uint32_t)kMaskThreads / nw4);
+      const uint32_t g = threadIdx.x / nw4;
+      const uint32_t w4 = threadIdx.x % nw4;
+      const int64_t gw = w_lo + 4 * (int64_t)w4;
+      const bool in_map = gw >= 0 && gw + 4 <= (int64_t)v.bm_words;
+      for (uint32_t w4b = w4; g < G && w4b < nw4; w4b += kMaskThreads) {
+        const int64_t gwb = w_lo + 4 * (int64_t)w4b;
+        if (!(gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words)) continue;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t q = g; q < nb; q += G * 8) {
+          uint4 x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t qq = q + (uint32_t)u * G;
+            x[u] = qq < nb ? *reinterpret_cast<const uint4*>(v.bm + plan.off[qq] + gwb) : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            acc.x |= x[u].x;
+            acc.y |= x[u].y;
+            acc.z |= x[u].z;
+            acc.w |= x[u].w;
+          }
         }
-        for (; q < nb; ++q) {
-          const uint4 x0 = *reinterpret_cast<const uint4*>(v.bm + plan.off[q] + gw);
-          acc.x |= x0.x;
-          acc.y |= x0.y;
-          acc.z |= x0.z;
-          acc.w |= x0.w;
-        }
-        win4[w4] = acc;
+        if (acc.x) atomicOr(&win[4 * w4b + 0], acc.x);
+        if (acc.y) atomicOr(&win[4 * w4b + 1], acc.y);
+        if (acc.z) atomicOr(&win[4 * w4b + 2], acc.z);
+        if (acc.w) atomicOr(&win[4 * w4b + 3], acc.w);
       }
+      (void)in_map;
     }
     __syncthreads();
   }
@@ -283,8 +360,7 @@ __global__ void __launch_bounds__(kMaskThreads) k_mask(DevView v, const uint64_t
     const uint64_t cnt = min((uint64_t)32, t1 - t);
     if (cnt < 32) bits &= (1u << cnt) - 1u;
     if (PACKED) {
-      // t is a multiple of 32 -> whole uint32 word
-      reinterpret_cast<uint32_t*>(out_row)[t / 32] = bits;
+      reinterpret_cast<uint32_t*>(out_row)[t / 32] = bits;   // t is a multiple of 32
     } else {
       uint8_t* dst = out_row + t;
       if (cnt == 32 && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
@@ -472,10 +548,11 @@ static void mask_geometry(uint64_t m, uint64_t vocab, uint32_t& S, uint32_t& SW)
   S = (uint32_t)((vocab + sw - 1) / sw);
 }
 
-int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
-                uint8_t* mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
-                hipStream_t s) {
-  if (m == 0 || vocab == 0) return 0;
+static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t shift,
+                                int64_t reset_below, const uint64_t* lo_in, const uint64_t* hi_in,
+                                uint64_t* lo_out, uint64_t* hi_out, uint64_t m, uint8_t* mask,
+                                uint64_t ld, uint64_t vocab, int64_t mshift, int packed, bool do_lf,
+                                hipStream_t s) {
   if (packed && (ld % 4 != 0 || ld < 4 * ((vocab + 31) / 32) ||
                  (reinterpret_cast<uintptr_t>(mask) & 3))) {
     set_error("packed mask needs 4-byte aligned rows with ld >= 4*ceil(vocab/32)");
@@ -488,17 +565,52 @@ int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64
   }
   uint32_t S, SW;
   mask_geometry(m, vocab, S, SW);
-  const uint64_t grid = m * S;
+  const uint64_t grid = (m + 7) / 8 * 8 * S;
   if (grid > 0x7fffffffull) {
     set_error("too many rows for one launch");
     return -1;
   }
-  if (packed)
-    k_mask<true><<<(unsigned)grid, kMaskThreads, 0, s>>>(v, lo, hi, m, mask, ld, vocab, shift, S, SW);
-  else
-    k_mask<false><<<(unsigned)grid, kMaskThreads, 0, s>>>(v, lo, hi, m, mask, ld, vocab, shift, S, SW);
+  const unsigned g = (unsigned)grid;
+  (void)mshift;
+  if (do_lf) {
+    if (packed)
+      k_decode<true, true><<<g, kMaskThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out,
+                                                      m, mask, ld, vocab, S, SW);
+    else
+      k_decode<false, true><<<g, kMaskThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out,
+                                                       m, mask, ld, vocab, S, SW);
+  } else {
+    if (packed)
+      k_decode<true, false><<<g, kMaskThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out,
+                                                       m, mask, ld, vocab, S, SW);
+    else
+      k_decode<false, false><<<g, kMaskThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out,
+                                                        hi_out, m, mask, ld, vocab, S, SW);
+  }
   FM_HIP(hipGetLastError());
   return 0;
+}
+
+int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
+                uint8_t* mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
+                hipStream_t s) {
+  if (m == 0 || vocab == 0) return 0;
+  return launch_decode_kernel(v, nullptr, shift, 0, lo, hi, nullptr, nullptr, m, mask, ld, vocab, shift,
+                              packed, false, s);
+}
+
+int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
+                  const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                  uint64_t m, uint8_t* mask, uint64_t ld, uint64_t vocab, int packed, hipStream_t s) {
+  if (m == 0) return 0;
+  if (vocab == 0)   // LF only: the per-row kernel is safe in place
+    return launch_lf_step(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, s);
+  if (lo_in == lo_out || hi_in == hi_out) {
+    set_error("fused decode step: state in/out buffers must not alias (ping-pong them)");
+    return -1;
+  }
+  return launch_decode_kernel(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, mask, ld, vocab,
+                              shift, packed, true, s);
 }
 
 size_t distinct_ws_bytes(uint64_t total_cap) { return (size_t)total_cap * 40 + 256; }

@@ -44,8 +44,8 @@ SIGNATURES = {
                                          c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_allowed_mask_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64,
                                       c_uint64, c_int64, c_int, c_void_p]),
-    "fm_decode_step_batch": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_uint64,
-                                     c_void_p, c_uint64, c_uint64, c_int, c_void_p]),
+    "fm_decode_step_batch": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_int, c_void_p]),
     "fm_distinct_count_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64,
                                         c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_stats": (c_int, [c_void_p, u64p, u64p, u64p, u64p, u64p]),

@@ -286,12 +286,27 @@ class FMIndex:
         return out
 
     def decode_step(self, tokens, lo, hi, mask, vocab: int, shift: int, reset_below: int = -(1 << 63),
-                    packed: bool = False):
+                    packed: bool = False, lo_out=None, hi_out=None):
+        """Fused LF step + allowed mask (one launch).  With ``lo_out``/``hi_out``
+        the new state goes there (must not alias lo/hi); otherwise lo/hi are
+        updated in place through a temporary."""
+        import torch
+
+        inplace = lo_out is None
+        if inplace and vocab:
+            lo_out = torch.empty_like(lo)
+            hi_out = torch.empty_like(hi)
+        elif inplace:
+            lo_out, hi_out = lo, hi
         ld = mask.stride(0) * mask.element_size()
         check(lib().fm_decode_step_batch(self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below),
-                                         c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), lo.numel(),
+                                         c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
+                                         c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()), lo.numel(),
                                          c_void_p(mask.data_ptr()), ld, int(vocab), 1 if packed else 0,
                                          c_void_p(_stream_of(lo))), "decode_step")
+        if inplace and vocab:
+            lo.copy_(lo_out)
+            hi.copy_(hi_out)
         return mask
 
     def distinct_count_batch(self, lo, hi):

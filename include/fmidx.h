@@ -156,12 +156,14 @@ int fm_allowed_mask_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
                           uint8_t* d_mask, uint64_t ld, uint64_t vocab, int64_t shift,
                           int packed, void* stream);
 
-/* Fused decode step: LF step (as fm_lf_step_batch, updating d_lo/d_hi in
- * place) followed by the allowed mask of the new ranges.  A row whose token
- * is < reset_below (e.g. -1) is reset to the full range (0, n) instead of
- * stepping (a fresh sequence with an empty pattern). */
+/* Fused decode step, one launch: each row's LF step (as fm_lf_step_batch,
+ * with restart for tokens < reset_below) from (d_lo_in, d_hi_in) into
+ * (d_lo_out, d_hi_out), then the allowed mask of the new range.  The in and
+ * out state buffers must not alias (callers ping-pong them); with vocab == 0
+ * only the LF step runs and in-place update is allowed. */
 int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
-                         uint64_t* d_lo, uint64_t* d_hi, uint64_t m, uint8_t* d_mask, uint64_t ld,
+                         const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out,
+                         uint64_t* d_hi_out, uint64_t m, uint8_t* d_mask, uint64_t ld,
                          uint64_t vocab, int packed, void* stream);
 
 /* Device distinct_count for m ranges: ascending symbols + counts per row in
