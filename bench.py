@@ -344,13 +344,14 @@ def main():
     read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4) for i in range(K)])
     mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
     mask_us = float(np.median(mask_ms)) * 1e3
-    L = st["levels"]
-    # LF: two 64-B rank blocks per level per row that was live (restarts cost nothing)
+    NL = st["levels"]
+    # LF: per digit level and endpoint one 128-B rank block + one 8-B
+    # superblock count, for every row that was live (restarts cost nothing)
     prev_lo = np.concatenate([lo_hist[W - 1:W].cpu().numpy(), lo_np[:-1]])
     prev_hi = np.concatenate([hi_hist[W - 1:W].cpu().numpy(), hi_np[:-1]])
     tok_np = tokens[W:S].cpu().numpy()
     live = (prev_lo < prev_hi) & (tok_np >= 0)
-    lf_bytes = 64 * 2 * L * live.sum(1)
+    lf_bytes = (128 + 8) * 2 * NL * live.sum(1)
     lf_us = float(np.median(lf_ms)) * 1e3
     rank_gbs = float(lf_bytes.mean()) / (lf_us * 1e-6) / 1e9
     # dominant kernel = the fused k_decode (one launch per step)
@@ -383,7 +384,7 @@ def main():
             "global_batch": world * B,
             "batch_per_gpu": B,
             "vocab": V,
-            "wavelet_levels": L,
+            "wavelet_digit_levels": NL,
             "parallelism": f"replicas{world}",
             "mask": "uint8[B,V]",
         },

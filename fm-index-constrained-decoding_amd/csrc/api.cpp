@@ -681,7 +681,7 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
              uint64_t* bitmap_bytes, uint64_t* bitmap_block) {
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
-  if (levels) *levels = x.L;
+  if (levels) *levels = x.NL;
   if (wm_bytes) *wm_bytes = x.wm_bytes;
   if (bwt_bytes) *bwt_bytes = x.n * 4;
   if (bitmap_bytes) *bitmap_bytes = x.bm_bytes;

@@ -83,55 +83,93 @@ __global__ void __launch_bounds__(kThreads) k_chunk_scan(const uint64_t* __restr
   if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == kThreads - 1) *total = ex;
 }
 
-// ---- wavelet matrix ------------------------------------------------------
-// One wave per 448-symbol block: 7 ballots -> 7 payload words (lanes 1..7 store).
-__global__ void __launch_bounds__(kThreads) k_pack(const uint32_t* __restrict__ cur, uint64_t n,
-                                                  uint32_t bitpos, uint64_t* __restrict__ lvl,
-                                                  uint64_t* __restrict__ blkcnt, uint64_t nblk) {
-  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (b >= nblk) return;
-  const uint32_t lane = lane_id();
-  const uint64_t base = b * kBlockBits;
-  uint64_t mine = 0, ones = 0;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const uint64_t i = base + (uint64_t)k * 64 + lane;
-    const int bit = (i < n) ? (int)((cur[i] >> bitpos) & 1u) : 0;
-    const uint64_t word = __ballot(bit);
-    ones += (uint64_t)__popcll(word);
-    if (lane == (uint32_t)(k + 1)) mine = word;
-  }
-  if (lane >= 1 && lane <= 7) lvl[b * kBlockWords + lane] = mine;
-  if (lane == 0) blkcnt[b] = ones;
+// ---- 16-ary wavelet matrix ------------------------------------------------
+// One wave per 192-digit rank block (3 chunks of 64 lanes).
+
+__device__ __forceinline__ uint32_t digit_at(const uint32_t* __restrict__ cur, uint64_t i, uint64_t n,
+                                             uint32_t shift) {
+  return i < n ? ((cur[i] >> shift) & 15u) : 16u;   // 16 = past the end
 }
 
-// Stable partition of the level (zeros first) and the block's absolute count.
-__global__ void __launch_bounds__(kThreads) k_partition(const uint32_t* __restrict__ cur,
-                                                       uint32_t* __restrict__ nxt, uint64_t n,
-                                                       uint32_t bitpos, uint64_t* __restrict__ lvl,
-                                                       const uint64_t* __restrict__ cum,
-                                                       uint64_t zeros, uint64_t nblk) {
+// per-block digit histogram, digit-major: hist[d * nblk + b]
+__global__ void __launch_bounds__(kThreads) k_hist16(const uint32_t* __restrict__ cur, uint64_t n,
+                                                    uint32_t shift, uint64_t* __restrict__ hist,
+                                                    uint64_t nblk) {
   const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (b >= nblk) return;
   const uint32_t lane = lane_id();
-  const uint64_t base = b * kBlockBits;
-  uint64_t ones = cum[b];
-  if (lane == 0) lvl[b * kBlockWords] = ones;
-  const uint64_t below_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const uint64_t i = base + (uint64_t)k * 64 + lane;
+  for (int c = 0; c < 3; ++c) {
+    const uint32_t d = digit_at(cur, b * kBlkDigits + (uint64_t)c * 64 + lane, n, shift);
+#pragma unroll
+    for (uint32_t dd = 0; dd < 16; ++dd) {
+      const uint32_t k = (uint32_t)__popcll(__ballot(d == dd));
+      if (lane == dd) mine += k;
+    }
+  }
+  if (lane < 16) hist[(uint64_t)lane * nblk + b] = mine;
+}
+
+// Write the rank block (header + packed digits), the superblock counts, and
+// stable-partition the level by digit: dest = base[d][b] + rank within block.
+__global__ void __launch_bounds__(kThreads) k_level16(const uint32_t* __restrict__ cur,
+                                                     uint32_t* __restrict__ nxt, uint64_t n,
+                                                     uint32_t shift, const uint64_t* __restrict__ base,
+                                                     uint64_t nblk, uint4* __restrict__ blocks,
+                                                     uint64_t* __restrict__ sbc, uint64_t nsb) {
+  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (b >= nblk) return;
+  const uint32_t lane = lane_id();
+  uint8_t* blk = reinterpret_cast<uint8_t*>(blocks + b * kBlkU4);
+  const uint64_t b_sb = (b / kSbBlocks) * kSbBlocks;
+  // header + superblock counts: lane d handles digit d
+  uint64_t my_base = 0;
+  if (lane < 16) {
+    my_base = base[(uint64_t)lane * nblk + b];
+    const uint64_t sb_start = base[(uint64_t)lane * nblk + b_sb];
+    reinterpret_cast<uint16_t*>(blk)[lane] = (uint16_t)(my_base - sb_start);
+    if (b == b_sb) sbc[(b / kSbBlocks) * kRadix + lane] = sb_start - base[(uint64_t)lane * nblk];
+  }
+  // payload: lane j < 48 packs digits 4j..4j+3 into two bytes
+  if (lane < 48) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t d = digit_at(cur, b * kBlkDigits + 4 * lane + t, n, shift);
+      v |= (d & 15u) << (4 * t);
+    }
+    reinterpret_cast<uint16_t*>(blk + 32)[lane] = (uint16_t)v;
+  }
+  // partition
+  uint32_t run = 0;   // lane d: digits d seen so far in this block
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint64_t i = b * kBlkDigits + (uint64_t)c * 64 + lane;
     const bool valid = i < n;
     const uint32_t v = valid ? cur[i] : 0u;
-    const int bit = valid ? (int)((v >> bitpos) & 1u) : 0;
-    const uint64_t word = __ballot(bit);
-    const uint64_t mine = ones + (uint64_t)__popcll(word & below_mask);
-    if (valid) {
-      const uint64_t dest = bit ? zeros + mine : i - mine;
-      nxt[dest] = v;
+    const uint32_t d = valid ? ((v >> shift) & 15u) : 16u;
+    uint64_t same = __ballot(valid);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint64_t bt = __ballot((d >> t) & 1u);
+      same &= ((d >> t) & 1u) ? bt : ~bt;
     }
-    ones += (uint64_t)__popcll(word);
+    const uint32_t within = (uint32_t)__popcll(same & below);
+    const uint64_t bd = __shfl(my_base, (int)(d & 15u), 64);
+    const uint32_t rd = (uint32_t)__shfl((int)run, (int)(d & 15u), 64);
+    if (valid) nxt[bd + rd + within] = v;
+#pragma unroll
+    for (uint32_t dd = 0; dd < 16; ++dd) {
+      const uint32_t k = (uint32_t)__popcll(__ballot(d == dd));
+      if (lane == dd) run += k;
+    }
   }
+}
+
+__global__ void k_gather_z(const uint64_t* __restrict__ base, uint64_t nblk, uint64_t* __restrict__ z) {
+  if (threadIdx.x < 16) z[threadIdx.x] = base[(uint64_t)threadIdx.x * nblk];
 }
 
 __global__ void k_max_sym(const uint32_t* __restrict__ a, uint64_t n, uint32_t* __restrict__ out) {
@@ -292,32 +330,37 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     return -1;
   }
   const uint64_t K = 1ull << L;
-  const uint64_t nblk = n / kBlockBits + 1;
+  const uint32_t NL = (L + 3) / 4;
+  const uint64_t nblk = n / kBlkDigits + 1;
+  const uint64_t nsb = nblk / kSbBlocks + 1;
 
-  // -- wavelet matrix
-  uint64_t* wm = nullptr;
+  // -- 16-ary wavelet matrix
+  uint4* wm = nullptr;
+  uint64_t* sbc = nullptr;
+  uint64_t* Zd = nullptr;
   uint32_t *cur = nullptr, *nxt = nullptr;
-  uint64_t *blkcnt = nullptr, *cum = nullptr, *d_tot = nullptr;
-  if (dmalloc(&wm, (size_t)L * nblk * kBlockWords) || dmalloc(&cur, n) || dmalloc(&nxt, n) ||
-      dmalloc(&blkcnt, nblk) || dmalloc(&cum, nblk) || dmalloc(&d_tot, 1))
+  uint64_t *hist = nullptr, *base = nullptr;
+  if (dmalloc(&wm, (size_t)NL * nblk * kBlkU4) || dmalloc(&sbc, (size_t)NL * nsb * kRadix) ||
+      dmalloc(&Zd, (size_t)NL * kRadix) || dmalloc(&cur, n) || dmalloc(&nxt, n) ||
+      dmalloc(&hist, nblk * kRadix) || dmalloc(&base, nblk * kRadix))
     return -1;
+  FM_HIP(hipMemsetAsync(sbc, 0, (size_t)NL * nsb * kRadix * 8, s));
   FM_HIP(hipMemcpyAsync(cur, d_bwt, n * 4, hipMemcpyDeviceToDevice, s));
   const unsigned gblk = (unsigned)((nblk + kWaves - 1) / kWaves);
-  uint64_t zeros[kMaxLevels] = {0};
-  for (uint32_t lev = 0; lev < L; ++lev) {
-    const uint32_t bitpos = L - 1 - lev;
-    uint64_t* lvl = wm + (uint64_t)lev * nblk * kBlockWords;
-    k_pack<<<gblk, kThreads, 0, s>>>(cur, n, bitpos, lvl, blkcnt, nblk);
+  for (uint32_t lev = 0; lev < NL; ++lev) {
+    const uint32_t shift = 4 * (NL - 1 - lev);
+    k_hist16<<<gblk, kThreads, 0, s>>>(cur, n, shift, hist, nblk);
     FM_HIP(hipGetLastError());
-    if (exclusive_scan_u64(blkcnt, cum, nblk, s, d_tot)) return -1;
-    uint64_t ones = 0;
-    FM_HIP(hipMemcpyAsync(&ones, d_tot, 8, hipMemcpyDeviceToHost, s));
-    FM_HIP(hipStreamSynchronize(s));
-    zeros[lev] = n - ones;
-    k_partition<<<gblk, kThreads, 0, s>>>(cur, nxt, n, bitpos, lvl, cum, zeros[lev], nblk);
+    if (exclusive_scan_u64(hist, base, nblk * kRadix, s, nullptr)) return -1;
+    k_gather_z<<<1, 64, 0, s>>>(base, nblk, Zd + lev * kRadix);
+    k_level16<<<gblk, kThreads, 0, s>>>(cur, nxt, n, shift, base, nblk, wm + (uint64_t)lev * nblk * kBlkU4,
+                                        sbc + (uint64_t)lev * nsb * kRadix, nsb);
     FM_HIP(hipGetLastError());
     std::swap(cur, nxt);
   }
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(hist));
+  FM_HIP(hipFree(base));
   // -- C / D from the final order
   uint64_t *S = nullptr, *E = nullptr, *cnt = nullptr, *C = nullptr;
   int64_t* D = nullptr;
@@ -343,9 +386,6 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   FM_HIP(hipFree(d_sigma));
   FM_HIP(hipFree(cur));
   FM_HIP(hipFree(nxt));
-  FM_HIP(hipFree(blkcnt));
-  FM_HIP(hipFree(cum));
-  FM_HIP(hipFree(d_tot));
 
   // -- range bitmaps
   const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", 13);
@@ -376,19 +416,25 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
 
   h->n = n;
   h->L = L;
+  h->NL = NL;
   h->max_sym = max_sym;
   h->sigma = sigma;
   h->wm = wm;
+  h->sb = sbc;
+  h->Z = Zd;
   h->C = C;
   h->D = D;
   h->bm = bm;
-  h->wm_bytes = (uint64_t)L * nblk * 64;
+  h->wm_bytes = (uint64_t)NL * (nblk * 128 + nsb * kRadix * 8);
   h->bm_bytes = total_words * 4;
   DevView& v = h->view;
   v = DevView{};
   v.n = n;
   v.nblk = nblk;
+  v.nsb = nsb;
   v.wm = wm;
+  v.sb = sbc;
+  v.Z = Zd;
   v.D = D;
   v.C = C;
   v.bwt = d_bwt;
@@ -397,8 +443,8 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     v.bm_off[j] = bm_off[j];
     v.bm_count[j] = bm_count[j];
   }
-  for (uint32_t lev = 0; lev < L; ++lev) v.zeros[lev] = zeros[lev];
   v.L = L;
+  v.NL = NL;
   v.max_sym = max_sym;
   v.bm_words = words;
   v.bm_levels = bm_levels;

@@ -3,15 +3,21 @@
 //
 // Layout (all resident in HBM, built once per index):
 //
-//   wm      wavelet matrix over the BWT, L levels (L = bit width of the largest
-//           symbol; 17 for a 128k vocabulary + SHIFT).  Level l is an array of
-//           64-byte rank blocks: word 0 = number of 1 bits before the block
-//           (absolute, uint64), words 1..7 = 448 payload bits.  One rank costs
-//           exactly one 64-B line.  The MSB of the symbol is level 0.
-//   zeros   number of 0 bits of every level (kernel-argument array).
+//   wm      16-ary wavelet matrix over the BWT: NL = ceil(L/4) digit levels
+//           (L = bit width of the largest symbol; 17 -> 5 levels for a 128k
+//           vocabulary + SHIFT), level 0 = the most significant 4-bit digit.
+//           Level l is an array of 128-byte rank blocks: 16 x uint16 counts
+//           of each digit before the block (relative to its superblock) + 96
+//           bytes = 192 packed 4-bit digits.  rank_d(i) = one block line + one
+//           superblock count; an LF step is NL dependent round trips instead
+//           of the 17 of a binary wavelet tree/matrix.
+//   sb      per level and superblock (341 blocks = 65472 digits) the absolute
+//           count of each digit before it (16 x uint64).
+//   Z       per level, Z[l][d] = number of digits < d in that level (the start
+//           of digit d's partition in the next level).
 //   D       D[c] = C[c] - S[c] as int64, where C[c] is the FM-index C array and
 //           S[c] the start of symbol c in the wavelet matrix's final order, so
-//           LF(i, c) = desc_c(i) + D[c] (desc = the L-level descent).
+//           LF(i, c) = desc_c(i) + D[c] (desc = the NL-level descent).
 //   C       C[0 .. 2^L] (C[c+1]-C[c] = occurrences of c).
 //   bwt     the BWT as plain uint32 symbols (streamed for narrow ranges).
 //   bm      range-presence bitmaps: level j holds one bitmap of W bits for each
@@ -26,95 +32,113 @@
 
 namespace fmidx {
 
-constexpr int kMaxLevels = 26;         // 2^26 symbol table; token ids + 10 need 18 at most
-constexpr int kBlockBits = 448;        // payload bits per 64-B rank block
-constexpr int kBlockWords = 8;         // uint64 words per rank block
+constexpr int kMaxSymBits = 26;        // 2^26 symbol table; token ids + 10 need 18 at most
+constexpr int kMaxLevels = kMaxSymBits;
+constexpr int kRadix = 16;             // 4-bit digits
+constexpr int kMaxDigitLevels = (kMaxSymBits + 3) / 4;
+constexpr int kBlkDigits = 192;        // digits per 128-B rank block
+constexpr int kBlkU4 = 8;              // uint4 per rank block
+constexpr int kSbBlocks = 341;         // blocks per superblock (65472 digits < 2^16)
 constexpr int kMaxBmLevels = 24;
 
 // Everything a kernel needs, passed by value as a kernel argument.
 struct DevView {
   uint64_t n;                 // BWT length (corpus tokens + 1 sentinel)
-  uint64_t nblk;              // rank blocks per level = n / 448 + 1
-  const uint64_t* wm;         // L * nblk * 8 words
+  uint64_t nblk;              // rank blocks per level = n / 192 + 1
+  uint64_t nsb;               // superblocks per level = nblk / 341 + 1
+  const uint4* wm;            // NL * nblk * 8 uint4
+  const uint64_t* sb;         // NL * nsb * 16
+  const uint64_t* Z;          // NL * 16
   const int64_t* D;           // [2^L]
   const uint64_t* C;          // [2^L + 1]
   const uint32_t* bwt;        // [n]
   const uint32_t* bm;         // bitmap hierarchy
   uint64_t bm_off[kMaxBmLevels];   // word offset of each bitmap level
   uint64_t bm_count[kMaxBmLevels]; // bitmaps per level
-  uint64_t zeros[kMaxLevels];
-  uint32_t L;                 // wavelet levels
+  uint32_t L;                 // symbol bits
+  uint32_t NL;                // digit levels
   uint32_t max_sym;           // largest symbol value present
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
-  uint32_t pad_;
 };
 
 // ---------------------------------------------------------------------------
-// rank1 inside one 64-byte block: ones before bit ``off`` (off < 448).
-__device__ __forceinline__ uint64_t block_rank(const uint64_t* __restrict__ line, uint32_t off) {
-  const uint4* p = reinterpret_cast<const uint4*>(line);
-  const uint4 a = p[0];
-  const uint4 b = p[1];
-  const uint4 c = p[2];
-  const uint4 d = p[3];
-  uint64_t w[8];
-  w[0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
-  w[1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
-  w[2] = (uint64_t)b.x | ((uint64_t)b.y << 32);
-  w[3] = (uint64_t)b.z | ((uint64_t)b.w << 32);
-  w[4] = (uint64_t)c.x | ((uint64_t)c.y << 32);
-  w[5] = (uint64_t)c.z | ((uint64_t)c.w << 32);
-  w[6] = (uint64_t)d.x | ((uint64_t)d.y << 32);
-  w[7] = (uint64_t)d.z | ((uint64_t)d.w << 32);
-  const uint32_t q = off >> 6;
-  const uint32_t r = off & 63u;
-  uint64_t cnt = w[0];
-#pragma unroll
-  for (uint32_t j = 0; j < 7; ++j) {
-    const uint64_t word = w[1 + j];
-    const uint64_t m = (j < q) ? ~0ull : ((j == q) ? ((r == 0) ? 0ull : (~0ull >> (64 - r))) : 0ull);
-    cnt += (uint64_t)__popcll(word & m);
+// occurrences of digit d among the first m (<= 16) nibbles of w
+__device__ __forceinline__ uint32_t nib_count(uint64_t w, uint32_t d, uint32_t m) {
+  const uint64_t ones = 0x1111111111111111ull;
+  const uint64_t x = w ^ (ones * d);
+  const uint64_t nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & ones;
+  const uint64_t mk = (m >= 16) ? ~0ull : ((1ull << (4 * m)) - 1);
+  return (uint32_t)__popcll(~nz & ones & mk);
+}
+
+__device__ __forceinline__ uint32_t u4_get(const uint4& x, uint32_t i) {
+  return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
+}
+
+__device__ __forceinline__ uint32_t digit_of(uint32_t c, uint32_t NL, uint32_t lev) {
+  return (c >> (4 * (NL - 1 - lev))) & 15u;
+}
+
+// Contribution of one uint4 (slot q of a rank block) to rank_d(k-th digit):
+// slots 0,1 hold the 16 uint16 header counts, slots 2..7 32 digits each.
+__device__ __forceinline__ uint32_t block_part(const uint4& x, uint32_t q, uint32_t d, uint32_t k) {
+  if (q < 2) {
+    if ((d >> 3) != q) return 0;
+    const uint32_t w = u4_get(x, (d & 7) >> 1);
+    return (d & 1) ? (w >> 16) : (w & 0xFFFFu);
   }
+  const uint32_t s = 32 * (q - 2);
+  const uint32_t m = k > s ? min(32u, k - s) : 0u;
+  const uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32);
+  const uint64_t hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  return nib_count(lo, d, min(16u, m)) + nib_count(hi, d, m > 16 ? m - 16 : 0u);
+}
+
+__device__ __forceinline__ const uint4* rank_block(const DevView& v, uint32_t lev, uint64_t b) {
+  return v.wm + ((uint64_t)lev * v.nblk + b) * kBlkU4;
+}
+
+__device__ __forceinline__ const uint64_t* sb_row(const DevView& v, uint32_t lev, uint64_t b) {
+  return v.sb + ((uint64_t)lev * v.nsb + b / kSbBlocks) * kRadix;
+}
+
+// rank_d(i) at level lev by one thread (0 <= i <= n).
+__device__ __forceinline__ uint64_t rank16(const DevView& v, uint32_t lev, uint64_t i, uint32_t d) {
+  const uint64_t b = i / kBlkDigits;
+  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
+  const uint4* blk = rank_block(v, lev, b);
+  uint4 x[kBlkU4];
+#pragma unroll
+  for (int q = 0; q < kBlkU4; ++q) x[q] = blk[q];
+  uint64_t cnt = sb_row(v, lev, b)[d];
+#pragma unroll
+  for (uint32_t q = 0; q < kBlkU4; ++q) cnt += block_part(x[q], q, d, k);
   return cnt;
 }
 
-__device__ __forceinline__ const uint64_t* level_base(const DevView& v, uint32_t lev) {
-  return v.wm + (uint64_t)lev * v.nblk * kBlockWords;
-}
-
-// ones in level ``lev`` before position i (0 <= i <= n)
-__device__ __forceinline__ uint64_t rank1(const DevView& v, uint32_t lev, uint64_t i) {
-  const uint64_t b = i / kBlockBits;
-  const uint32_t off = (uint32_t)(i - b * kBlockBits);
-  return block_rank(level_base(v, lev) + b * kBlockWords, off);
-}
-
-// L-level descent of the half-open range [l, r) along symbol c.  On return
-// [l, r) is the run of c's occurrences inside the wavelet matrix's final
-// order; r - l = occurrences of c in BWT[l0, r0).  Stops early when empty.
-__device__ __forceinline__ void wm_descend(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
-  for (uint32_t lev = 0; lev < v.L; ++lev) {
-    const uint64_t bl = l / kBlockBits;
-    const uint64_t br = r / kBlockBits;
-    const uint64_t* base = level_base(v, lev);
-    const uint64_t r1l = block_rank(base + bl * kBlockWords, (uint32_t)(l - bl * kBlockBits));
-    const uint64_t r1r = block_rank(base + br * kBlockWords, (uint32_t)(r - br * kBlockBits));
-    if ((c >> (v.L - 1 - lev)) & 1u) {
-      l = v.zeros[lev] + r1l;
-      r = v.zeros[lev] + r1r;
-    } else {
-      l -= r1l;
-      r -= r1r;
-    }
-    if (l >= r) return;
-  }
+// rank_d(i) by an aligned group of 8 lanes (q = lane & 7): one uint4 each,
+// summed with three xor-shuffles.  Every lane of the group gets the result.
+__device__ __forceinline__ uint64_t rank16_coop(const DevView& v, uint32_t lev, uint64_t i, uint32_t d,
+                                                uint32_t q) {
+  const uint64_t b = i / kBlkDigits;
+  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
+  const uint4 x = rank_block(v, lev, b)[q];
+  const uint64_t base = sb_row(v, lev, b)[d];
+  uint32_t part = block_part(x, q, d, k);
+  part += __shfl_xor(part, 1, 64);
+  part += __shfl_xor(part, 2, 64);
+  part += __shfl_xor(part, 4, 64);
+  return base + part;
 }
 
 // One reference backward_search_step on a half-open state (fm_index.cpp:67-97
-// as driven by index.py:110): (0,0) = empty in and out.
-__device__ __forceinline__ void lf_step(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
+// as driven by index.py:110), computed by an aligned group of 16 lanes:
+// lanes 0-7 rank the low end, lanes 8-15 the high end, NL dependent rounds.
+// (0,0) = empty in and out.  All 16 lanes receive the result.
+__device__ __forceinline__ void lf_step16(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
+                                          uint32_t lane16) {
   if (hi > v.n) hi = v.n;                    // high clamp (fm_index.cpp:74-76)
   if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {  // low > high / unknown symbol
     lo = 0;
@@ -122,16 +146,38 @@ __device__ __forceinline__ void lf_step(const DevView& v, int64_t sym, uint64_t&
     return;
   }
   const uint32_t c = (uint32_t)sym;
+  const uint32_t q = lane16 & 7u;
+  const bool side = lane16 >= 8;
   uint64_t l = lo, r = hi;
-  wm_descend(v, c, l, r);
+  for (uint32_t lev = 0; lev < v.NL; ++lev) {
+    const uint32_t d = digit_of(c, v.NL, lev);
+    const uint64_t z = v.Z[lev * kRadix + d];
+    const uint64_t mine = rank16_coop(v, lev, side ? r : l, d, q);
+    const uint64_t other = __shfl_xor(mine, 8, 64);
+    l = z + (side ? other : mine);
+    r = z + (side ? mine : other);
+    if (l >= r) break;
+  }
   if (l >= r) {
     lo = 0;
     hi = 0;
     return;
   }
-  const int64_t d = v.D[c];
-  lo = (uint64_t)((int64_t)l + d);
-  hi = (uint64_t)((int64_t)r + d);
+  const int64_t dd = v.D[c];
+  lo = (uint64_t)((int64_t)l + dd);
+  hi = (uint64_t)((int64_t)r + dd);
+}
+
+// Full NL-level descent of both endpoints by one thread (no early exit).
+__device__ __forceinline__ void descend_full(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
+  for (uint32_t lev = 0; lev < v.NL; ++lev) {
+    const uint32_t d = digit_of(c, v.NL, lev);
+    const uint64_t z = v.Z[lev * kRadix + d];
+    const uint64_t rl = rank16(v, lev, l, d);
+    const uint64_t rr = rank16(v, lev, r, d);
+    l = z + rl;
+    r = z + rr;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -144,8 +190,11 @@ struct Index {
   uint64_t sigma = 0;            // distinct symbols in the BWT
   uint64_t max_sym = 0;
   uint32_t L = 0;
+  uint32_t NL = 0;
   // device allocations
-  uint64_t* wm = nullptr;
+  uint4* wm = nullptr;
+  uint64_t* sb = nullptr;
+  uint64_t* Z = nullptr;
   int64_t* D = nullptr;
   uint64_t* C = nullptr;
   uint32_t* bwt = nullptr;

@@ -24,7 +24,7 @@ namespace fmidx {
 
 namespace {
 
-constexpr int kLfThreads = 64;
+constexpr int kLfThreads = 256;
 constexpr int kMaskThreads = 256;
 constexpr int kMaxPlan = 160;           // >= 6 * kMaxBmLevels
 constexpr uint32_t kMaxSliceTokens = 32768;
@@ -33,11 +33,13 @@ constexpr int kWinWords = kMaxSliceTokens / 32 + 12;
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
 // ------------------------------------------------------------------ LF
+// 16 lanes per row (kLfThreads / 16 rows per block).
 __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __restrict__ tok,
                                                   int64_t shift, int64_t reset_below,
                                                   const uint64_t* lo_in, const uint64_t* hi_in,
                                                   uint64_t* lo_out, uint64_t* hi_out, uint64_t m) {
-  const uint64_t i = (uint64_t)blockIdx.x * kLfThreads + threadIdx.x;
+  const uint64_t i = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 4;
+  const uint32_t lane16 = threadIdx.x & 15u;
   if (i >= m) return;
   const int64_t t = tok[i];
   uint64_t l = lo_in[i], h = hi_in[i];
@@ -45,10 +47,12 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
     l = 0;
     h = v.n;
   } else {
-    lf_step(v, t + shift, l, h);
+    lf_step16(v, t + shift, l, h, lane16);
   }
-  lo_out[i] = l;
-  hi_out[i] = h;
+  if (lane16 == 0) {
+    lo_out[i] = l;
+    hi_out[i] = h;
+  }
 }
 
 __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t* __restrict__ tok,
@@ -56,31 +60,19 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
                                                       int64_t shift, const uint64_t* lo_in,
                                                       const uint64_t* hi_in, uint64_t* lo_out,
                                                       uint64_t* hi_out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kLfThreads + threadIdx.x;
+  const uint64_t i = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 4;
+  const uint32_t lane16 = threadIdx.x & 15u;
   if (i >= m) return;
   uint64_t l = lo_in ? lo_in[i] : 0;
   uint64_t h = hi_in ? hi_in[i] : v.n;
   const int64_t a = off[i], b = off[i + 1];
   for (int64_t j = a; j < b; ++j) {
-    lf_step(v, tok[j] + shift, l, h);
+    lf_step16(v, tok[j] + shift, l, h, lane16);
     if (l == 0 && h == 0) break;       // index.py:111-112
   }
-  lo_out[i] = l;
-  hi_out[i] = h;
-}
-
-// Full L-level descent of both endpoints (no early exit), positions <= n.
-__device__ void descend_full(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
-  for (uint32_t lev = 0; lev < v.L; ++lev) {
-    const uint64_t r1l = rank1(v, lev, l);
-    const uint64_t r1r = rank1(v, lev, r);
-    if ((c >> (v.L - 1 - lev)) & 1u) {
-      l = v.zeros[lev] + r1l;
-      r = v.zeros[lev] + r1r;
-    } else {
-      l -= r1l;
-      r -= r1r;
-    }
+  if (lane16 == 0) {
+    lo_out[i] = l;
+    hi_out[i] = h;
   }
 }
 
@@ -275,7 +267,7 @@ __global__ void __launch_bounds__(kMaskThreads) k_decode(DevView v, const int64_
   const uint64_t t0 = (uint64_t)slice * SW;
   if (t0 >= vocab) return;
   const uint64_t t1 = min(vocab, t0 + SW);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 16) {
     uint64_t l = lo_in[row], h = hi_in[row];
     if (DO_LF) {
       const int64_t t = tok[row];
@@ -283,16 +275,18 @@ __global__ void __launch_bounds__(kMaskThreads) k_decode(DevView v, const int64_
         l = 0;
         h = v.n;
       } else {
-        lf_step(v, t + shift, l, h);
+        lf_step16(v, t + shift, l, h, threadIdx.x);
       }
-      if (slice == 0) {
+      if (slice == 0 && threadIdx.x == 0) {
         lo_out[row] = l;
         hi_out[row] = h;
       }
     }
     if (h > v.n) h = v.n;
-    s_lohi[0] = l;
-    s_lohi[1] = h;
+    if (threadIdx.x == 0) {
+      s_lohi[0] = l;
+      s_lohi[1] = h;
+    }
   }
   // LDS window over symbol space, 128-bit aligned: words [w_lo, w_lo + nwin)
   const int64_t w_lo = floor_div32((int64_t)t0 + shift) & ~(int64_t)3;
@@ -383,13 +377,56 @@ struct Frontier {
   uint32_t* pre[2];
 };
 
+// per-digit counts before position i at level lev (16 values, one thread)
+__device__ __forceinline__ void digit_counts(const DevView& v, uint32_t lev, uint64_t i, uint64_t* out) {
+  const uint64_t b = i / kBlkDigits;
+  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
+  const uint4* blk = rank_block(v, lev, b);
+  const uint64_t* sbr = sb_row(v, lev, b);
+  uint4 x[kBlkU4];
+#pragma unroll
+  for (int q = 0; q < kBlkU4; ++q) x[q] = blk[q];
+#pragma unroll
+  for (uint32_t d = 0; d < 16; ++d) {
+    uint64_t c = sbr[d];
+#pragma unroll
+    for (uint32_t q = 0; q < kBlkU4; ++q) c += block_part(x[q], q, d, k);
+    out[d] = c;
+  }
+}
+
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[4]*/, uint32_t& total) {
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) lds[wave] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t t = lds[w];
+    if ((uint32_t)w < wave) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+
+// interval_symbols with counts: level-synchronous BFS over the 16-ary
+// wavelet matrix, one workgroup per row; children are appended in digit
+// order so the final frontier is in ascending symbol order.
 __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __restrict__ lo_a,
                                                  const uint64_t* __restrict__ hi_a, uint64_t m,
                                                  const uint64_t* __restrict__ cap_off,
                                                  uint64_t* __restrict__ syms,
                                                  uint64_t* __restrict__ counts,
                                                  uint64_t* __restrict__ k_out, Frontier fr) {
-  __shared__ uint32_t wave_cnt[4];
+  __shared__ uint32_t wave_tot[4];
   const uint64_t row = blockIdx.x;
   if (row >= m) return;
   uint64_t lo = lo_a[row], hi = hi_a[row];
@@ -415,57 +452,41 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     apre[0] = 0;
   }
   __syncthreads();
-  const uint32_t lane = lane_id();
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint64_t fc = 1;
   bool overflow = false;
-  for (uint32_t lev = 0; lev < v.L; ++lev) {
-    const uint64_t z = v.zeros[lev];
+  for (uint32_t lev = 0; lev < v.NL; ++lev) {
+    const uint64_t* Z = v.Z + lev * kRadix;
     uint64_t out = 0;
     for (uint64_t t0 = 0; t0 < fc; t0 += 256) {
       const uint64_t i = t0 + threadIdx.x;
-      bool h0 = false, h1 = false;
-      uint64_t z0 = 0, z1 = 0, o0 = 0, o1 = 0;
-      uint32_t p = 0;
+      uint64_t cl[16], ch[16];
+      uint32_t p = 0, nchild = 0;
       if (i < fc) {
-        const uint64_t l = alo[i], h = ahi[i];
         p = apre[i];
-        const uint64_t r1l = rank1(v, lev, l);
-        const uint64_t r1h = rank1(v, lev, h);
-        z0 = l - r1l;
-        z1 = h - r1h;
-        o0 = z + r1l;
-        o1 = z + r1h;
-        h0 = z0 < z1;
-        h1 = o0 < o1;
-      }
-      const uint64_t b0 = __ballot(h0);
-      const uint64_t b1 = __ballot(h1);
-      const uint32_t pos_w = __popcll(b0 & below) + __popcll(b1 & below);
-      if (lane == 0) wave_cnt[wave] = __popcll(b0) + __popcll(b1);
-      __syncthreads();
-      uint32_t wbase = 0, tot = 0;
+        digit_counts(v, lev, alo[i], cl);
+        digit_counts(v, lev, ahi[i], ch);
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint32_t c = wave_cnt[w];
-        if ((uint32_t)w < wave) wbase += c;
-        tot += c;
+        for (int d = 0; d < 16; ++d) nchild += (ch[d] > cl[d]) ? 1u : 0u;
       }
-      const uint64_t pos = out + wbase + pos_w;
-      if (h0 && pos < cap) {
-        blo[pos] = z0;
-        bhi[pos] = z1;
-        bpre[pos] = p << 1;
-      }
-      if (h1 && pos + h0 < cap) {
-        blo[pos + h0] = o0;
-        bhi[pos + h0] = o1;
-        bpre[pos + h0] = (p << 1) | 1u;
+      uint32_t tot;
+      const uint64_t pos0 = out + block_scan_u32(nchild, wave_tot, tot);
+      if (nchild) {
+        uint64_t pos = pos0;
+#pragma unroll
+        for (uint32_t d = 0; d < 16; ++d) {
+          if (ch[d] > cl[d]) {
+            if (pos < cap) {
+              blo[pos] = Z[d] + cl[d];
+              bhi[pos] = Z[d] + ch[d];
+              bpre[pos] = (p << 4) | d;
+            }
+            ++pos;
+          }
+        }
       }
       out += tot;
-      __syncthreads();
     }
+    __syncthreads();
     if (out > cap) {
       overflow = true;
       break;
@@ -501,7 +522,7 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s) {
   if (m == 0) return 0;
-  const unsigned g = (unsigned)((m + kLfThreads - 1) / kLfThreads);
+  const unsigned g = (unsigned)((m * 16 + kLfThreads - 1) / kLfThreads);
   k_lf<<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   FM_HIP(hipGetLastError());
   return 0;
@@ -511,7 +532,7 @@ int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,
                   uint64_t* hi_out, hipStream_t s) {
   if (m == 0) return 0;
-  const unsigned g = (unsigned)((m + kLfThreads - 1) / kLfThreads);
+  const unsigned g = (unsigned)((m * 16 + kLfThreads - 1) / kLfThreads);
   k_search<<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   FM_HIP(hipGetLastError());
   return 0;

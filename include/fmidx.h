@@ -177,7 +177,8 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
 
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
-/* Wavelet levels L, bytes of each device structure. */
+/* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip
+ * each per LF step), bytes of each device structure. */
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
              uint64_t* bitmap_bytes, uint64_t* bitmap_block);
 
