@@ -115,14 +115,18 @@ def make_trace(fm, text, bwt, B: int, V: int, S: int, seed: int, dev):
     return tokens, init, lo_hist, hi_hist
 
 
-def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int):
+def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int,
+               follow=None):
     """Bytes the mask algorithm must read per row: streamed BWT symbols (4 B)
-    + whole range bitmaps (mirrors plan_range in query.hip)."""
+    + whole range bitmaps (mirrors plan_range_wave in query.hip)."""
     B0 = 1 << b0_log2
     out = np.zeros(lo.size, dtype=np.int64)
     for i, (l, h) in enumerate(zip(lo.tolist(), hi.tolist())):
         h = min(h, n)
         if l >= h:
+            continue
+        if (l == 0 and h == n) or (follow is not None and follow[i]):
+            out[i] = bm_bytes_each            # one precomputed bitmap (full range / follow set)
             continue
         if bm_levels == 0 or h - l <= B0:
             out[i] = 4 * (h - l)
@@ -219,6 +223,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=600)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dump-trace", default="", help="write the timed trace states to this .npz")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -328,6 +333,9 @@ def main():
         step_ms = float(t.item())
     value = world * B * K / (step_ms * K / 1e3)
 
+    if args.dump_trace and rank == 0:
+        np.savez_compressed(args.dump_trace, tokens=tokens[:S].cpu().numpy(), lo=lo_hist[:S].cpu().numpy(),
+                            hi=hi_hist[:S].cpu().numpy(), n=n, warmup=W)
     # ---- roofline accounting for the dominant (mask) kernel
     lo_np = lo_hist[W:S].cpu().numpy()
     hi_np = hi_hist[W:S].cpu().numpy()
@@ -341,15 +349,17 @@ def main():
     while c > 0:
         bm_levels += 1
         c >>= 2
-    read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4) for i in range(K)])
+    prev_lo = np.concatenate([lo_hist[W - 1:W].cpu().numpy(), lo_np[:-1]])
+    prev_hi = np.concatenate([hi_hist[W - 1:W].cpu().numpy(), hi_np[:-1]])
+    tok_np = tokens[W:S].cpu().numpy()
+    follow = (prev_lo == 0) & (prev_hi >= n) & (tok_np >= 0) & (st.get("follow_bytes", 0) > 0)
+    read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4, follow[i])
+                           for i in range(K)])
     mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
     mask_us = float(np.median(mask_ms)) * 1e3
     NL = st["levels"]
     # LF: per digit level and endpoint one 128-B rank block + one 8-B
     # superblock count, for every row that was live (restarts cost nothing)
-    prev_lo = np.concatenate([lo_hist[W - 1:W].cpu().numpy(), lo_np[:-1]])
-    prev_hi = np.concatenate([hi_hist[W - 1:W].cpu().numpy(), hi_np[:-1]])
-    tok_np = tokens[W:S].cpu().numpy()
     live = (prev_lo < prev_hi) & (tok_np >= 0)
     lf_bytes = (128 + 8) * 2 * NL * live.sum(1)
     lf_us = float(np.median(lf_ms)) * 1e3

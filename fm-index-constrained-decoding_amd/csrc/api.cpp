@@ -31,10 +31,15 @@ void set_error(const char* fmt, ...) {
 }
 
 void Index::release() {
-  void* ptrs[] = {wm, D, C, bwt, bm, sa, text, ws};
+  void* ptrs[] = {wm, sb, Z, D, C, bwt, bm, bm_full, bm_follow, sa, text, ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   wm = nullptr;
+  sb = nullptr;
+  Z = nullptr;
+  bm_full = nullptr;
+  bm_follow = nullptr;
+  follow_bytes = 0;
   D = nullptr;
   C = nullptr;
   bwt = nullptr;
@@ -684,7 +689,7 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
   if (levels) *levels = x.NL;
   if (wm_bytes) *wm_bytes = x.wm_bytes;
   if (bwt_bytes) *bwt_bytes = x.n * 4;
-  if (bitmap_bytes) *bitmap_bytes = x.bm_bytes;
+  if (bitmap_bytes) *bitmap_bytes = x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0);
   if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;
   return 0;
 }
@@ -694,6 +699,16 @@ int fm_device_bwt(const fm_index* h, const uint32_t** out) {
   *out = h->idx.bwt;
   return 0;
 }
+
+#ifdef FMIDX_STAMPS
+// Diagnostic build only (not part of include/fmidx.h): per-workgroup phase
+// stamps of the decode kernel go to d_buf (8 uint64 per workgroup), or off.
+int fm_debug_set_stamps(fm_index* h, uint64_t* d_buf) {
+  FM_CHECK_BUILT(h);
+  h->idx.view.stamps = d_buf;
+  return 0;
+}
+#endif
 
 int fm_synchronize(fm_index* h) {
   FM_CHECK_HANDLE(h);

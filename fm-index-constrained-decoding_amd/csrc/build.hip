@@ -239,6 +239,22 @@ __global__ void __launch_bounds__(kThreads) k_bm_base(const uint32_t* __restrict
   for (uint32_t w = threadIdx.x; w < words / 4; w += kThreads) dst[w] = s4[w];
 }
 
+// Bitmap of every symbol in BWT[0, n): LDS bitmap per workgroup over a grid
+// stride, merged with global atomicOr (once per set word per workgroup).
+__global__ void __launch_bounds__(kThreads) k_bm_full(const uint32_t* __restrict__ bwt, uint64_t n,
+                                                     uint32_t words, uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t bits[];
+  for (uint32_t w = threadIdx.x; w < words; w += kThreads) bits[w] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads) {
+    const uint32_t c = bwt[i];
+    atomicOr(&bits[c >> 5], 1u << (c & 31));
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < words; w += kThreads)
+    if (bits[w]) atomicOr(&out[w], bits[w]);
+}
+
 __global__ void __launch_bounds__(kThreads) k_bm_up(const uint32_t* __restrict__ child,
                                                    uint32_t words, uint32_t* __restrict__ out) {
   const uint64_t p = blockIdx.x;
@@ -388,7 +404,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   FM_HIP(hipFree(nxt));
 
   // -- range bitmaps
-  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", 13);
+  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", 12);
   const uint32_t words = (uint32_t)(((uint64_t)max_sym + 1 + 127) / 128 * 4);
   const uint64_t nb0 = n >> log2b0;
   uint32_t bm_levels = 0;
@@ -403,7 +419,14 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     ++bm_levels;
   }
   uint32_t* bm = nullptr;
+  uint32_t* bm_full = nullptr;
   if (dmalloc(&bm, total_words)) return -1;
+  if (bm_ok) {
+    if (dmalloc(&bm_full, words)) return -1;
+    FM_HIP(hipMemsetAsync(bm_full, 0, (size_t)words * 4, s));
+    k_bm_full<<<1024, kThreads, words * 4, s>>>(d_bwt, n, words, bm_full);
+    FM_HIP(hipGetLastError());
+  }
   if (bm_levels > 0) {
     k_bm_base<<<(unsigned)nb0, kThreads, words * 4, s>>>(d_bwt, log2b0, words, bm + bm_off[0]);
     FM_HIP(hipGetLastError());
@@ -425,6 +448,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   h->C = C;
   h->D = D;
   h->bm = bm;
+  h->bm_full = bm_full;
   h->wm_bytes = (uint64_t)NL * (nblk * 128 + nsb * kRadix * 8);
   h->bm_bytes = total_words * 4;
   DevView& v = h->view;
@@ -439,6 +463,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   v.C = C;
   v.bwt = d_bwt;
   v.bm = bm;
+  v.bm_full = bm_full;
   for (uint32_t j = 0; j < bm_levels; ++j) {
     v.bm_off[j] = bm_off[j];
     v.bm_count[j] = bm_count[j];
@@ -449,6 +474,18 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   v.bm_words = words;
   v.bm_levels = bm_levels;
   v.bm_log2 = log2b0;
+  // -- follow-set bitmaps (one per symbol's C-block), built with the mask
+  //    kernel itself once the view above is complete
+  if (bm_ok && env_u32("FMIDX_FOLLOW_BITMAPS", 1) != 0) {
+    const uint64_t nsym = (uint64_t)max_sym + 1;
+    uint32_t* fb = nullptr;
+    if (dmalloc(&fb, nsym * words)) return -1;
+    if (launch_follow_bitmaps(v, C, nsym, fb, s)) return -1;
+    FM_HIP(hipStreamSynchronize(s));
+    h->bm_follow = fb;
+    h->follow_bytes = nsym * words * 4;
+    v.bm_follow = fb;
+  }
   h->built = true;
   return 0;
 }

@@ -53,6 +53,8 @@ struct DevView {
   const uint64_t* C;          // [2^L + 1]
   const uint32_t* bwt;        // [n]
   const uint32_t* bm;         // bitmap hierarchy
+  const uint32_t* bm_full;    // bitmap of BWT[0, n) (all symbols), bm_words words
+  const uint32_t* bm_follow;  // per symbol c: bitmap of BWT[C[c], C[c+1]) (follow set), or null
   uint64_t bm_off[kMaxBmLevels];   // word offset of each bitmap level
   uint64_t bm_count[kMaxBmLevels]; // bitmaps per level
   uint32_t L;                 // symbol bits
@@ -61,7 +63,23 @@ struct DevView {
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
+#ifdef FMIDX_STAMPS
+  uint64_t* stamps;           // diagnostic build only: per-workgroup phase timestamps
+#endif
 };
+
+// Diagnostic phase stamps (s_memrealtime, 100 MHz), compiled only with -DFMIDX_STAMPS.
+#ifdef FMIDX_STAMPS
+#define FM_STAMP(v, slot)                                                              \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && (v).stamps)                                                \
+      (v).stamps[(uint64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FM_STAMP(v, slot) \
+  do {                    \
+  } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // occurrences of digit d among the first m (<= 16) nibbles of w
@@ -146,6 +164,12 @@ __device__ __forceinline__ void lf_step16(const DevView& v, int64_t sym, uint64_
     return;
   }
   const uint32_t c = (uint32_t)sym;
+  if (lo == 0 && hi == v.n) {                // [sdsl] backward_search full-range case
+    const uint64_t a = v.C[c], b = v.C[c + 1];
+    lo = a < b ? a : 0;
+    hi = a < b ? b : 0;
+    return;
+  }
   const uint32_t q = lane16 & 7u;
   const bool side = lane16 >= 8;
   uint64_t l = lo, r = hi;
@@ -199,9 +223,11 @@ struct Index {
   uint64_t* C = nullptr;
   uint32_t* bwt = nullptr;
   uint32_t* bm = nullptr;
+  uint32_t* bm_full = nullptr;
+  uint32_t* bm_follow = nullptr;
   uint64_t* sa = nullptr;
   uint32_t* text = nullptr;
-  uint64_t wm_bytes = 0, bm_bytes = 0;
+  uint64_t wm_bytes = 0, bm_bytes = 0, follow_bytes = 0;
   // grow-only workspace for batched traversals
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -231,6 +257,8 @@ int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64
 int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                   const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                   uint64_t m, uint8_t* mask, uint64_t ld, uint64_t vocab, int packed, hipStream_t s);
+int launch_follow_bitmaps(const DevView& v, const uint64_t* C, uint64_t nsym, uint32_t* out,
+                          hipStream_t s);
 int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
                     void* ws, uint64_t total_cap, hipStream_t s);

@@ -224,7 +224,9 @@ class FMIndex:
         vals = [c_uint64() for _ in range(5)]
         check(lib().fm_stats(self._h, *[byref(v) for v in vals]), "stats")
         keys = ["levels", "wm_bytes", "bwt_bytes", "bitmap_bytes", "bitmap_block"]
-        return {k: int(v.value) for k, v in zip(keys, vals)}
+        out = {k: int(v.value) for k, v in zip(keys, vals)}
+        out["follow_bytes"] = int(os.environ.get("FMIDX_FOLLOW_BITMAPS", "1") != "0" and out["bitmap_block"] > 0)
+        return out
 
     def get_range_batch(self, patterns: Sequence[Sequence[int]], shift: int = 0,
                         starts: Optional[Tuple[Sequence[int], Sequence[int]]] = None):

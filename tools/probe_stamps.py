@@ -1,0 +1,72 @@
+"""Where does a decode step's time go?  Loads the diagnostic library
+(libfmidx_stamps.so), replays trace steps one launch at a time and prints
+per-workgroup phase durations (s_memrealtime, 10 ns ticks)."""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "fm-index-constrained-decoding_amd")
+os.environ["FMIDX_LIB"] = os.path.join(PKG, "fmidx", os.environ.get("STAMPS_LIB", "libfmidx_stamps.so"))
+sys.path[:0] = [REPO, PKG]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import SHIFT, build_index, make_trace  # noqa: E402
+from fmidx._lib import lib  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+V, B, W = 128256, 256, 5
+fm, text, bwt, _ = build_index(int(float(os.environ.get("TOKENS", "3e8"))), V, 20250905, dev)
+n = bwt.numel()
+tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, W + 12, 20250905, dev)
+dl = lib()
+dl.fm_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+T = int(os.environ.get("MASK_THREADS", "256"))
+want = max(1, int(os.environ.get("FMIDX_WAVE_BUDGET", "4096")) // (((B + 7) // 8 * 8) * (T // 64)))
+S0 = min(want, max(1, (V + 1023) // 1024))
+SW = int(os.environ.get("FMIDX_MASK_SW", "0")) or ((V + S0 - 1) // S0)
+SW = min(32768, (SW + 31) & ~31)
+S = (V + SW - 1) // SW
+grid = (B + 7) // 8 * 8 * S
+stamps = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
+lo_o = torch.empty(B, dtype=torch.int64, device=dev)
+hi_o = torch.empty(B, dtype=torch.int64, device=dev)
+names = ["lohi", "zero", "lf+plan", "stream", "bitmap", "barrier", "emit"]
+summary = []
+for s in range(W, W + 12):
+    lo_i, hi_i = lo_hist[s - 1].clone(), hi_hist[s - 1].clone()
+    fm.decode_step(tokens[s], lo_i, hi_i, mask, V, SHIFT, reset_below=0, lo_out=lo_o, hi_out=hi_o)  # warm
+    torch.cuda.synchronize()
+    stamps.zero_()
+    dl.fm_debug_set_stamps(fm._h, ctypes.c_void_p(stamps.data_ptr()))
+    fm.decode_step(tokens[s], lo_i, hi_i, mask, V, SHIFT, reset_below=0, lo_out=lo_o, hi_out=hi_o)
+    torch.cuda.synchronize()
+    dl.fm_debug_set_stamps(fm._h, None)
+    st = stamps.view(grid, 8).cpu().numpy().astype(np.int64)
+    ok = st[:, 0] > 0
+    st = st[ok]
+    t0 = st[:, 0].min()
+    span = (st[:, 7].max() - t0) * 10 / 1000
+    start_spread = (st[:, 0].max() - t0) * 10 / 1000
+    ph = np.diff(st, axis=1) * 10 / 1000     # us
+    b_ids = np.nonzero(ok)[0]
+    rows = (b_ids // (8 * S)) * 8 + (b_ids % (8 * S)) % 8
+    w_new = (hi_hist[s] - lo_hist[s]).cpu().numpy()[rows]
+    w_old = (hi_hist[s - 1] - lo_hist[s - 1]).cpu().numpy()[rows]
+    tot = (st[:, 7] - st[:, 0]) * 10 / 1000
+    end_rel = (st[:, 7] - t0) * 10 / 1000
+    summary.append((span, start_spread))
+    if os.environ.get("QUIET"):
+        continue
+    print(f"step {s}: kernel span {span:.1f}us, dispatch spread {start_spread:.1f}us, "
+          f"median WG {np.median(tot):.1f}us, mean phases " +
+          " ".join(f"{nm}={ph[:, i].mean():.2f}" for i, nm in enumerate(names)))
+    for j in np.argsort(-end_rel)[:4]:
+        print(f"   slowest-ending WG row {rows[j]} width {w_old[j]}->{w_new[j]} start "
+              f"{(st[j, 0] - t0) * 10 / 1000:.1f} end {end_rel[j]:.1f}: " +
+              " ".join(f"{nm}={ph[j, i]:.2f}" for i, nm in enumerate(names)))
+print(f"SUMMARY lib={os.environ.get('STAMPS_LIB')} SW={SW} S={S} grid={grid}: mean span "
+      f"{np.mean([a for a, _ in summary]):.1f}us, mean dispatch spread {np.mean([b for _, b in summary]):.1f}us")

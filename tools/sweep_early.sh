@@ -1,0 +1,6 @@
+set -e
+for EW in 0 64 1000000000000; do
+  echo "EARLY_ZERO_WIDTH=$EW"
+  FMIDX_EARLY_ZERO_WIDTH=$EW timeout -k 10 200 python bench.py --no-cpu 2>&1 >/dev/null | grep step
+  FMIDX_EARLY_ZERO_WIDTH=$EW QUIET=1 timeout -k 10 200 python tools/probe_stamps.py 2>&1 | grep SUMMARY
+done
