@@ -316,3 +316,42 @@ def test_properties_at_scale(dev):
         for j in rng.choice(int(k[i]), size=min(5, int(k[i])), replace=False):
             lo2, hi2 = idx.backward_search_step(int(sy[j]), int(a[i]), int(b[i]) - 1)
             assert hi2 - lo2 == int(c[j])
+
+
+def test_doc_sharded_masks_on_gpu(dev):
+    """Two doc-range shards (with halo) built as separate GPU indexes: the OR
+    of their masks equals the unsharded mask through incremental steps."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from fmidx.sharding import ShardedDecoder, shard_corpus
+
+    docs = markov_docs(41, 120, 80, 60)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    F = [t for d in reversed(docs) for t in d]
+    rng = np.random.default_rng(8)
+    B, V, steps = 48, 90, 6
+    starts = rng.integers(0, len(F) - 30, size=B)
+    pats = [F[s: s + int(rng.integers(1, 6))] for s in starts]
+    decs = []
+    for r in range(3):
+        sd, _ = shard_corpus(docs, 3, r, halo=5 + steps + 1)
+        ix = FMIndex(device=0)
+        ix.initialize(sd, in_memory=True)
+        decs.append(ShardedDecoder(ix, V, 10))
+    masks = [d.start(pats, dev) for d in decs]
+    got = masks[0] | masks[1] | masks[2]
+    want = allowed_mask(ora, *zip(*[ora.get_range(p) for p in pats]), V, 10)
+    assert np.array_equal(got.cpu().numpy(), want)
+    cur = [list(p) for p in pats]
+    pos = [s + len(p) for s, p in zip(starts, pats)]
+    for _ in range(steps):
+        tk = [F[pos[b]] if rng.random() < 0.8 else int(rng.integers(0, 85)) for b in range(B)]
+        pos = [p + 1 for p in pos]
+        cur = [c + [t] for c, t in zip(cur, tk)]
+        t = torch.tensor(tk, dtype=torch.int64, device=dev)
+        ms = [d.step(t) for d in decs]
+        got = ms[0] | ms[1] | ms[2]
+        want = allowed_mask(ora, *zip(*[ora.get_range(c) for c in cur]), V, 10)
+        assert np.array_equal(got.cpu().numpy(), want)

@@ -1,0 +1,156 @@
+"""Doc-range sharding (fmidx.sharding) on CPU with torch.distributed/gloo,
+world_size 2: OR of per-shard masks == the unsharded mask, for the initial
+pattern search and for incremental decode steps (with restarts).  Each
+rank's shard index is the oracle behind the FMIndex batched API (test
+infrastructure); the sharding logic and the collective are the product's."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle.fm_oracle import OracleIndex, allowed_mask
+
+V = 90
+SHIFT = 10
+
+
+class OracleShard:
+    """Oracle index exposing the batched API ShardedDecoder uses."""
+
+    def __init__(self, docs):
+        self.ix = OracleIndex()
+        self.ix.initialize(docs, in_memory=True)
+
+    def get_range_batch(self, patterns, shift):
+        assert shift == SHIFT
+        r = [self.ix.get_range(p) for p in patterns]
+        return np.array([a for a, _ in r], dtype=np.uint64), np.array([b for _, b in r], dtype=np.uint64)
+
+    def lf_step_batch(self, tokens, lo, hi, shift, reset_below=-(1 << 63)):
+        n = self.ix.size()
+        for i in range(lo.numel()):
+            t, l, h = int(tokens[i]), int(lo[i]), int(hi[i])
+            if t < reset_below:
+                l, h = 0, n
+            elif l >= h or t + shift < 0:
+                l, h = 0, 0
+            else:
+                l, h = self.ix.backward_search_step(t + shift, l, h - 1)
+            lo[i], hi[i] = l, h
+        return lo, hi
+
+    def allowed_mask(self, lo, hi, vocab, shift):
+        return torch.from_numpy(allowed_mask(self.ix, lo.tolist(), hi.tolist(), vocab, shift))
+
+
+def make_case(seed=5):
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(40):
+        ln = int(rng.integers(1, 30))
+        tok = int(rng.integers(0, 60))
+        d = []
+        for _ in range(ln):
+            d.append(tok)
+            tok = (tok * 17 + 3) % 60 if rng.random() < 0.7 else int(rng.integers(0, 60))
+        docs.append(d)
+    F = [t for d in reversed(docs) for t in d]
+    B = 24
+    starts = rng.integers(0, len(F) - 40, size=B)
+    lens = rng.integers(1, 8, size=B)
+    patterns = [F[s: s + ln] for s, ln in zip(starts, lens)]
+    steps = []
+    pos = [s + ln for s, ln in zip(starts, lens)]
+    for _ in range(8):
+        tk = []
+        for b in range(B):
+            r = rng.random()
+            if r < 0.75:
+                tk.append(F[pos[b]])
+            elif r < 0.9:
+                tk.append(int(rng.integers(0, 70)))
+            else:
+                tk.append(-1)   # restart
+            pos[b] += 1
+        steps.append(tk)
+    return docs, patterns, steps
+
+
+def expected_masks(docs, patterns, steps):
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    pats = [list(p) for p in patterns]
+    out = []
+    rng = [ora.get_range(p) for p in pats]
+    out.append(allowed_mask(ora, [r[0] for r in rng], [r[1] for r in rng], V, SHIFT))
+    for tk in steps:
+        for b, t in enumerate(tk):
+            pats[b] = [] if t < 0 else pats[b] + [t]
+        rng = [ora.get_range(p) for p in pats]
+        out.append(allowed_mask(ora, [r[0] for r in rng], [r[1] for r in rng], V, SHIFT))
+    return out
+
+
+def _worker(rank, world, port, halo, reduce, outdir):
+    import torch.distributed as dist
+
+    from fmidx.sharding import ShardedDecoder, shard_corpus
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    docs, patterns, steps = make_case()
+    shard_docs_, _ = shard_corpus(docs, world, rank, halo)
+    dec = ShardedDecoder(OracleShard(shard_docs_), V, SHIFT, group=dist.group.WORLD, reduce=reduce)
+    masks = [dec.start(patterns, "cpu").numpy().copy()]
+    for tk in steps:
+        masks.append(dec.step(torch.tensor(tk, dtype=torch.int64)).numpy().copy())
+    np.save(os.path.join(outdir, f"r{rank}.npy"), np.stack(masks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, halo, reduce):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d), nprocs=world, join=True)
+        return [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
+
+
+@pytest.mark.parametrize("reduce", ["max_u8", "gather_bits"])
+def test_sharded_or_equals_unsharded(reduce):
+    docs, patterns, steps = make_case()
+    want = np.stack(expected_masks(docs, patterns, steps))
+    got = _run(2, 8 + 8 + 1, reduce)      # halo >= longest pattern (7 + 8 steps) + 1
+    for g in got:                          # every rank holds the reduced mask
+        assert np.array_equal(g, want)
+
+
+def test_halo_is_required():
+    docs, patterns, steps = make_case()
+    want = np.stack(expected_masks(docs, patterns, steps))
+    got = _run(2, 0, "max_u8")
+    assert not np.array_equal(got[0], want)   # boundary-crossing n-grams are lost without a halo
+
+
+def test_shard_docs_balanced():
+    from fmidx.sharding import halo_tokens, shard_docs
+
+    lens = [5, 1, 1, 9, 2, 2, 8, 3]
+    parts = shard_docs(lens, 3)
+    assert parts[0][0] == 0 and parts[-1][1] == len(lens)
+    assert all(a <= b for a, b in parts) and all(parts[i][1] == parts[i + 1][0] for i in range(2))
+    docs = [[1, 2], [3, 4, 5], [6]]
+    assert halo_tokens(docs, 2, 4) == [3, 4, 5, 1]   # F continues with d1 then d0
+    assert halo_tokens(docs, 0, 4) == []
