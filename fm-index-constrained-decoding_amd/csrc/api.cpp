@@ -682,6 +682,15 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
                                 h->idx.ws, total_cap, reinterpret_cast<hipStream_t>(stream));
 }
 
+int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, uint64_t V,
+                    uint64_t ld_scores, uint64_t ld_out, const uint32_t* d_bits, uint64_t ld_bits,
+                    const uint32_t* d_unigram_bits, const fm_row_params* d_rows, int64_t eos,
+                    void* stream) {
+  static_assert(sizeof(fm_row_params) == 32, "fm_row_params layout");
+  return fmidx::launch_epilogue(dtype, d_scores, d_out, B, V, ld_scores, ld_out, d_bits, ld_bits,
+                                d_unigram_bits, d_rows, eos, reinterpret_cast<hipStream_t>(stream));
+}
+
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
              uint64_t* bitmap_bytes, uint64_t* bitmap_block) {
   FM_CHECK_BUILT(h);

@@ -264,6 +264,11 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
                     void* ws, uint64_t total_cap, hipStream_t s);
 size_t distinct_ws_bytes(uint64_t total_cap);
 
+// epilogue.hip
+int launch_epilogue(int dtype, const void* scores, void* out, uint64_t B, uint64_t V, uint64_t lds,
+                    uint64_t ldo, const uint32_t* bits, uint64_t ldb, const uint32_t* uni,
+                    const void* row_params, int64_t eos, hipStream_t s);
+
 void set_error(const char* fmt, ...);
 
 }  // namespace fmidx

@@ -1,0 +1,474 @@
+"""Document-constrained logits processors on the MI355X engine.
+
+Drop-in counterparts of the reference's in-process processors, same
+constructor arguments and call semantics, bit-identical outputs:
+
+* ``QwenIndexBasedLogitsProcessor``  -- document_constrained_generation_causal_qwen.py:7-214
+* ``CausalIndexBasedLogitsProcessor`` -- document_constrained_generation_causal.py:7-180
+* ``SeqIndexBasedLogitsProcessor``   -- document_constrained_generation_seq.py:6-123
+* ``VllmIndexBasedLogitsProcessor``  -- document_constrained_generation_vllm.py:6-137
+
+What changes is how a step executes.  The reference walks rows in Python,
+makes one SWIG call per pattern token (index.py:109-112) two or three times
+per row, fans distinct_count_multi out over threads, copies each row's
+distinct list host->device and builds the mask with ``torch.isin`` and two
+index-puts per row.  Here a step is: the cheap per-row token bookkeeping in
+Python (end marker, think marker, trailing n-gram rule, eos/pad rules), ONE
+batched range search for all rows (``fm_get_range_batch``), ONE packed
+allowed-token mask launch for all rows (``fm_allowed_mask_batch``) and ONE
+fused epilogue that writes ``scores + mask`` (``fm_apply_boosts``) -- no
+per-row device traffic.  The boost values are rounded to the scores dtype
+exactly as torch rounds a Python float on assignment, and the add happens in
+that dtype, so outputs match the reference bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_void_p
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+
+SHIFT = 10
+FLAG_BITS, FLAG_UNIGRAM, FLAG_EOS, FLAG_SPECIAL = 1, 2, 4, 8
+ROW_DTYPE = np.dtype([("base", "<f4"), ("v_dist", "<f4"), ("v_uni", "<f4"), ("v_eos", "<f4"),
+                      ("flags", "<u4"), ("reserved", "<i4"), ("special", "<i8")])
+_DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _round(x, dtype) -> float:
+    """The value a Python number takes when index-put into a ``dtype`` tensor
+    (the reference's ``mask[row, idx] = boost``), through the same setitem path."""
+    t = torch.zeros(1, dtype=dtype)
+    t[0] = x
+    return float(t[0])
+
+
+class _BatchedCore:
+    """Shared machinery: batched ranges, packed allowed bits, fused epilogue."""
+
+    def __init__(self, index):
+        self.index = index
+        self._uni_cache = {}
+
+    # -- index work ---------------------------------------------------------
+    def counts(self, patterns: Sequence[Sequence[int]]) -> List[int]:
+        if not patterns:
+            return []
+        lo, hi = self.index.get_range_batch(patterns, SHIFT)
+        return (hi.astype(np.int64) - lo.astype(np.int64)).tolist()
+
+    def ranges(self, patterns: Sequence[Sequence[int]]):
+        if not patterns:
+            z = np.zeros(0, dtype=np.uint64)
+            return z, z
+        return self.index.get_range_batch(patterns, SHIFT)
+
+    def allowed_bits(self, lo: np.ndarray, hi: np.ndarray, vocab: int):
+        device = torch.device("cuda", self.index.device)
+        lo_t = torch.tensor(lo.astype(np.int64), device=device)
+        hi_t = torch.tensor(hi.astype(np.int64), device=device)
+        return self.index.allowed_mask(lo_t, hi_t, vocab, SHIFT, packed=True)
+
+    def unigram_bits(self, vocab: int, device):
+        key = (str(device), vocab)
+        if key not in self._uni_cache:
+            words = (vocab + 31) // 32
+            bits = np.zeros(words * 32, dtype=np.uint8)
+            toks = np.asarray([t for t in self.index.occurring_distinct if 0 <= t < vocab], dtype=np.int64)
+            bits[toks] = 1
+            packed = np.packbits(bits, bitorder="little").view(np.int32)
+            self._uni_cache[key] = torch.from_numpy(packed.copy()).to(device)
+        return self._uni_cache[key]
+
+    def epilogue(self, scores: torch.Tensor, rows: np.ndarray, bits, eos: int) -> torch.Tensor:
+        """scores [B, V] (any supported dtype/device) -> scores + mask."""
+        dev_index = torch.device("cuda", self.index.device)
+        dtype = scores.dtype
+        if dtype not in _DTYPE_CODE:
+            raise TypeError(f"unsupported scores dtype {dtype}")
+        src = scores.to(dev_index).contiguous()
+        out = torch.empty_like(src)
+        B, V = src.shape
+        rp = torch.from_numpy(rows.view(np.uint8).copy()).to(dev_index)
+        uni = self.unigram_bits(V, dev_index)
+        stream = torch.cuda.current_stream(dev_index).cuda_stream
+        ldb = bits.stride(0) if bits is not None else 0
+        with torch.cuda.device(dev_index):
+            check(lib().fm_apply_boosts(_DTYPE_CODE[dtype], c_void_p(src.data_ptr()), c_void_p(out.data_ptr()), B, V,
+                                        src.stride(0), out.stride(0),
+                                        c_void_p(bits.data_ptr()) if bits is not None else None, ldb,
+                                        c_void_p(uni.data_ptr()), c_void_p(rp.data_ptr()), int(eos),
+                                        c_void_p(stream)), "apply_boosts")
+        return out.to(scores.device)
+
+
+def _find_marker_rows(input_ids: torch.Tensor, marker: Sequence[int]) -> List[torch.Tensor]:
+    """remove_end_marker's result list (…causal_qwen.py:44-56): for every row and
+    every occurrence of the marker, the tokens after it (rows without one are
+    dropped, rows with several repeat) -- vectorised search, same order."""
+    ids = input_ids.cpu()
+    m = len(marker)
+    out: List[torch.Tensor] = []
+    if ids.shape[1] < m:
+        return out
+    win = ids.unfold(1, m, 1)                                  # [B, L-m+1, m]
+    hit = (win == torch.tensor(marker, dtype=ids.dtype)).all(2)
+    for r, i in zip(*torch.nonzero(hit, as_tuple=True)):
+        out.append(input_ids[int(r), int(i) + m:])
+    return out
+
+
+def _distinct_rule(stop_at_count: int, count: int, last: int, eos: int, pad: int):
+    """The per-row distinct-set rule shared by every variant: returns a special
+    token, or None for "the allowed set of the row's range"."""
+    if stop_at_count > 0 and count <= stop_at_count:
+        return eos
+    if last == eos:
+        return pad
+    if last == pad:
+        return pad
+    return None
+
+
+class QwenIndexBasedLogitsProcessor:
+    """document_constrained_generation_causal_qwen.py:7-214 (soft boosts, think gating)."""
+
+    SYSTEM_TOKENS = [151667, 271, 151668, 271]
+    FINISHED_THINKING = (151668, 271)
+
+    def __init__(self, index, num_beams: int, min_new_tokens: int = 5, pad_token_id: int = 0,
+                 eos_token_id: int = 2, force_decoding_from: Optional[List[int]] = None, stop_at_count: int = 0,
+                 always_allow_eos: bool = False, forced_bos_token_id: Optional[int] = None,
+                 length_reward_factor: float = 2.0):
+        self.index = index
+        self.pad_token_id = pad_token_id
+        self.eos_token_id = eos_token_id
+        self._num_beams = num_beams
+        self.force_decoding_from = force_decoding_from
+        self.stop_at_count = stop_at_count
+        self.always_allow_eos = always_allow_eos
+        self.forced_bos_token_id = forced_bos_token_id
+        self.min_new_tokens = min_new_tokens
+        self.length_reward_factor = length_reward_factor
+        self.BOOST = 10.0
+        self.end_marker = [151645, 198, 151644, 77091, 198]
+        self._core = _BatchedCore(index)
+
+    @classmethod
+    def remove_system_tokens(cls, sent: List[int]) -> List[int]:
+        st = cls.SYSTEM_TOKENS
+        if len(sent) < len(st):
+            return [] if sent == st[: len(sent)] else sent
+        return sent[len(st):] if sent[: len(st)] == st else sent
+
+    @classmethod
+    def finished_thinking(cls, sent: List[int]) -> bool:
+        a, b = cls.FINISHED_THINKING
+        return any(sent[i] == a and sent[i + 1] == b for i in range(len(sent) - 1))
+
+    def __call__(self, input_ids, scores):
+        return self._process(input_ids, scores)
+
+    def _process(self, input_ids: torch.LongTensor, scores: torch.FloatTensor) -> torch.Tensor:
+        input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
+        B, V = scores.shape
+        rows = np.zeros(B, dtype=ROW_DTYPE)
+        L = input_ids.size(1)
+        if L == 0:
+            return self._core.epilogue(scores, rows, None, self.eos_token_id)
+        sents = input_ids.view(-1, self._num_beams, L).reshape(-1, L).tolist()
+        # think gating + remove_system_tokens + the trailing n-gram rule, whose
+        # loop returns on its first iteration: only count([last]) matters
+        proc: List[Optional[List[int]]] = []
+        need_last = []
+        for s in sents:
+            if not self.finished_thinking(s):
+                proc.append(None)
+                continue
+            s = self.remove_system_tokens(s)
+            proc.append(s)
+            if s:
+                need_last.append(len(proc) - 1)
+        last_counts = self._core.counts([[proc[i][-1]] for i in need_last])
+        for i, c in zip(need_last, last_counts):
+            if c == 0:
+                proc[i] = []
+        fdf = self.force_decoding_from
+        pat_rows, pats = [], []
+        for i, s in enumerate(proc):
+            if s and s[-1] not in (self.eos_token_id, self.pad_token_id):
+                pat_rows.append(i)
+                pats.append((fdf + s) if fdf is not None else s)
+        lo, hi = self._core.ranges(pats)
+        cnt = {i: int(h) - int(l) for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist())}
+        full_lo = np.zeros(B, dtype=np.uint64)
+        full_hi = np.zeros(B, dtype=np.uint64)
+        for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist()):
+            full_lo[i], full_hi[i] = l, h
+        bits = self._core.allowed_bits(full_lo, full_hi, V)
+        has_bits = bits.ne(0).any(1).cpu().numpy()   # distinct non-empty, one sync for the batch
+        dt = scores.dtype
+        boost = self.BOOST
+        eos_val = None
+        if self.always_allow_eos and L >= self.min_new_tokens:
+            eos_val = _round(boost * (self.length_reward_factor ** L), dt)
+        for i, s in enumerate(proc):
+            if s is None:
+                continue
+            r = rows[i]
+            if not s:
+                r["flags"] = FLAG_UNIGRAM
+                r["v_uni"] = _round(boost, dt)
+            else:
+                special = _distinct_rule(self.stop_at_count, cnt.get(i, 0), s[-1], self.eos_token_id,
+                                         self.pad_token_id)
+                r["v_dist"] = _round(boost * (self.length_reward_factor ** len(s)), dt)
+                if special is not None:
+                    r["flags"] = FLAG_SPECIAL | FLAG_UNIGRAM
+                    r["special"] = special
+                    empty = False
+                else:
+                    r["flags"] = FLAG_BITS | FLAG_UNIGRAM
+                    empty = not bool(has_bits[i])
+                r["v_uni"] = _round(boost if empty else boost / 2, dt)
+            if eos_val is not None:
+                r["flags"] |= FLAG_EOS
+                r["v_eos"] = eos_val
+        return self._core.epilogue(scores, rows, bits, self.eos_token_id)
+
+
+class CausalIndexBasedLogitsProcessor:
+    """document_constrained_generation_causal.py:7-180 (soft boosts, model-name marker)."""
+
+    END_MARKERS = {"qwen": [151645, 198, 151644, 77091, 198], "llama": [78191, 128007, 271]}
+
+    def __init__(self, index, num_beams: int, model_name: str, pad_token_id: int = 0, eos_token_id: int = 2,
+                 force_decoding_from: Optional[List[int]] = None, stop_at_count: int = 0,
+                 always_allow_eos: bool = False, forced_bos_token_id: Optional[int] = None,
+                 length_reward_factor=2.0):
+        self.index = index
+        self.pad_token_id = pad_token_id
+        self.eos_token_id = eos_token_id
+        self._num_beams = num_beams
+        self.force_decoding_from = force_decoding_from
+        self.stop_at_count = stop_at_count
+        self.always_allow_eos = always_allow_eos
+        self.forced_bos_token_id = forced_bos_token_id
+        self.length_reward_factor = length_reward_factor
+        self.BOOST = 10.0
+        self.model_name = model_name
+        self.end_marker = self.END_MARKERS["llama"]
+        if model_name.lower().startswith("qwen"):
+            self.end_marker = self.END_MARKERS["qwen"]
+        self._core = _BatchedCore(index)
+
+    def __call__(self, input_ids, scores):
+        return self._process(input_ids, scores)
+
+    def _process(self, input_ids, scores):
+        input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
+        B, V = scores.shape
+        dt = scores.dtype
+        rows = np.zeros(B, dtype=ROW_DTYPE)
+        boost = self.BOOST
+        if self.forced_bos_token_id is not None:
+            if input_ids.size(1) == 0:
+                rows["flags"] = FLAG_SPECIAL
+                rows["special"] = self.forced_bos_token_id
+                rows["v_dist"] = _round(boost, dt)
+                return self._core.epilogue(scores, rows, None, self.eos_token_id)
+            input_ids = input_ids[:, 1:]
+        L = input_ids.size(1)
+        bits = None
+        if L == 0:
+            rows["flags"] = FLAG_UNIGRAM
+            rows["v_uni"] = _round(boost, dt)
+        else:
+            sents = input_ids.view(-1, self._num_beams, L).reshape(-1, L).tolist()
+            # trailing n-gram: count([last]) == 0 -> [] (an empty sent returns None ~ [])
+            last_counts = self._core.counts([[s[-1]] for s in sents])
+            proc = [[] if c == 0 else s for s, c in zip(sents, last_counts)]
+            fdf = self.force_decoding_from
+            pat_rows, pats = [], []
+            for i, s in enumerate(proc):
+                if s and s[-1] not in (self.eos_token_id, self.pad_token_id):
+                    pat_rows.append(i)
+                    pats.append((fdf + s) if fdf is not None else s)
+            lo, hi = self._core.ranges(pats)
+            cnt = {i: int(h) - int(l) for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist())}
+            full_lo = np.zeros(B, dtype=np.uint64)
+            full_hi = np.zeros(B, dtype=np.uint64)
+            for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist()):
+                full_lo[i], full_hi[i] = l, h
+            bits = self._core.allowed_bits(full_lo, full_hi, V)
+            for i, s in enumerate(proc):
+                r = rows[i]
+                if not s:
+                    r["flags"] = FLAG_UNIGRAM
+                    r["v_uni"] = _round(boost, dt)
+                    continue
+                special = _distinct_rule(self.stop_at_count, cnt.get(i, 0), s[-1], self.eos_token_id,
+                                         self.pad_token_id)
+                r["v_dist"] = _round(boost * (self.length_reward_factor ** len(s)), dt)
+                r["v_uni"] = _round(boost / 2, dt)          # always BOOST / 2 in this variant
+                if special is not None:
+                    r["flags"] = FLAG_SPECIAL | FLAG_UNIGRAM
+                    r["special"] = special
+                else:
+                    r["flags"] = FLAG_BITS | FLAG_UNIGRAM
+        if self.always_allow_eos:
+            rows["flags"] |= FLAG_EOS
+            rows["v_eos"] = _round(boost * (self.length_reward_factor ** L), dt)
+        return self._core.epilogue(scores, rows, bits, self.eos_token_id)
+
+
+class _HardMaskBase:
+    """Shared by the hard-mask (-inf) variants."""
+
+    def _hard(self, sents: List[List[int]], pattern_of, count_of, V: int, dt, B: int):
+        rows = np.zeros(B, dtype=ROW_DTYPE)
+        rows["base"] = float("-inf")
+        boost = _round(self.BOOST, dt)
+        fdf = self.force_decoding_from if self.force_decoding_from is not None else []
+        pats, cpats, pat_rows = [], [], []
+        for i, s in enumerate(sents):
+            if s[-1] in (self.eos_token_id, self.pad_token_id):
+                continue
+            pat_rows.append(i)
+            pats.append(fdf + pattern_of(s))
+            cpats.append(fdf + count_of(s))
+        lo, hi = self._core.ranges(pats)
+        counts = self._core.counts(cpats)
+        cnt = dict(zip(pat_rows, counts))
+        full_lo = np.zeros(B, dtype=np.uint64)
+        full_hi = np.zeros(B, dtype=np.uint64)
+        for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist()):
+            full_lo[i], full_hi[i] = l, h
+        bits = self._core.allowed_bits(full_lo, full_hi, V)
+        for i, s in enumerate(sents):
+            r = rows[i]
+            special = _distinct_rule(self.stop_at_count, cnt.get(i, 0), s[-1], self.eos_token_id,
+                                     self.pad_token_id)
+            r["v_dist"] = boost
+            if special is not None:
+                r["flags"] = FLAG_SPECIAL
+                r["special"] = special
+            else:
+                r["flags"] = FLAG_BITS
+        return rows, bits
+
+
+class VllmIndexBasedLogitsProcessor(_HardMaskBase):
+    """document_constrained_generation_vllm.py:6-137 (vLLM V0 per-sequence hard mask)."""
+
+    def __init__(self, index, num_beams: int, pad_token_id: int = 0, eos_token_id: int = 2,
+                 force_decoding_from: Optional[List[int]] = None, stop_at_count: int = 0,
+                 always_allow_eos: bool = False, forced_bos_token_id: Optional[int] = None):
+        self.index = index
+        self.pad_token_id = pad_token_id
+        self.eos_token_id = eos_token_id
+        self._num_beams = num_beams
+        self.force_decoding_from = force_decoding_from
+        self.stop_at_count = stop_at_count
+        self.always_allow_eos = always_allow_eos
+        self.forced_bos_token_id = forced_bos_token_id
+        self.BOOST = 0.0
+        self._core = _BatchedCore(index)
+
+    def clone(self):
+        return VllmIndexBasedLogitsProcessor(num_beams=self._num_beams, index=self.index,
+                                             pad_token_id=self.pad_token_id, eos_token_id=self.eos_token_id,
+                                             force_decoding_from=self.force_decoding_from,
+                                             stop_at_count=self.stop_at_count,
+                                             always_allow_eos=self.always_allow_eos,
+                                             forced_bos_token_id=self.forced_bos_token_id)
+
+    def __call__(self, input_ids, scores):
+        input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
+        scores = scores.unsqueeze(0)
+        B, V = scores.shape
+        dt = scores.dtype
+        boost = _round(self.BOOST, dt)
+        if self.forced_bos_token_id is not None:
+            if input_ids.size(1) == 0:
+                rows = np.zeros(B, dtype=ROW_DTYPE)
+                rows["base"] = float("-inf")
+                rows["flags"] = FLAG_SPECIAL
+                rows["special"] = self.forced_bos_token_id
+                rows["v_dist"] = boost
+                return self._core.epilogue(scores, rows, None, self.eos_token_id)
+            input_ids = input_ids[:, 1:]
+        L = input_ids.size(1)
+        bits = None
+        if L == 0:
+            rows = np.zeros(B, dtype=ROW_DTYPE)
+            rows["base"] = float("-inf")
+            rows["flags"] = FLAG_UNIGRAM
+            rows["v_uni"] = boost
+        else:
+            sents = input_ids.view(-1, self._num_beams, L).reshape(-1, L).tolist()
+            rows, bits = self._hard(sents, lambda s: s, lambda s: s[:-1], V, dt, B)
+        if self.always_allow_eos:
+            rows["flags"] |= FLAG_EOS
+            rows["v_eos"] = boost
+        return self._core.epilogue(scores, rows, bits, self.eos_token_id)
+
+
+class SeqIndexBasedLogitsProcessor(_HardMaskBase):
+    """document_constrained_generation_seq.py:6-123 (seq2seq hard mask; decoder start skipped)."""
+
+    def __init__(self, index, num_beams: int, pad_token_id: int = 0, eos_token_id: int = 2,
+                 force_decoding_from: Optional[List[int]] = None, stop_at_count: int = 0,
+                 always_allow_eos: bool = False, forced_bos_token_id: Optional[int] = None):
+        self.index = index
+        self.pad_token_id = pad_token_id
+        self.eos_token_id = eos_token_id
+        self._num_beams = num_beams
+        self.force_decoding_from = force_decoding_from
+        self.stop_at_count = stop_at_count
+        self.always_allow_eos = always_allow_eos
+        self.forced_bos_token_id = forced_bos_token_id
+        self.BOOST = 0.0
+        self._core = _BatchedCore(index)
+
+    def __call__(self, input_ids, scores):
+        return self._process(input_ids, scores)
+
+    def _process(self, input_ids, scores):
+        B, V = scores.shape
+        dt = scores.dtype
+        boost = _round(self.BOOST, dt)
+        if self.forced_bos_token_id is not None:
+            if input_ids.size(1) == 1:
+                rows = np.zeros(B, dtype=ROW_DTYPE)
+                rows["base"] = float("-inf")
+                rows["flags"] = FLAG_SPECIAL
+                rows["special"] = self.forced_bos_token_id
+                rows["v_dist"] = boost
+                return self._core.epilogue(scores, rows, None, self.eos_token_id)
+            input_ids = input_ids[:, 1:]
+        L = input_ids.size(1)
+        bits = None
+        if L == 1:
+            rows = np.zeros(B, dtype=ROW_DTYPE)
+            rows["base"] = float("-inf")
+            rows["flags"] = FLAG_UNIGRAM
+            rows["v_uni"] = boost
+        else:
+            sents = input_ids.view(-1, self._num_beams, L).reshape(-1, L).tolist()
+            rows, bits = self._hard(sents, lambda s: s[1:], lambda s: s[1:-1], V, dt, B)
+        if self.always_allow_eos:
+            rows["flags"] |= FLAG_EOS
+            rows["v_eos"] = boost
+        return self._core.epilogue(scores, rows, bits, self.eos_token_id)
+
+
+# reference class name of the primary processor
+IndexBasedLogitsProcessor = QwenIndexBasedLogitsProcessor
+
+__all__ = ["QwenIndexBasedLogitsProcessor", "CausalIndexBasedLogitsProcessor", "SeqIndexBasedLogitsProcessor",
+           "VllmIndexBasedLogitsProcessor", "IndexBasedLogitsProcessor"]

@@ -175,6 +175,35 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
                             const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
                             uint64_t* d_counts, uint64_t* d_k, void* stream);
 
+/* ---- fused logits-processor epilogue (no index needed) ------------------ */
+
+/* Per-row parameters of fm_apply_boosts (32 bytes, packed as declared). */
+typedef struct fm_row_params {
+  float base;      /* mask value of every other token: 0.0 (soft) or -inf (hard) */
+  float v_dist;    /* value of the allowed / distinct tokens */
+  float v_uni;     /* value of all_unigrams not in the distinct set */
+  float v_eos;     /* value of eos when FM_ROW_EOS is set (applied last) */
+  uint32_t flags;  /* FM_ROW_* */
+  int32_t reserved;
+  int64_t special; /* the single distinct token when FM_ROW_SPECIAL is set */
+} fm_row_params;
+
+#define FM_ROW_BITS 1u     /* distinct set = bit row b of d_bits */
+#define FM_ROW_UNIGRAM 2u  /* all_unigrams (d_unigram_bits) get v_uni */
+#define FM_ROW_EOS 4u      /* token eos gets v_eos */
+#define FM_ROW_SPECIAL 8u  /* token `special` is (also) in the distinct set */
+
+/* out[b, t] = scores[b, t] + mask[b, t], the mask of the reference processors
+ * (document_constrained_generation_causal_qwen.py:151-214 and the hard-mask
+ * variants) assembled on the fly from the allowed-token bit rows of
+ * fm_allowed_mask_batch(packed=1) and the per-row parameters, in the scores
+ * dtype (0 = f32, 1 = bf16, 2 = f16) with torch's rounding.  Row values must
+ * already be rounded to that dtype.  out may alias scores. */
+int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, uint64_t V,
+                    uint64_t ld_scores, uint64_t ld_out, const uint32_t* d_bits, uint64_t ld_bits,
+                    const uint32_t* d_unigram_bits, const fm_row_params* d_rows, int64_t eos,
+                    void* stream);
+
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
 /* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip

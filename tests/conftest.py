@@ -37,3 +37,10 @@ def golden_index_cases():
 
     with open(os.path.join(GOLDEN, "index_cases.json")) as f:
         return json.load(f)["cases"]
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    import pathlib
+
+    return pathlib.Path(GOLDEN)
