@@ -352,6 +352,47 @@ int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n
   return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
 }
 
+int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t n, int keep_sa_text,
+                                   void* stream) {
+  FM_CHECK_HANDLE(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!d_text || n == 0) {
+    set_error("empty text");
+    return -1;
+  }
+  auto& x = h->idx;
+  FM_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  x.release();
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
+  if (keep_sa_text) {
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
+    FM_HIP(hipMemcpyAsync(x.text, d_text, n * 4, hipMemcpyDeviceToDevice, x.stream));
+  }
+  if (fmidx::gpu_suffix_sort(d_text, n, x.bwt, keep_sa_text ? x.sa : nullptr, x.stream)) {
+    x.release();
+    return -1;
+  }
+  return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
+}
+
+int fm_suffix_sort_device(const uint32_t* d_text, uint64_t n, uint32_t* d_bwt, uint64_t* d_sa, void* stream) {
+  if (!d_text) {
+    set_error("null text");
+    return -1;
+  }
+  return fmidx::gpu_suffix_sort(d_text, n, d_bwt, d_sa, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_wt_int_levels_device(const uint32_t* d_bwt, uint64_t n, uint32_t L, uint64_t* d_words, void* stream) {
+  if (!d_bwt || !d_words || n == 0) {
+    set_error("null or empty input");
+    return -1;
+  }
+  return fmidx::gpu_wt_int_levels(d_bwt, n, L, d_words, reinterpret_cast<hipStream_t>(stream));
+}
+
 int fm_size(const fm_index* h, uint64_t* out) {
   FM_CHECK_BUILT(h);
   *out = h->idx.n;

@@ -265,6 +265,8 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
 size_t distinct_ws_bytes(uint64_t total_cap);
 
 // epilogue.hip
+int gpu_suffix_sort(const uint32_t* text, uint64_t n, uint32_t* bwt_out, uint64_t* sa_out, hipStream_t s);
+int gpu_wt_int_levels(const uint32_t* bwt, uint64_t n, uint32_t L, uint64_t* words, hipStream_t s);
 int launch_epilogue(int dtype, const void* scores, void* out, uint64_t B, uint64_t V, uint64_t lds,
                     uint64_t ldo, const uint32_t* bits, uint64_t ldb, const uint32_t* uni,
                     const void* row_params, int64_t eos, hipStream_t s);

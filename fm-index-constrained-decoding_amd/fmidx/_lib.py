@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_int64, c_size_t, c_uint8, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_int, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FMIDX_LIB", os.path.join(HERE, "libfmidx.so"))
@@ -26,6 +26,9 @@ SIGNATURES = {
     "fm_initialize": (c_int, [c_void_p, u64p, c_uint64]),
     "fm_initialize_from_file": (c_int, [c_void_p, c_char_p, c_int]),
     "fm_initialize_from_bwt_device": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "fm_initialize_from_text_device": (c_int, [c_void_p, c_void_p, c_uint64, c_int, c_void_p]),
+    "fm_suffix_sort_device": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "fm_wt_int_levels_device": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p, c_void_p]),
     "fm_size": (c_int, [c_void_p, u64p]),
     "fm_sigma": (c_int, [c_void_p, u64p]),
     "fm_backward_search_step": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, u64p]),

@@ -118,6 +118,17 @@ class FMIndex:
             c_void_p(text.data_ptr()) if text is not None else None,
             c_void_p(stream)), "initialize_from_bwt_device")
 
+    def initialize_from_text_device(self, text, keep_sa_text: bool = False) -> None:
+        """GPU construction (suffix sort + BWT + index) from T' (int32 tensor in
+        HBM, ending with the unique sentinel 0); replaces sdsl construct_im
+        (fm_index.cpp:33-41) for corpora too large for host suffix sorting."""
+        import torch
+
+        assert text.is_cuda and text.dtype == torch.int32 and text.is_contiguous()
+        check(lib().fm_initialize_from_text_device(self._h, c_void_p(text.data_ptr()), text.numel(),
+                                                   1 if keep_sa_text else 0, c_void_p(_stream_of(text))),
+              "initialize_from_text_device")
+
     # -- SWIG surface --------------------------------------------------------
     def size(self) -> int:
         out = c_uint64()
@@ -351,4 +362,34 @@ def load_FMIndex(path: str, device: Optional[int] = None) -> FMIndex:
     return obj
 
 
-__all__ = ["FMIndex", "load_FMIndex", "FMIndexError"]
+__all__ = ["FMIndex", "load_FMIndex", "FMIndexError", "suffix_sort_device", "wt_int_levels_device"]
+
+
+def suffix_sort_device(text, want_sa: bool = False):
+    """GPU suffix sorting of T' (int32 CUDA tensor, unique sentinel 0 last):
+    returns (bwt int32, sa int64 or None) on the same device."""
+    import torch
+
+    assert text.is_cuda and text.dtype == torch.int32 and text.is_contiguous()
+    n = text.numel()
+    bwt = torch.empty(n, dtype=torch.int32, device=text.device)
+    sa = torch.empty(n, dtype=torch.int64, device=text.device) if want_sa else None
+    with torch.cuda.device(text.device):
+        check(lib().fm_suffix_sort_device(c_void_p(text.data_ptr()), n, c_void_p(bwt.data_ptr()),
+                                          c_void_p(sa.data_ptr()) if sa is not None else None,
+                                          c_void_p(_stream_of(text))), "suffix_sort_device")
+    return bwt, sa
+
+
+def wt_int_levels_device(bwt, L: int):
+    """sdsl wt_int level bit vectors of a device BWT: int64 tensor [L, ceil(n/64)]
+    (bit patterns of uint64 words, LSB-first)."""
+    import torch
+
+    assert bwt.is_cuda and bwt.dtype == torch.int32 and bwt.is_contiguous()
+    n = bwt.numel()
+    words = torch.empty((L, (n + 63) // 64), dtype=torch.int64, device=bwt.device)
+    with torch.cuda.device(bwt.device):
+        check(lib().fm_wt_int_levels_device(c_void_p(bwt.data_ptr()), n, int(L), c_void_p(words.data_ptr()),
+                                            c_void_p(_stream_of(bwt))), "wt_int_levels_device")
+    return words

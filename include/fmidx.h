@@ -72,6 +72,29 @@ int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n
                                   const uint64_t* d_sa, const uint32_t* d_text,
                                   void* stream);
 
+/* Index construction on the GPU from a device-resident T' (replaces sdsl
+ * construct_im / construct, fm_index.cpp:33-48, whose divsufsort runs on the
+ * host): suffix array by prefix doubling with 64-bit positions, then the BWT
+ * and the index.  ``d_text``: n uint32 symbols, T'[n-1] == 0 the unique
+ * sentinel, n < 2^34.  ``keep_sa_text`` != 0 also keeps SA and T' on the
+ * device for fm_locate / fm_extract_text.  The caller keeps ``d_text``. */
+int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t n, int keep_sa_text,
+                                   void* stream);
+
+/* The GPU suffix sorter on its own (current device, ``stream``): writes
+ * BWT[j] = T'[SA[j] - 1 mod n] to ``d_bwt`` (n uint32, may be NULL) and the
+ * suffix array to ``d_sa`` (n uint64, may be NULL). */
+int fm_suffix_sort_device(const uint32_t* d_text, uint64_t n, uint32_t* d_bwt, uint64_t* d_sa,
+                          void* stream);
+
+/* The levelwise wavelet tree of sdsl's csa_wt_int<> (wt_int): level l =
+ * the bits (MSB first) of the BWT stably sorted by its top l bits, packed
+ * LSB-first into ceil(n/64) uint64 words per level, levels contiguous in
+ * ``d_words`` (L * ceil(n/64) words).  For exporting sdsl-compatible level
+ * vectors and for building the CPU baseline at full scale. */
+int fm_wt_int_levels_device(const uint32_t* d_bwt, uint64_t n, uint32_t L, uint64_t* d_words,
+                            void* stream);
+
 /* ---- SWIG surface (host pointers, synchronous) ------------------------- */
 
 /* FMIndex::size() -- fm_index.cpp:50-52: corpus tokens + 1 sentinel. */

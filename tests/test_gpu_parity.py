@@ -355,3 +355,120 @@ def test_doc_sharded_masks_on_gpu(dev):
         got = ms[0] | ms[1] | ms[2]
         want = allowed_mask(ora, *zip(*[ora.get_range(c) for c in cur]), V, 10)
         assert np.array_equal(got.cpu().numpy(), want)
+
+
+# ---------------------------------------------------------------- GPU construction
+def _sa_cases():
+    rng = np.random.default_rng(404)
+    cases = {
+        "single": [0],
+        "two": [11, 0],
+        "run": [12] * 300 + [0],                               # one symbol: log2(n) rounds
+        "period3": ([11, 12, 13] * 200) + [0],
+        "period7_mixed": ([14, 11, 11, 12, 15, 11, 13] * 90) + [16, 0],
+        "binary_random": rng.integers(1, 3, size=2000).tolist() + [0],
+        "zipfish": (np.minimum(rng.zipf(1.3, size=5000), 5000) + 10).tolist() + [0],
+        "big_symbols": (rng.integers(10, 130000, size=3000)).tolist() + [0],
+        "wide_symbols": (rng.integers(10, (1 << 20), size=1500)).tolist() + [0],   # 1 symbol per first key
+    }
+    return cases
+
+
+@pytest.mark.parametrize("chunk", [None, "1024"])
+def test_gpu_suffix_sort_vs_oracle(dev, chunk):
+    """fm_suffix_sort_device == suffix sorting by definition, including the
+    multi-chunk and larger-than-a-chunk group paths (FMIDX_SA_CHUNK=1024)."""
+    import torch
+
+    from fmidx.fm_index import suffix_sort_device
+    from oracle.fm_oracle import suffix_array
+
+    old = os.environ.get("FMIDX_SA_CHUNK")
+    if chunk:
+        os.environ["FMIDX_SA_CHUNK"] = chunk
+    try:
+        for name, t in _sa_cases().items():
+            text = np.asarray(t, dtype=np.int64)
+            want = suffix_array(text)
+            tt = torch.tensor(text.astype(np.int32), device=dev)
+            bwt, sa = suffix_sort_device(tt, want_sa=True)
+            assert np.array_equal(sa.cpu().numpy(), want), name
+            n = text.size
+            want_bwt = text[(want + n - 1) % n]
+            assert np.array_equal(bwt.cpu().numpy(), want_bwt.astype(np.int32)), name
+    finally:
+        if chunk:
+            if old is None:
+                del os.environ["FMIDX_SA_CHUNK"]
+            else:
+                os.environ["FMIDX_SA_CHUNK"] = old
+
+
+def test_gpu_suffix_sort_rejects_bad_sentinel(dev):
+    import torch
+
+    from fmidx import FMIndexError
+    from fmidx.fm_index import suffix_sort_device
+
+    for bad in ([11, 12, 13], [11, 0, 12, 0], [0, 11, 12]):
+        with pytest.raises(FMIndexError):
+            suffix_sort_device(torch.tensor(bad, dtype=torch.int32, device=dev))
+
+
+def test_initialize_from_text_device_vs_oracle(dev):
+    import torch
+
+    from fmidx.fm_index import FMIndex
+
+    docs = markov_docs(55, 200, 400, 120)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    text = torch.tensor(ora.text.astype(np.int32), device=dev)
+    fm = FMIndex(device=0)
+    fm.initialize_from_text_device(text, keep_sa_text=True)
+    n = ora.size()
+    assert fm.size() == n
+    rng = np.random.default_rng(9)
+    for _ in range(100):
+        a = int(rng.integers(0, n))
+        b = int(rng.integers(a, n + 1))
+        s = int(rng.integers(10, 420))
+        assert fm.backward_search_step(s, a, b) == ora.backward_search_step(s, a, b)
+        assert fm.distinct_count(a, b) == ora.distinct_count(a, b)
+        assert fm.locate(a) == ora.locate(a)
+
+
+def test_wt_int_levels_device(dev):
+    import torch
+
+    from fmidx.fm_index import wt_int_levels_device
+    from oracle.cpu_ref import levels_numpy
+
+    rng = np.random.default_rng(3)
+    for n, hi in ((1, 2), (63, 40), (64, 300), (1000, 130000), (4099, 17)):
+        b = rng.integers(0, hi, size=n).astype(np.int64)
+        L = max(1, int(b.max()).bit_length())
+        got = wt_int_levels_device(torch.tensor(b.astype(np.int32), device=dev), L).cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, levels_numpy(b, L)), (n, hi)
+
+
+def test_gpu_suffix_sort_at_scale_matches_doubling(dev):
+    """~50M-token synthetic corpus: the chunked GPU sorter and the torch
+    prefix-doubling builder agree on the whole BWT (forced small chunks)."""
+    import torch
+
+    from fmidx.fm_index import suffix_sort_device
+    from fmidx.synth import bwt_from_sa, markov_corpus_gpu, suffix_array_gpu
+
+    text, _ = markov_corpus_gpu(50_000_000, 128256, 99, dev)
+    want = bwt_from_sa(text, suffix_array_gpu(text))
+    old = os.environ.get("FMIDX_SA_CHUNK")
+    os.environ["FMIDX_SA_CHUNK"] = str(1 << 22)
+    try:
+        got, _ = suffix_sort_device(text)
+    finally:
+        if old is None:
+            del os.environ["FMIDX_SA_CHUNK"]
+        else:
+            os.environ["FMIDX_SA_CHUNK"] = old
+    assert torch.equal(got, want)
