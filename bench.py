@@ -7,7 +7,7 @@ allowed-next-token mask bool[B, V] of the new ranges (SURVEY §8a A2-A8,
 incremental mode of §5 "long-context").  Inputs (index, decode trace,
 states) are resident in HBM before timing.
 
-Workload: seeded order-1 Markov corpus with Zipf(1.1) rows over
+Workload (BASELINE configs[2]: n = 4.5e9 "enwiki" scale, B = 256): seeded order-1 Markov corpus with Zipf(1.1) rows over
 V = 128256 (+SHIFT 10, 17 wavelet levels), lognormal docs (mean ~500),
 encoded exactly as index.py:47-53; suffix array built on the GPU.  Decode
 trace: B rows start from U{1..32}-token true corpus patterns; each step a row
@@ -37,8 +37,8 @@ for _p in (REPO, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-from fmidx.fm_index import FMIndex  # noqa: E402
-from fmidx.synth import bwt_from_sa, markov_corpus_gpu, suffix_array_gpu  # noqa: E402
+from fmidx.fm_index import FMIndex, suffix_sort_device, wt_int_levels_device  # noqa: E402
+from fmidx.synth import markov_corpus_gpu  # noqa: E402
 
 SHIFT = 10
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 measured stream)
@@ -56,11 +56,11 @@ def build_index(n_tokens: int, vocab: int, seed: int, dev):
     text, beg = markov_corpus_gpu(n_tokens, vocab, seed, dev)
     torch.cuda.synchronize()
     t1 = time.time()
-    sa = suffix_array_gpu(text)
+    log(f"corpus n={text.numel()} docs={beg.numel() - 1} in {t1 - t0:.1f}s; GPU suffix sorting ...")
+    bwt, _ = suffix_sort_device(text)      # csrc/sa.hip: prefix doubling, 64-bit positions
     torch.cuda.synchronize()
     t2 = time.time()
-    bwt = bwt_from_sa(text, sa)
-    del sa
+    log(f"suffix sorting {t2 - t1:.1f}s; building the index ...")
     fm = FMIndex(device=dev.index)
     fm.initialize_from_bwt_device(bwt)
     torch.cuda.synchronize()
@@ -159,29 +159,14 @@ def cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, warmup, seconds, dev):
 
     n = bwt.numel()
     L = max(1, int(bwt.max().item()).bit_length())
-    wpl = (n + 63) // 64
-    words = np.zeros((L, wpl), dtype=np.uint64)
-    b64 = bwt.to(torch.int64)
-    pw = (torch.ones(1, dtype=torch.int64, device=dev) << torch.arange(64, device=dev, dtype=torch.int64))
-    for lev in range(L):
-        if lev == 0:
-            seq = b64
-        else:
-            _, order = torch.sort(b64 >> (L - lev), stable=True)
-            seq = b64[order]
-            del order
-        bits = ((seq >> (L - 1 - lev)) & 1)
-        pad = torch.zeros(wpl * 64, dtype=torch.int64, device=dev)
-        pad[:n] = bits
-        w = (pad.view(-1, 64) * pw).sum(1)
-        words[lev] = w.cpu().numpy().view(np.uint64)
-        del seq, bits, pad, w
-    cnt = torch.bincount(b64, minlength=(1 << L) + 1)
+    # sdsl wt_int level bit vectors built on the GPU (csrc/sa.hip), copied to the host
+    words = wt_int_levels_device(bwt, L).cpu().numpy().view(np.uint64)
+    cnt = torch.bincount(bwt.to(torch.int64), minlength=(1 << L) + 1)
     C = torch.zeros((1 << L) + 1, dtype=torch.int64, device=dev)
     torch.cumsum(cnt[: 1 << L], 0, out=C[1:])
     sigma = int((cnt > 0).sum().item())
     C = C.cpu().numpy().view(np.uint64)
-    del b64, cnt
+    del cnt
     t0 = time.time()
     ref = CpuRef(words, n, L, C, sigma)
     log(f"cpu_ref build {time.time() - t0:.1f}s")
@@ -216,7 +201,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--tokens", type=float, default=float(os.environ.get("FMIDX_BENCH_TOKENS", 3.0e8)))
+    ap.add_argument("--tokens", type=float, default=float(os.environ.get("FMIDX_BENCH_TOKENS", 4.5e9)))
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--vocab", type=int, default=128256)
     ap.add_argument("--seed", type=int, default=20250905)
@@ -389,7 +374,7 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
-                        f"of n={n} tokens (C2 scale), B={B} rows, V={V}, incremental ranges",
+                        f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else 'C2 simplewiki'} scale), B={B} rows, V={V}, incremental ranges",
             "corpus_tokens": n,
             "global_batch": world * B,
             "batch_per_gpu": B,

@@ -10,6 +10,7 @@
 // Every pass is a coalesced stream over n symbols.
 #include "fmidx_internal.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -190,13 +191,16 @@ __global__ void k_count_zero(const uint32_t* __restrict__ a, uint64_t n, unsigne
 }
 
 // Symbol runs of the final wavelet order: S[c] = first row, E[c] = one past.
+// Grid-stride: a dispatch holds at most 2^32 work-items per dimension, so a
+// one-thread-per-row grid would silently cover only part of n > 2^32.
 __global__ void k_bounds(const uint32_t* __restrict__ fin, uint64_t n, uint64_t* __restrict__ S,
                          uint64_t* __restrict__ E) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t c = fin[i];
-  if (i == 0 || fin[i - 1] != c) S[c] = i;
-  if (i + 1 == n || fin[i + 1] != c) E[c] = i + 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = fin[i];
+    if (i == 0 || fin[i - 1] != c) S[c] = i;
+    if (i + 1 == n || fin[i + 1] != c) E[c] = i + 1;
+  }
 }
 
 __global__ void k_counts(const uint64_t* __restrict__ S, const uint64_t* __restrict__ E, uint64_t K,
@@ -388,7 +392,8 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   FM_HIP(hipMemsetAsync(E, 0, K * 8, s));
   FM_HIP(hipMemsetAsync(cnt, 0, (K + 1) * 8, s));
   FM_HIP(hipMemsetAsync(d_sigma, 0, 8, s));
-  k_bounds<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(cur, n, S, E);
+  k_bounds<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 20), kThreads, 0, s>>>(cur, n, S,
+                                                                                                     E);
   k_counts<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(S, E, K, cnt, d_sigma);
   if (exclusive_scan_u64(cnt, C, K + 1, s, nullptr)) return -1;
   k_dtable<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(C, S, K, D);

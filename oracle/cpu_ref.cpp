@@ -265,8 +265,15 @@ void* cr_build(const uint64_t* level_words, uint64_t n, uint32_t L, const uint64
       const uint64_t tail = n & 63;
       if (tail) h->tree[(base >> 6) + wpl - 1] &= (1ull << tail) - 1;
     } else {
-      for (uint64_t i = 0; i < n; ++i)
-        if ((src[i >> 6] >> (i & 63)) & 1ull) h->tree[(base + i) >> 6] |= 1ull << ((base + i) & 63);
+      // unaligned level start: each source word lands in two destination words
+      const uint32_t off = (uint32_t)(base & 63);
+      uint64_t* dst = &h->tree[base >> 6];
+      for (uint64_t w = 0; w < wpl; ++w) {
+        uint64_t x = src[w];
+        if (w + 1 == wpl && (n & 63)) x &= (1ull << (n & 63)) - 1;
+        dst[w] |= x << off;
+        dst[w + 1] |= x >> (64 - off);
+      }
     }
   }
   h->rk.build(h->tree.data(), total_bits);
