@@ -209,6 +209,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=600)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dump-trace", default="", help="write the timed trace states to this .npz")
+    ap.add_argument("--eager-replay", action="store_true",
+                    help="after the timed region, launch the K timed steps once more eagerly (no graph) "
+                         "so PMC counters can be collected per dispatch (tools/pmc_traffic.sh)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -318,6 +321,14 @@ def main():
         step_ms = float(t.item())
     value = world * B * K / (step_ms * K / 1e3)
 
+    if args.eager_replay:
+        lo.copy_(state_lo)
+        hi.copy_(state_hi)
+        for i in range(K):
+            src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+            fm.decode_step(tokens[W + i], src[0], src[1], mask, V, SHIFT, reset_below=0,
+                           lo_out=dst[0], hi_out=dst[1])
+        torch.cuda.synchronize()
     if args.dump_trace and rank == 0:
         np.savez_compressed(args.dump_trace, tokens=tokens[:S].cpu().numpy(), lo=lo_hist[:S].cpu().numpy(),
                             hi=hi_hist[:S].cpu().numpy(), n=n, warmup=W)
