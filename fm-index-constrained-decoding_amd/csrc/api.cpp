@@ -34,6 +34,17 @@ void Index::release() {
   void* ptrs[] = {wm, sb, Z, D, C, bwt, bm, bm_full, bm_follow, sa, text, ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (int l = 0; l < kW2MaxLevels; ++l) {
+    if (w2_blocks[l]) (void)hipFree(w2_blocks[l]);
+    if (w2_sb[l]) (void)hipFree(w2_sb[l]);
+    w2_blocks[l] = nullptr;
+    w2_sb[l] = nullptr;
+  }
+  if (w2_Z) (void)hipFree(w2_Z);
+  if (D2) (void)hipFree(D2);
+  w2_Z = nullptr;
+  D2 = nullptr;
+  w2_bytes = 0;
   wm = nullptr;
   sb = nullptr;
   Z = nullptr;

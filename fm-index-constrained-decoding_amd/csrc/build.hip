@@ -10,6 +10,8 @@
 // Every pass is a coalesced stream over n symbols.
 #include "fmidx_internal.h"
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -275,6 +277,68 @@ __global__ void __launch_bounds__(kThreads) k_bm_up(const uint32_t* __restrict__
   }
 }
 
+// ---- 2-level wavelet matrix (LF path) ------------------------------------
+// One workgroup per superblock (64 blocks of 1024 digits): per block, the
+// header (running digit counts since the superblock start) is written before
+// the block's own digits are counted; the superblock totals go to sbtot.
+__global__ void __launch_bounds__(kThreads) k_w2_super(const uint32_t* __restrict__ cur, uint64_t n,
+                                                      uint32_t shift, uint32_t bits, uint64_t nblk,
+                                                      uint8_t* __restrict__ blocks, uint64_t blk_bytes,
+                                                      uint32_t* __restrict__ sbtot) {
+  extern __shared__ uint32_t sh[];   // run[R], cnt[R]
+  const uint32_t R = 1u << bits;
+  uint32_t* run = sh;
+  uint32_t* cnt = sh + R;
+  for (uint32_t d = threadIdx.x; d < 2 * R; d += kThreads) sh[d] = 0;
+  __syncthreads();
+  const uint64_t sbk = blockIdx.x;
+  const uint32_t per_sb = 1u << (kW2SbLog2 - kW2BlkLog2);
+  for (uint32_t j = 0; j < per_sb; ++j) {
+    const uint64_t b = sbk * per_sb + j;
+    if (b >= nblk) break;
+    uint8_t* blk = blocks + b * blk_bytes;
+    uint16_t* hdr = reinterpret_cast<uint16_t*>(blk);
+    for (uint32_t d = threadIdx.x; d < R; d += kThreads) hdr[d] = (uint16_t)run[d];
+    uint8_t* pay = blk + 2 * R;
+#pragma unroll
+    for (int t = 0; t < kW2Blk / kThreads; ++t) {
+      const uint32_t k = t * kThreads + threadIdx.x;
+      const uint64_t i = b * kW2Blk + k;
+      uint32_t d = 0;
+      if (i < n) {
+        d = (cur[i] >> shift) & (R - 1);
+        atomicAdd(&cnt[d], 1u);
+      }
+      if (bits > 8)
+        reinterpret_cast<uint16_t*>(pay)[k] = (uint16_t)d;
+      else
+        pay[k] = (uint8_t)d;
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < R; d += kThreads) {
+      run[d] += cnt[d];
+      cnt[d] = 0;
+    }
+    __syncthreads();
+  }
+  for (uint32_t d = threadIdx.x; d < R; d += kThreads) sbtot[sbk * R + d] = run[d];
+}
+
+// Per digit: absolute counts before every superblock, and the total.
+__global__ void k_w2_sbscan(const uint32_t* __restrict__ sbtot, uint64_t nsb, uint32_t R,
+                            uint64_t* __restrict__ sb, uint64_t* __restrict__ total) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= R) return;
+  uint64_t acc = 0;
+#pragma unroll 8
+  for (uint64_t s = 0; s < nsb; ++s) {
+    const uint32_t v = sbtot[s * R + d];
+    sb[s * R + d] = acc;
+    acc += v;
+  }
+  total[d] = acc;
+}
+
 template <typename T>
 int dmalloc(T** p, size_t count) {
   *p = nullptr;
@@ -491,7 +555,102 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     h->follow_bytes = nsym * words * 4;
     v.bm_follow = fb;
   }
+  if (device_build_w2(h, d_bwt, n, s)) return -1;
   h->built = true;
+  return 0;
+}
+
+// 2-level wavelet matrix over the BWT for the LF path (see W2Level).  Level l
+// holds the sequence stably partitioned by the digits of levels < l (a stable
+// radix sort by each digit's bit range); after the last level every symbol c
+// occupies one run starting at S2[c], so LF(i, c) = descent + C[c] - S2[c].
+int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
+  const uint32_t L = h->L;
+  const uint32_t NL2 = (L + 8) / 9;
+  if (NL2 > (uint32_t)kW2MaxLevels) {
+    set_error("2-level wavelet matrix: %u symbol bits need %u levels", L, NL2);
+    return -1;
+  }
+  uint32_t bits[kW2MaxLevels] = {0, 0, 0}, shift[kW2MaxLevels] = {0, 0, 0};
+  {
+    uint32_t left = L, sh = L;
+    for (uint32_t l = 0; l < NL2; ++l) {
+      const uint32_t w = (left + (NL2 - l) - 1) / (NL2 - l);   // ceil split, widest first
+      bits[l] = w;
+      sh -= w;
+      shift[l] = sh;
+      left -= w;
+    }
+  }
+  const uint64_t nblk = (n >> kW2BlkLog2) + 1;
+  const uint64_t nsb = (nblk >> (kW2SbLog2 - kW2BlkLog2)) + 1;
+  uint32_t *cur = nullptr, *nxt = nullptr, *sbtot = nullptr;
+  uint32_t maxR = 1u << bits[0];
+  if (dmalloc(&cur, n) || dmalloc(&nxt, n) || dmalloc(&sbtot, nsb * maxR) || dmalloc(&h->w2_Z, NL2 * (uint64_t)maxR))
+    return -1;
+  FM_HIP(hipMemcpyAsync(cur, d_bwt, n * 4, hipMemcpyDeviceToDevice, s));
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  FM_HIP(rocprim::radix_sort_keys(nullptr, tmp_bytes, cur, nxt, (size_t)n, 0, L, s));
+  if (dmalloc(reinterpret_cast<uint8_t**>(&tmp), tmp_bytes)) return -1;
+  uint64_t* total = nullptr;
+  if (dmalloc(&total, maxR)) return -1;
+  uint64_t bytes = 0;
+  for (uint32_t l = 0; l < NL2; ++l) {
+    const uint32_t R = 1u << bits[l];
+    const uint64_t blk_bytes = 2ull * R + (uint64_t)kW2Blk * (bits[l] > 8 ? 2 : 1);
+    if (dmalloc(&h->w2_blocks[l], nblk * blk_bytes) || dmalloc(&h->w2_sb[l], nsb * (uint64_t)R)) return -1;
+    bytes += nblk * blk_bytes + nsb * (uint64_t)R * 8;
+    k_w2_super<<<(unsigned)nsb, kThreads, 2 * R * 4, s>>>(cur, n, shift[l], bits[l], nblk, h->w2_blocks[l],
+                                                         blk_bytes, sbtot);
+    FM_HIP(hipGetLastError());
+    k_w2_sbscan<<<(R + 255) / 256, 256, 0, s>>>(sbtot, nsb, R, h->w2_sb[l], total);
+    FM_HIP(hipGetLastError());
+    // Z[d] = digits < d at this level
+    std::vector<uint64_t> tot(R), z(R);
+    FM_HIP(hipMemcpyAsync(tot.data(), total, R * 8, hipMemcpyDeviceToHost, s));
+    FM_HIP(hipStreamSynchronize(s));
+    uint64_t acc = 0;
+    for (uint32_t d = 0; d < R; ++d) {
+      z[d] = acc;
+      acc += tot[d];
+    }
+    uint64_t* Zl = h->w2_Z + (uint64_t)l * maxR;
+    FM_HIP(hipMemcpyAsync(Zl, z.data(), R * 8, hipMemcpyHostToDevice, s));
+    // next level's sequence: stable partition by this digit
+    size_t tb = tmp_bytes;
+    FM_HIP(rocprim::radix_sort_keys(tmp, tb, cur, nxt, (size_t)n, shift[l], shift[l] + bits[l], s));
+    std::swap(cur, nxt);
+    DevView& v = h->view;
+    v.w2[l].blocks = h->w2_blocks[l];
+    v.w2[l].sb = h->w2_sb[l];
+    v.w2[l].Z = Zl;
+    v.w2[l].blk_bytes = blk_bytes;
+    v.w2[l].bits = bits[l];
+    v.w2[l].shift = shift[l];
+  }
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(tmp));
+  FM_HIP(hipFree(total));
+  FM_HIP(hipFree(sbtot));
+  FM_HIP(hipFree(nxt));
+  // S2 / D2 from the final order
+  const uint64_t K = 1ull << L;
+  uint64_t *S = nullptr, *E = nullptr;
+  if (dmalloc(&S, K) || dmalloc(&E, K) || dmalloc(&h->D2, K)) return -1;
+  FM_HIP(hipMemsetAsync(S, 0, K * 8, s));
+  FM_HIP(hipMemsetAsync(E, 0, K * 8, s));
+  k_bounds<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 20), kThreads, 0, s>>>(cur, n, S,
+                                                                                                     E);
+  k_dtable<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(h->C, S, K, h->D2);
+  FM_HIP(hipGetLastError());
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(S));
+  FM_HIP(hipFree(E));
+  FM_HIP(hipFree(cur));
+  h->view.D2 = h->D2;
+  h->view.NL2 = NL2;
+  h->w2_bytes = bytes;
   return 0;
 }
 

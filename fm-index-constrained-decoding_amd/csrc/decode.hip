@@ -1,0 +1,584 @@
+// decode.hip -- the hot path: allowed-next-token masks, fused with the LF step.
+//
+// One decode step of the reference processors for every row b (SURVEY §8a
+// A2-A8): the backward-search step of the row's range by its new token
+// (index.py:109-112 -> fm_index.cpp:67-97), then
+//     allowed[b, t] = 1  <=>  t + shift occurs in BWT[lo_b, hi_b)
+// -- the boolean core of get_distinct_count_multi (fm_index.cpp:146-166 +
+// index.py:161-174, sentinel dropped) that the processors scatter into their
+// score masks (document_constrained_generation_causal_qwen.py:185-204).
+//
+// Geometry (gfx950): one workgroup of kDecThreads = 512 threads (8 waves)
+// per (row, vocab slice); 2 slices per row at B = 256 (the measured best:
+// 1024 threads x 1 slice and 256 x 4 are 0.3-1.6 us slower per step).
+//   wave 0        LF step (2-level wavelet matrix: 2 dependent round trips),
+//                 then the read plan of the new range
+//   waves 1..15   rows whose incoming range is already narrow stay narrow
+//                 after the step, so their mask row is zero-filled right away,
+//                 overlapping the LF chain
+//   all waves     partial ends of the range streamed from the plain BWT into
+//                 LDS bits (LDS atomics), whole-block bitmaps ORed in
+//   all waves     emit: 16 tokens per lane per store, consecutive lanes on
+//                 consecutive 16-B chunks (a wave writes 1 KB contiguous)
+#include "fmidx_internal.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace fmidx {
+
+namespace {
+
+#ifndef FMIDX_DEC_THREADS
+#define FMIDX_DEC_THREADS 512
+#endif
+#ifndef FMIDX_STORE_AUX
+#define FMIDX_STORE_AUX 16
+#endif
+constexpr int kDecThreads = FMIDX_DEC_THREADS;
+// cache policy of the mask stores (buffer-store aux bits): 16 = sc1, i.e.
+// write-through -- the 33 MB of mask a step writes leaves no dirty L2 lines
+// for the kernel-end writeback to flush (MI355X_MICROARCH.md "boundary":
+// + bytes / 6 TB/s behind a predecessor that leaves bytes dirty); 0 = plain.
+constexpr int kStoreAux = FMIDX_STORE_AUX;
+constexpr int kMaxPlan = 160;                 // >= 6 * kMaxBmLevels
+constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
+constexpr int kWinWords = kMaxSliceTokens / 32 + 16;
+constexpr uint64_t kEarlyZeroWidth = 64;      // rows this narrow get their zeros written up front
+constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
+// release/acquire, which on gfx950 also drains every wave's outstanding
+// global stores (s_waitcnt vmcnt(0)) -- measured as several us behind the
+// early zero-fill of the mask rows.  Nothing crossing these barriers is
+// global data, so only LDS (lgkmcnt) is drained.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct Plan {
+  uint32_t nb;               // bitmaps to OR
+  uint64_t off[kMaxPlan];    // word offsets of those bitmaps
+};
+
+// Canonical decomposition of [lo, hi) into two streamed partial ends plus the
+// maximal aligned bitmap blocks (B0*4^j rows at level j), computed by wave 0
+// with one lane per bitmap level: with a_j / b_j = x / y rounded up / down to
+// level-j alignment and `top` the highest level holding a whole block, level
+// j < top contributes [a_j, a_{j+1}) and [b_{j+1}, b_j), level top [a_top,
+// b_top) -- the same set the greedy left-to-right cover produces (<= 6 per level).
+__device__ void plan_range_wave(const DevView& v, uint64_t lo, uint64_t hi, int64_t follow, Plan& p) {
+  const uint32_t lane = threadIdx.x;   // called by the 64 lanes of wave 0
+  const uint32_t* one = nullptr;
+  if (lo == 0 && hi == v.n && v.bm_full)
+    one = v.bm_full;                                    // the whole BWT
+  else if (follow >= 0 && v.bm_follow)
+    one = v.bm_follow + (uint64_t)follow * v.bm_words;  // C-block of symbol `follow`
+  if (one) {                                            // one precomputed bitmap
+    if (lane == 0) {
+      p.nb = 1;
+      p.off[0] = (uint64_t)(one - v.bm);
+    }
+    return;
+  }
+  const uint32_t lg = v.bm_log2;
+  const uint64_t B0 = 1ull << lg;
+  bool split = v.bm_levels > 0 && hi - lo > B0;
+  uint64_t x = 0, y = 0;
+  if (split) {
+    x = (lo + B0 - 1) >> lg;
+    y = hi >> lg;
+    split = x < y;
+  }
+  if (lane == 0) p.nb = 0;
+  if (!split) return;
+  const uint32_t J = v.bm_levels;
+  const uint32_t j = lane;
+  uint64_t aj = 0, bj = 0, aj1 = 0, bj1 = 0;
+  bool valid = false;
+  if (j < J) {
+    const uint64_t s0 = 1ull << (2 * j), s1 = 1ull << (2 * (j + 1));
+    aj = (x + s0 - 1) & ~(s0 - 1);
+    bj = y & ~(s0 - 1);
+    aj1 = (x + s1 - 1) & ~(s1 - 1);
+    bj1 = y & ~(s1 - 1);
+    valid = aj < bj;
+  }
+  const uint64_t vb = __ballot(valid);
+  const uint32_t top = 63u - (uint32_t)__clzll(vb);
+  uint32_t cnt = 0;
+  if (j < top)
+    cnt = (uint32_t)(((aj1 - aj) + (bj - bj1)) >> (2 * j));
+  else if (j == top)
+    cnt = (uint32_t)((bj - aj) >> (2 * j));
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += t;
+  }
+  const uint32_t start = incl - cnt;
+  if (cnt) {
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < j; ++i) off += (v.bm_count[0] >> (2 * i)) * (uint64_t)v.bm_words;
+    const uint64_t s0 = 1ull << (2 * j);
+    uint32_t k = start;
+    if (j < top) {
+      for (uint64_t pos = aj; pos < aj1; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+      for (uint64_t pos = bj1; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+    } else {
+      for (uint64_t pos = aj; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+    }
+  }
+  if (j == top) p.nb = start + cnt;
+}
+
+// The streamed parts of plan_range_wave, derivable by every thread.
+__device__ __forceinline__ void stream_parts(const DevView& v, uint64_t lo, uint64_t hi, int64_t follow,
+                                             uint64_t& a0, uint64_t& b0, uint64_t& a1, uint64_t& b1) {
+  a0 = b0 = a1 = b1 = 0;
+  if ((lo == 0 && hi == v.n && v.bm_full) || (follow >= 0 && v.bm_follow)) return;
+  a0 = lo;
+  b0 = hi;
+  if (v.bm_levels == 0) return;
+  const uint32_t lg = v.bm_log2;
+  const uint64_t B0 = 1ull << lg;
+  if (hi - lo <= B0) return;
+  const uint64_t x = (lo + B0 - 1) >> lg, y = hi >> lg;
+  if (x >= y) return;
+  b0 = x << lg;
+  a1 = y << lg;
+  b1 = hi;
+}
+
+__device__ __forceinline__ int64_t floor_div32(int64_t x) { return x >= 0 ? x / 32 : -((-x + 31) / 32); }
+
+__device__ __forceinline__ void set_bit(uint32_t* win, uint32_t sym, int64_t base_bit, int64_t lim) {
+  const int64_t rel = (int64_t)sym - base_bit;
+  if (rel >= 0 && rel < lim) atomicOr(&win[rel >> 5], 1u << (rel & 31));
+}
+
+// Streamed parts of a range: BWT[a0, b0) and BWT[a1, b1).  Each part is an
+// unaligned head (< 4 symbols), a 16-B aligned middle read as uint4, and an
+// unaligned tail.  The first round's loads -- every head/tail symbol (threads
+// 0..11) and kUnroll uint4 per thread of the concatenated middles -- are all
+// issued before any is consumed, so a partial end of up to 16K symbols costs
+// one memory round trip.
+struct StreamParts {
+  uint64_t q0, n0, q1, n1;       // uint4 middles: [q0, q0+n0) and [q1, q1+n1)
+  uint64_t piece[4];             // head/tail start positions
+  uint32_t plen[4];              // head/tail lengths (0..3)
+};
+
+__device__ __forceinline__ void split_part(uint64_t a, uint64_t b, uint64_t& q, uint64_t& nq, uint64_t& h,
+                                           uint32_t& hl, uint64_t& t, uint32_t& tl) {
+  hl = tl = 0;
+  q = nq = 0;
+  h = t = 0;
+  if (a >= b) return;
+  const uint64_t a4 = (a + 3) & ~3ull, b4 = b & ~3ull;
+  if (a4 >= b4) {            // fewer than one aligned uint4: up to 6 symbols as head+tail
+    h = a;
+    hl = (uint32_t)min((uint64_t)3, b - a);
+    t = a + hl;
+    tl = (uint32_t)(b - t);
+    return;
+  }
+  h = a;
+  hl = (uint32_t)(a4 - a);
+  t = b4;
+  tl = (uint32_t)(b - b4);
+  q = a4 / 4;
+  nq = (b4 - a4) / 4;
+}
+
+__device__ __forceinline__ StreamParts make_parts(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1) {
+  StreamParts p;
+  split_part(a0, b0, p.q0, p.n0, p.piece[0], p.plen[0], p.piece[1], p.plen[1]);
+  split_part(a1, b1, p.q1, p.n1, p.piece[2], p.plen[2], p.piece[3], p.plen[3]);
+  return p;
+}
+
+__device__ __forceinline__ uint4 part_u4(const uint4* src, const StreamParts& p, uint64_t j) {
+  return src[j < p.n0 ? p.q0 + j : p.q1 + (j - p.n0)];
+}
+
+__device__ __forceinline__ void set_u4(uint32_t* win, const uint4& q, int64_t base_bit, int64_t lim) {
+  set_bit(win, q.x, base_bit, lim);
+  set_bit(win, q.y, base_bit, lim);
+  set_bit(win, q.z, base_bit, lim);
+  set_bit(win, q.w, base_bit, lim);
+}
+
+__device__ void stream_symbols(const uint32_t* __restrict__ bwt, const StreamParts& sp, int64_t base_bit,
+                               int64_t lim, uint32_t* win) {
+  const uint64_t ntot = sp.n0 + sp.n1;
+  const uint4* src = reinterpret_cast<const uint4*>(bwt);
+  uint32_t hsym = ~0u;          // head/tail symbols: threads 0..11, loaded with the first round
+  if (threadIdx.x < 12) {
+    const uint32_t pc = threadIdx.x / 3, k = threadIdx.x % 3;
+    if (k < sp.plen[pc]) hsym = bwt[sp.piece[pc] + k];
+  }
+  for (uint64_t base = threadIdx.x; base < ntot; base += (uint64_t)kDecThreads * kUnroll) {
+    uint4 q[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t j = base + (uint64_t)u * kDecThreads;
+      q[u] = (j < ntot) ? part_u4(src, sp, j) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (q[u].x != ~0u) set_u4(win, q[u], base_bit, lim);
+  }
+  if (hsym != ~0u) set_bit(win, hsym, base_bit, lim);
+}
+
+// blockIdx -> (row, slice).  Blocks b and b+8 share an XCD under round-robin
+// dispatch, so the S slices of a row are given blockIdx values congruent mod 8:
+// their redundant reads of the row's rank blocks / BWT / bitmaps share one L2.
+// Speed only; any placement is correct.
+__device__ __forceinline__ void map_block(uint32_t b, uint32_t S, uint64_t& row, uint32_t& slice) {
+  const uint32_t per = 8u * S;
+  const uint32_t r = b % per;
+  row = (uint64_t)(b / per) * 8 + (r & 7u);
+  slice = r >> 3;
+}
+
+// Buffer descriptor over [base, base + bytes) from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* b = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(b, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x) {
+  v4u v = {x.x, x.y, x.z, x.w};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
+}
+
+__device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t x) {
+  __builtin_amdgcn_raw_buffer_store_b32(x, r, off, 0, kStoreAux);
+}
+
+// 16 mask bits -> 16 bytes of 0/1
+__device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
+  uint32_t q[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = (((b >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u;
+  return make_uint4(q[0], q[1], q[2], q[3]);
+}
+
+// One workgroup = one vocab slice of one row.  With DO_LF the row's LF step
+// (or restart) is computed first by wave 0 (redundantly per slice; slice 0
+// publishes the new state), otherwise [lo_in, hi_in) is the range to mask.
+// Mask chunks: CH = 16 tokens (uint8 mask, one uint4 store) or 32 tokens
+// (packed, one uint32 store); chunk k of a slice is owned by one thread in
+// both the early zero-fill and the final emit.
+template <bool PACKED, bool DO_LF>
+__global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t* __restrict__ tok,
+                                                       int64_t shift, int64_t reset_below,
+                                                       const uint64_t* __restrict__ lo_in,
+                                                       const uint64_t* __restrict__ hi_in,
+                                                       uint64_t* __restrict__ lo_out,
+                                                       uint64_t* __restrict__ hi_out, uint64_t m,
+                                                       uint8_t* __restrict__ mask, uint64_t ld,
+                                                       uint64_t vocab, uint32_t S, uint32_t SW,
+                                                       uint64_t early_width) {
+  constexpr uint32_t CH = PACKED ? 32 : 16;
+  __shared__ Plan plan;
+  __shared__ uint64_t s_lohi[2];
+  __shared__ int64_t s_follow;
+  __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
+  FM_STAMP(v, 0);
+  // Materialise every kernel-argument field used later now, so their scalar
+  // loads issue together at entry instead of one cache-missing round trip
+  // per first use deep inside the dependent chain.
+  asm volatile("" ::"s"(v.n), "s"(v.nblk), "s"(v.nsb), "s"(v.wm), "s"(v.sb), "s"(v.Z), "s"(v.D), "s"(v.C));
+  asm volatile("" ::"s"(v.bwt), "s"(v.bm), "s"(v.bm_full), "s"(v.bm_follow), "s"(v.bm_count[0]),
+               "s"(v.L), "s"(v.NL), "s"(v.max_sym), "s"(v.bm_words), "s"(v.bm_levels), "s"(v.bm_log2));
+  uint64_t row;
+  uint32_t slice;
+  map_block(blockIdx.x, S, row, slice);
+  if (row >= m) return;
+  const uint64_t t0 = (uint64_t)slice * SW;
+  if (t0 >= vocab) return;
+  const uint64_t t1 = min(vocab, t0 + SW);
+  const uint64_t ntok = t1 - t0;
+  const uint64_t nch = (ntok + CH - 1) / CH;
+  uint8_t* out_row = mask + row * ld;
+  // Rows whose incoming range is narrow stay narrow after the LF step (it
+  // can only shrink a range), so their slice is zero-filled right away --
+  // the stores overlap the LF chain -- and the final pass rewrites only the
+  // chunks holding an allowed token.
+  bool early_zero;
+  {
+    const uint64_t l0 = lo_in[row], h0 = min(hi_in[row], v.n);
+    const bool reset = DO_LF && tok[row] < reset_below;
+    early_zero = !reset && (l0 >= h0 || h0 - l0 <= early_width);
+  }
+  const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
+  // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
+  const __amdgpu_buffer_rsrc_t orsrc =
+      make_rsrc(PACKED ? out_row + t0 / 8 : out_row + t0, (uint32_t)(PACKED ? (ntok + 31) / 32 * 4 : ntok));
+  FM_STAMP(v, 1);
+  // Zero-fill by waves 1.. only: loads and stores share vmcnt in issue order,
+  // so a wave with stores in flight cannot wait on a load without also
+  // waiting for them -- wave 0 (LF + plan) must stay store-free.
+  if (early_zero && threadIdx.x >= 64) {
+    for (uint64_t k = threadIdx.x - 64; k < nch; k += kDecThreads - 64) {
+      const uint64_t t = t0 + k * CH;
+      if (PACKED) {
+        store4(orsrc, (uint32_t)(k * 4), 0u);
+      } else if (aligned16 && t + CH <= t1) {
+        store16(orsrc, (uint32_t)(k * 16), make_uint4(0, 0, 0, 0));
+      } else {
+        for (uint64_t j = t; j < min(t1, t + CH); ++j) out_row[j] = 0;
+      }
+    }
+  }
+  FM_STAMP(v, 2);
+  // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
+  // (all 64 lanes), published with the range by a single barrier.
+  if (threadIdx.x < 64) {
+    uint64_t l = lo_in[row], h = hi_in[row];
+    int64_t follow = -1;
+    if (DO_LF) {
+      const int64_t t = tok[row];
+      if (t < reset_below) {
+        l = 0;
+        h = v.n;
+      } else {
+        // from the full range the LF step lands on symbol c's C-block, whose
+        // allowed set is c's precomputed follow-set bitmap
+        if (l == 0 && h >= v.n) follow = t + shift;
+        lf_step_w2(v, t + shift, l, h);
+        if (l >= h) follow = -1;
+      }
+      if (slice == 0 && threadIdx.x == 0) {
+        lo_out[row] = l;
+        hi_out[row] = h;
+      }
+    }
+    l = __shfl(l, 0, 64);
+    h = __shfl(h, 0, 64);
+    follow = __shfl(follow, 0, 64);
+    if (h > v.n) h = v.n;
+    if (threadIdx.x == 0) {
+      s_lohi[0] = l;
+      s_lohi[1] = h;
+      s_follow = follow;
+      plan.nb = 0;
+    }
+    if (l < h) plan_range_wave(v, l, h, follow, plan);
+  }
+  // LDS window over symbol space, 128-bit aligned: words [w_lo, w_lo + nwin)
+  const int64_t w_lo = floor_div32((int64_t)t0 + shift) & ~(int64_t)3;
+  const int64_t sym_end = (int64_t)t1 + shift + 64;
+  const uint32_t nwin = (uint32_t)(((sym_end - w_lo * 32 + 31) / 32 + 3) & ~3ll);
+  for (uint32_t w = threadIdx.x; w < nwin; w += kDecThreads) win[w] = 0;
+  lds_barrier();
+  const uint64_t lo = s_lohi[0], hi = s_lohi[1];
+  FM_STAMP(v, 3);
+  if (lo < hi) {
+    // streamed partial ends, then bitmap ORs; one barrier after
+    const int64_t base_bit = w_lo * 32;
+    const int64_t lim = (int64_t)nwin * 32;
+    // The first batch of bitmap words (<= 8 per thread) is loaded before the
+    // partial ends are streamed, so both are in flight in one round trip.
+    const uint32_t nb = plan.nb;
+    const uint32_t nw4 = nwin / 4;
+    const uint32_t G = max(1u, (uint32_t)kDecThreads / nw4);   // thread groups splitting the bitmaps
+    const uint32_t g = threadIdx.x / nw4;
+    uint32_t w4b = threadIdx.x % nw4;
+    int64_t gwb = w_lo + 4 * (int64_t)w4b;
+    bool own = nb && g < G && w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
+    uint4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t qq = g + (uint32_t)u * G;
+      x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(v.bm + plan.off[qq] + gwb) : make_uint4(0, 0, 0, 0);
+    }
+    uint64_t a0, b0, a1, b1;
+    stream_parts(v, lo, hi, s_follow, a0, b0, a1, b1);
+    stream_symbols(v.bwt, make_parts(a0, b0, a1, b1), base_bit, lim, win);
+    FM_STAMP(v, 4);
+    // G groups split the bitmaps, each thread owns one uint4 of the window
+    // (several when the window is wider than the workgroup); partial ORs
+    // merge with LDS atomics.
+    bool first = true;
+    while (nb && g < G && w4b < nw4) {
+      if (own) {
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t q = g; q < nb; q += G * 8) {
+          if (!first) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const uint32_t qq = q + (uint32_t)u * G;
+              x[u] = qq < nb ? *reinterpret_cast<const uint4*>(v.bm + plan.off[qq] + gwb) : make_uint4(0, 0, 0, 0);
+            }
+          }
+          first = false;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            acc.x |= x[u].x;
+            acc.y |= x[u].y;
+            acc.z |= x[u].z;
+            acc.w |= x[u].w;
+          }
+        }
+        if (acc.x) atomicOr(&win[4 * w4b + 0], acc.x);
+        if (acc.y) atomicOr(&win[4 * w4b + 1], acc.y);
+        if (acc.z) atomicOr(&win[4 * w4b + 2], acc.z);
+        if (acc.w) atomicOr(&win[4 * w4b + 3], acc.w);
+      }
+      first = false;
+      w4b += kDecThreads;
+      gwb = w_lo + 4 * (int64_t)w4b;
+      own = w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
+    }
+    FM_STAMP(v, 5);
+    lds_barrier();
+  }
+  FM_STAMP(v, 6);
+  // the final stores to an early-zeroed chunk must land after its zero store
+  // (same thread, same address): drain this wave's outstanding stores first
+  if (early_zero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
+  const uint32_t e_first = early_zero ? 64u : 0u;
+  if (threadIdx.x >= e_first) {
+    for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
+      const int64_t rel = rel0 + (int64_t)k * CH;
+      const uint32_t wi = (uint32_t)(rel >> 5);
+      const uint32_t o = (uint32_t)(rel & 31);
+      const uint64_t w2 = (uint64_t)win[wi] | ((uint64_t)win[wi + 1] << 32);
+      uint32_t bits = (uint32_t)(w2 >> o);
+      const uint64_t t = t0 + k * CH;
+      const uint64_t cnt = min((uint64_t)CH, t1 - t);
+      if (CH == 16) bits &= 0xFFFFu;
+      if (cnt < CH) bits &= (1u << cnt) - 1u;
+      if (early_zero && bits == 0) continue;
+      if (PACKED) {
+        store4(orsrc, (uint32_t)(k * 4), bits);   // t0 and t are multiples of 32
+      } else if (aligned16 && cnt == 16) {
+        store16(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits));
+      } else {
+        for (uint64_t j = 0; j < cnt; ++j) out_row[t + j] = (uint8_t)((bits >> j) & 1u);
+      }
+    }
+  }
+  FM_STAMP(v, 7);
+}
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* s = std::getenv(name);
+  if (!s || !*s) return dflt;
+  return (uint32_t)std::strtoul(s, nullptr, 10);
+}
+
+}  // namespace
+
+// Slice geometry.  Residency budget: kernels of this shape keep about 16 waves
+// per CU resident (measured, profiles/r01_tuning); a launch of more waves than
+// budget dispatches its tail only as earlier workgroups retire.  So the slices
+// per row are chosen to keep rows * S * 16 waves within the budget (default
+// one slice per row at B >= 256), slices a multiple of 64 tokens.
+static void mask_geometry(uint64_t m, uint64_t vocab, uint32_t& S, uint32_t& SW) {
+  uint32_t s = env_u32("FMIDX_MASK_SLICES", 0);
+  const uint64_t s_min = (vocab + kMaxSliceTokens - 1) / kMaxSliceTokens;
+  if (s == 0) {
+    const uint64_t rows = (m + 7) / 8 * 8;
+    const uint64_t budget = env_u32("FMIDX_WAVE_BUDGET", 4096);
+    const uint64_t want = std::max<uint64_t>(1, budget / (rows * (kDecThreads / 64)));
+    const uint64_t max_s = std::max<uint64_t>(1, (vocab + 8191) / 8192);
+    s = (uint32_t)std::min(want, max_s);
+  }
+  s = (uint32_t)std::max<uint64_t>(s, std::max<uint64_t>(1, s_min));
+  uint64_t sw = (vocab + s - 1) / s;
+  sw = (sw + 63) & ~63ull;
+  if (sw > kMaxSliceTokens) sw = kMaxSliceTokens;
+  SW = (uint32_t)sw;
+  S = (uint32_t)((vocab + sw - 1) / sw);
+}
+
+static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t shift,
+                                int64_t reset_below, const uint64_t* lo_in, const uint64_t* hi_in,
+                                uint64_t* lo_out, uint64_t* hi_out, uint64_t m, uint8_t* mask,
+                                uint64_t ld, uint64_t vocab, int packed, bool do_lf, hipStream_t s) {
+  if (packed && (ld % 4 != 0 || ld < 4 * ((vocab + 31) / 32) ||
+                 (reinterpret_cast<uintptr_t>(mask) & 3))) {
+    set_error("packed mask needs 4-byte aligned rows with ld >= 4*ceil(vocab/32)");
+    return -1;
+  }
+  if (!packed && ld < vocab) {
+    set_error("mask leading dimension %llu < vocab %llu", (unsigned long long)ld,
+              (unsigned long long)vocab);
+    return -1;
+  }
+  uint32_t S, SW;
+  mask_geometry(m, vocab, S, SW);
+  const uint64_t grid = (m + 7) / 8 * 8 * S;
+  if (grid > 0x7fffffffull / kDecThreads) {
+    set_error("too many rows for one launch");
+    return -1;
+  }
+  const unsigned g = (unsigned)grid;
+  static const uint64_t ew = [] {
+    const char* e = std::getenv("FMIDX_EARLY_ZERO_WIDTH");
+    return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
+  }();
+#define FM_LAUNCH(P, L)                                                                                       \
+  k_decode<P, L><<<g, kDecThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, mask, \
+                                           ld, vocab, S, SW, ew)
+  if (do_lf) {
+    if (packed) FM_LAUNCH(true, true);
+    else FM_LAUNCH(false, true);
+  } else {
+    if (packed) FM_LAUNCH(true, false);
+    else FM_LAUNCH(false, false);
+  }
+#undef FM_LAUNCH
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
+                uint8_t* mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
+                hipStream_t s) {
+  if (m == 0 || vocab == 0) return 0;
+  return launch_decode_kernel(v, nullptr, shift, 0, lo, hi, nullptr, nullptr, m, mask, ld, vocab, packed,
+                              false, s);
+}
+
+// Follow-set bitmaps: row c = packed mask (symbol space, shift 0) of the
+// C-block [C[c], C[c+1]) -- exactly the bitmap layout plan_range_wave reads.
+int launch_follow_bitmaps(const DevView& v, const uint64_t* C, uint64_t nsym, uint32_t* out,
+                          hipStream_t s) {
+  const uint64_t ld = (uint64_t)v.bm_words * 4;
+  const uint64_t chunk = 32768;   // rows per launch
+  for (uint64_t c0 = 0; c0 < nsym; c0 += chunk) {
+    const uint64_t m = std::min(chunk, nsym - c0);
+    if (launch_decode_kernel(v, nullptr, 0, 0, C + c0, C + c0 + 1, nullptr, nullptr, m,
+                             reinterpret_cast<uint8_t*>(out + c0 * v.bm_words), ld,
+                             (uint64_t)v.bm_words * 32, 1, false, s))
+      return -1;
+  }
+  return 0;
+}
+
+int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
+                  const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                  uint64_t m, uint8_t* mask, uint64_t ld, uint64_t vocab, int packed, hipStream_t s) {
+  if (m == 0) return 0;
+  if (vocab == 0)   // LF only: the per-row kernel is safe in place
+    return launch_lf_step(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, s);
+  if (lo_in == lo_out || hi_in == hi_out) {
+    set_error("fused decode step: state in/out buffers must not alias (ping-pong them)");
+    return -1;
+  }
+  return launch_decode_kernel(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, mask, ld, vocab,
+                              packed, true, s);
+}
+
+}  // namespace fmidx

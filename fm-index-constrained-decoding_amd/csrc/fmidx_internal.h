@@ -40,6 +40,25 @@ constexpr int kBlkDigits = 192;        // digits per 128-B rank block
 constexpr int kBlkU4 = 8;              // uint4 per rank block
 constexpr int kSbBlocks = 341;         // blocks per superblock (65472 digits < 2^16)
 constexpr int kMaxBmLevels = 24;
+// 2-level wavelet matrix (the LF path): digits of <= 9 bits, so L <= 18 bits
+// in 2 levels (17 = 9 + 8 for a 128k vocabulary + SHIFT), <= 27 in 3.
+constexpr int kW2MaxLevels = 3;
+constexpr int kW2BlkLog2 = 10;                 // 1024 digits per rank block
+constexpr int kW2Blk = 1 << kW2BlkLog2;
+constexpr int kW2SbLog2 = 16;                  // 64 blocks per superblock (u16 block headers)
+
+// One level of the 2-level wavelet matrix.  Block b (digits [1024 b, 1024 b +
+// 1024)) = [R x uint16 count of each digit before the block, relative to its
+// superblock][1024 digits as uint8 (bits <= 8) or uint16].  rank_d(i) = sb +
+// header[d] + matches of d in the block's first i mod 1024 digits: three
+// independent loads, one round trip.
+struct W2Level {
+  const uint8_t* blocks;      // nblk2 * blk_bytes
+  const uint64_t* sb;         // [nsb2][R] absolute counts before each superblock
+  const uint64_t* Z;          // [R] digits < d in this level
+  uint64_t blk_bytes;         // 2R + 1024 * digit bytes
+  uint32_t bits, shift;       // digit = (c >> shift) & (R - 1)
+};
 
 // Everything a kernel needs, passed by value as a kernel argument.
 struct DevView {
@@ -57,6 +76,9 @@ struct DevView {
   const uint32_t* bm_follow;  // per symbol c: bitmap of BWT[C[c], C[c+1]) (follow set), or null
   uint64_t bm_off[kMaxBmLevels];   // word offset of each bitmap level
   uint64_t bm_count[kMaxBmLevels]; // bitmaps per level
+  W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
+  const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
+  uint32_t NL2;               // its levels (0 = not built)
   uint32_t L;                 // symbol bits
   uint32_t NL;                // digit levels
   uint32_t max_sym;           // largest symbol value present
@@ -205,6 +227,119 @@ __device__ __forceinline__ void descend_full(const DevView& v, uint32_t c, uint6
 }
 
 // ---------------------------------------------------------------------------
+// 2-level wavelet matrix rank / LF, computed by 32 lanes (q = lane & 31): lane
+// q covers digits [32 q, 32 q + 32) of the block (64 B of uint16 or 32 B of
+// uint8 digits), the partial counts meet in an xor-shuffle tree.
+__device__ __forceinline__ uint32_t eq16_count(uint32_t w, uint32_t dd, uint32_t valid2) {
+  const uint32_t x = w ^ dd;   // dd = d | d << 16
+  return ((valid2 & 1u) && (x & 0xFFFFu) == 0) + ((valid2 & 2u) && (x >> 16) == 0);
+}
+
+__device__ __forceinline__ uint32_t eq8_count(uint32_t w, uint32_t dd, uint32_t nvalid) {
+  const uint32_t x = w ^ dd;   // dd = d * 0x01010101
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) c += (j < nvalid) && ((x >> (8 * j)) & 0xFFu) == 0;
+  return c;
+}
+
+__device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
+  const uint64_t b = i >> kW2BlkLog2;
+  const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
+  const uint8_t* base = L.blocks + b * L.blk_bytes;
+  const uint32_t R = 1u << L.bits;
+  const uint64_t sbv = L.sb[(i >> kW2SbLog2) * R + d];
+  const uint32_t hdr = reinterpret_cast<const uint16_t*>(base)[d];
+  const uint32_t first = 32 * q;   // first digit of this lane
+  uint32_t cnt = 0;
+  if (L.bits > 8) {
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
+    uint4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = (first + 8 * u < k) ? p[u] : make_uint4(0, 0, 0, 0);
+    const uint32_t dd = d | (d << 16);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j0 = first + 8 * u;   // digits j0 .. j0+7
+      if (j0 >= k) continue;
+      const uint32_t nv = min(8u, k - j0);
+      cnt += eq16_count(x[u].x, dd, nv >= 2 ? 3u : (nv >= 1 ? 1u : 0u));
+      cnt += eq16_count(x[u].y, dd, nv >= 4 ? 3u : (nv >= 3 ? 1u : 0u));
+      cnt += eq16_count(x[u].z, dd, nv >= 6 ? 3u : (nv >= 5 ? 1u : 0u));
+      cnt += eq16_count(x[u].w, dd, nv >= 8 ? 3u : (nv >= 7 ? 1u : 0u));
+    }
+  } else {
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 2 * q;
+    uint4 x[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) x[u] = (first + 16 * u < k) ? p[u] : make_uint4(0, 0, 0, 0);
+    const uint32_t dd = d * 0x01010101u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j0 = first + 16 * u;
+      if (j0 >= k) continue;
+      const uint32_t nv = min(16u, k - j0);
+      cnt += eq8_count(x[u].x, dd, nv >= 4 ? 4u : nv);
+      cnt += eq8_count(x[u].y, dd, nv >= 8 ? 4u : (nv > 4 ? nv - 4 : 0u));
+      cnt += eq8_count(x[u].z, dd, nv >= 12 ? 4u : (nv > 8 ? nv - 8 : 0u));
+      cnt += eq8_count(x[u].w, dd, nv >= 16 ? 4u : (nv > 12 ? nv - 12 : 0u));
+    }
+  }
+  cnt += __shfl_xor(cnt, 1, 64);
+  cnt += __shfl_xor(cnt, 2, 64);
+  cnt += __shfl_xor(cnt, 4, 64);
+  cnt += __shfl_xor(cnt, 8, 64);
+  cnt += __shfl_xor(cnt, 16, 64);
+  return sbv + hdr + cnt;
+}
+
+// One reference backward_search_step on a half-open state (fm_index.cpp:67-97
+// as driven by index.py:110) over the 2-level wavelet matrix, by all 64 lanes
+// of a wave (lanes 0-31 rank the low end, 32-63 the high end): NL2 (= 2 for
+// a 128k vocabulary) dependent round trips.  (0,0) = empty in and out; every
+// lane receives the result.
+__device__ __forceinline__ void lf_step_w2(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
+  if (hi > v.n) hi = v.n;                    // high clamp (fm_index.cpp:74-76)
+  if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {  // low > high / unknown symbol
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  const uint32_t c = (uint32_t)sym;
+  if (lo == 0 && hi == v.n) {                // [sdsl] backward_search full-range case
+    const uint64_t a = v.C[c], b = v.C[c + 1];
+    lo = a < b ? a : 0;
+    hi = a < b ? b : 0;
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
+  // level-independent loads first: all in flight with the first rank
+  const int64_t dd = v.D2[c];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  uint64_t pos = side ? hi : lo;
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l) {
+    if (l >= (int)v.NL2) break;
+    const uint32_t d = (c >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    pos = z[l] + rank_w2(v.w2[l], pos, d, q);
+  }
+  const uint64_t other = __shfl_xor(pos, 32, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
+// ---------------------------------------------------------------------------
 // host-side owner of the device structures
 struct Index {
   int device = 0;
@@ -225,9 +360,13 @@ struct Index {
   uint32_t* bm = nullptr;
   uint32_t* bm_full = nullptr;
   uint32_t* bm_follow = nullptr;
+  uint8_t* w2_blocks[kW2MaxLevels] = {nullptr, nullptr, nullptr};
+  uint64_t* w2_sb[kW2MaxLevels] = {nullptr, nullptr, nullptr};
+  uint64_t* w2_Z = nullptr;
+  int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;
   uint32_t* text = nullptr;
-  uint64_t wm_bytes = 0, bm_bytes = 0, follow_bytes = 0;
+  uint64_t wm_bytes = 0, bm_bytes = 0, follow_bytes = 0, w2_bytes = 0;
   // grow-only workspace for batched traversals
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -237,6 +376,7 @@ struct Index {
 
 // build.hip
 int device_build_from_bwt(Index* h, const uint32_t* d_bwt_owned, uint64_t n, hipStream_t s);
+int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
 int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s,
                        uint64_t* d_total);
 

@@ -122,6 +122,8 @@ def test_swig_surface_errors(dev):
     (3, 300, 128256, 80, 7),
     (4, 120, 5, 200, 5),
     (5, 400, 2000, 150, None),
+    (6, 150, 1 << 20, 60, 6),     # 21-bit symbols: 3-level LF wavelet matrix
+    (7, 300, 246, 90, 6),         # 8-bit symbols: one uint8 LF level
 ])
 def test_random_corpora_vs_oracle(dev, seed, n_docs, vocab, max_len, bm):
     import torch

@@ -18,17 +18,18 @@ from fmidx._lib import lib  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 V, B, W = 128256, 256, 5
-fm, text, bwt, _ = build_index(int(float(os.environ.get("TOKENS", "3e8"))), V, 20250905, dev)
+fm, text, bwt, _ = build_index(int(float(os.environ.get("TOKENS", "4.5e9"))), V, 20250905, dev)
 n = bwt.numel()
 tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, W + 12, 20250905, dev)
 dl = lib()
 dl.fm_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
-T = int(os.environ.get("MASK_THREADS", "256"))
-want = max(1, int(os.environ.get("FMIDX_WAVE_BUDGET", "4096")) // (((B + 7) // 8 * 8) * (T // 64)))
-S0 = min(want, max(1, (V + 1023) // 1024))
-SW = int(os.environ.get("FMIDX_MASK_SW", "0")) or ((V + S0 - 1) // S0)
-SW = min(32768, (SW + 31) & ~31)
+T = 512                        # kDecThreads (decode.hip)
+S = int(os.environ.get("FMIDX_MASK_SLICES", "0"))
+if S == 0:                     # mirrors mask_geometry() in decode.hip
+    want = max(1, int(os.environ.get("FMIDX_WAVE_BUDGET", "4096")) // (((B + 7) // 8 * 8) * (T // 64)))
+    S = min(want, max(1, (V + 8191) // 8192))
+SW = min(262144, (((V + S - 1) // S) + 63) & ~63)
 S = (V + SW - 1) // SW
 grid = (B + 7) // 8 * 8 * S
 stamps = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
