@@ -116,16 +116,17 @@ def make_trace(fm, text, bwt, B: int, V: int, S: int, seed: int, dev):
 
 
 def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int,
-               follow=None):
-    """Bytes the mask algorithm must read per row: streamed BWT symbols (4 B)
-    + whole range bitmaps (mirrors plan_range_wave in query.hip)."""
+               follow=None, cached=None):
+    """Bytes the mask algorithm must read per row: one cached range bitmap,
+    or streamed BWT symbols (4 B) + whole aligned bitmaps (mirrors the plan
+    of k_decode in decode.hip)."""
     B0 = 1 << b0_log2
     out = np.zeros(lo.size, dtype=np.int64)
     for i, (l, h) in enumerate(zip(lo.tolist(), hi.tolist())):
         h = min(h, n)
         if l >= h:
             continue
-        if (l == 0 and h == n) or (follow is not None and follow[i]):
+        if (cached is not None and cached[i]) or (l == 0 and h == n) or (follow is not None and follow[i]):
             out[i] = bm_bytes_each            # one precomputed bitmap (full range / follow set)
             continue
         if bm_levels == 0 or h - l <= B0:
@@ -349,7 +350,9 @@ def main():
     prev_hi = np.concatenate([hi_hist[W - 1:W].cpu().numpy(), hi_np[:-1]])
     tok_np = tokens[W:S].cpu().numpy()
     follow = (prev_lo == 0) & (prev_hi >= n) & (tok_np >= 0) & (st.get("follow_bytes", 0) > 0)
-    read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4, follow[i])
+    cached = fm.cache_contains(lo_hist[W:S].reshape(-1).contiguous(),
+                               hi_hist[W:S].reshape(-1).contiguous()).view(K, B).cpu().numpy()
+    read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4, follow[i], cached[i])
                            for i in range(K)])
     mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
     mask_us = float(np.median(mask_ms)) * 1e3
@@ -368,7 +371,9 @@ def main():
     log(f"step {step_ms * 1e3:.1f}us [reps {', '.join(f'{t / K * 1e3:.1f}' for t in step_reps)}] "
         f"(standalone lf {lf_us:.1f}us, mask {mask_us:.1f}us, wall/step {wall / K * 1e6:.1f}us, graph) "
         f"bytes/step {decode_bytes / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
-        f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}")
+        f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}, "
+        f"cached rows {cached.mean():.3f} (cache: {st['cache_nodes']} ranges >= {st['cache_min']}, "
+        f"{st['cache_bytes'] / 2**30:.1f} GiB)")
 
     result = {
         "metric": METRIC,

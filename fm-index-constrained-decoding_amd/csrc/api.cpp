@@ -41,6 +41,11 @@ void Index::release() {
     w2_sb[l] = nullptr;
   }
   if (w2_Z) (void)hipFree(w2_Z);
+  if (cache_bm) (void)hipFree(cache_bm);
+  if (cache_tab) (void)hipFree(cache_tab);
+  cache_bm = nullptr;
+  cache_tab = nullptr;
+  cache_nodes = cache_bytes = 0;
   if (D2) (void)hipFree(D2);
   w2_Z = nullptr;
   D2 = nullptr;
@@ -753,6 +758,25 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
   if (bitmap_bytes) *bitmap_bytes = x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0);
   if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;
   return 0;
+}
+
+int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint64_t* cache_nodes,
+                uint64_t* cache_bytes, uint64_t* cache_min) {
+  FM_CHECK_BUILT(h);
+  const auto& x = h->idx;
+  if (w2_levels) *w2_levels = x.view.NL2;
+  if (w2_bytes) *w2_bytes = x.w2_bytes;
+  if (cache_nodes) *cache_nodes = x.cache_nodes;
+  if (cache_bytes) *cache_bytes = x.cache_bytes;
+  if (cache_min) *cache_min = x.view.cache_mask ? x.view.cache_min : 0;
+  return 0;
+}
+
+int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
+                          void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_cache_probe(h->idx.view, d_lo, d_hi, m, d_out, reinterpret_cast<hipStream_t>(stream));
 }
 
 int fm_device_bwt(const fm_index* h, const uint32_t** out) {

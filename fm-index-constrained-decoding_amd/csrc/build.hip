@@ -545,7 +545,9 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   v.bm_log2 = log2b0;
   // -- follow-set bitmaps (one per symbol's C-block), built with the mask
   //    kernel itself once the view above is complete
-  if (bm_ok && env_u32("FMIDX_FOLLOW_BITMAPS", 1) != 0) {
+  // (off by default: the range-bitmap cache below holds every C-block of
+  // width >= its threshold, and narrower ones are streamed)
+  if (bm_ok && env_u32("FMIDX_FOLLOW_BITMAPS", 0) != 0) {
     const uint64_t nsym = (uint64_t)max_sym + 1;
     uint32_t* fb = nullptr;
     if (dmalloc(&fb, nsym * words)) return -1;
@@ -556,6 +558,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     v.bm_follow = fb;
   }
   if (device_build_w2(h, d_bwt, n, s)) return -1;
+  if (device_build_cache(h, s)) return -1;
   h->built = true;
   return 0;
 }

@@ -55,8 +55,9 @@ constexpr int kUnroll = 4;                    // uint4 loads in flight per threa
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 struct Plan {
-  uint32_t nb;               // bitmaps to OR
-  uint64_t off[kMaxPlan];    // word offsets of those bitmaps
+  uint64_t a0, b0, a1, b1;            // streamed BWT row ranges (partial ends / narrow range)
+  uint32_t nb;                        // bitmaps to OR
+  const uint32_t* ptr[kMaxPlan];      // those bitmaps
 };
 
 // Canonical decomposition of [lo, hi) into two streamed partial ends plus the
@@ -75,7 +76,8 @@ __device__ void plan_range_wave(const DevView& v, uint64_t lo, uint64_t hi, int6
   if (one) {                                            // one precomputed bitmap
     if (lane == 0) {
       p.nb = 1;
-      p.off[0] = (uint64_t)(one - v.bm);
+      p.ptr[0] = one;
+      p.a0 = p.b0 = p.a1 = p.b1 = 0;
     }
     return;
   }
@@ -88,7 +90,13 @@ __device__ void plan_range_wave(const DevView& v, uint64_t lo, uint64_t hi, int6
     y = hi >> lg;
     split = x < y;
   }
-  if (lane == 0) p.nb = 0;
+  if (lane == 0) {
+    p.nb = 0;
+    p.a0 = lo;
+    p.b0 = split ? (x << lg) : hi;
+    p.a1 = split ? (y << lg) : 0;
+    p.b1 = split ? hi : 0;
+  }
   if (!split) return;
   const uint32_t J = v.bm_levels;
   const uint32_t j = lane;
@@ -122,31 +130,13 @@ __device__ void plan_range_wave(const DevView& v, uint64_t lo, uint64_t hi, int6
     const uint64_t s0 = 1ull << (2 * j);
     uint32_t k = start;
     if (j < top) {
-      for (uint64_t pos = aj; pos < aj1; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
-      for (uint64_t pos = bj1; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+      for (uint64_t pos = aj; pos < aj1; pos += s0) p.ptr[k++] = v.bm + off + (pos >> (2 * j)) * v.bm_words;
+      for (uint64_t pos = bj1; pos < bj; pos += s0) p.ptr[k++] = v.bm + off + (pos >> (2 * j)) * v.bm_words;
     } else {
-      for (uint64_t pos = aj; pos < bj; pos += s0) p.off[k++] = off + (pos >> (2 * j)) * v.bm_words;
+      for (uint64_t pos = aj; pos < bj; pos += s0) p.ptr[k++] = v.bm + off + (pos >> (2 * j)) * v.bm_words;
     }
   }
   if (j == top) p.nb = start + cnt;
-}
-
-// The streamed parts of plan_range_wave, derivable by every thread.
-__device__ __forceinline__ void stream_parts(const DevView& v, uint64_t lo, uint64_t hi, int64_t follow,
-                                             uint64_t& a0, uint64_t& b0, uint64_t& a1, uint64_t& b1) {
-  a0 = b0 = a1 = b1 = 0;
-  if ((lo == 0 && hi == v.n && v.bm_full) || (follow >= 0 && v.bm_follow)) return;
-  a0 = lo;
-  b0 = hi;
-  if (v.bm_levels == 0) return;
-  const uint32_t lg = v.bm_log2;
-  const uint64_t B0 = 1ull << lg;
-  if (hi - lo <= B0) return;
-  const uint64_t x = (lo + B0 - 1) >> lg, y = hi >> lg;
-  if (x >= y) return;
-  b0 = x << lg;
-  a1 = y << lg;
-  b1 = hi;
 }
 
 __device__ __forceinline__ int64_t floor_div32(int64_t x) { return x >= 0 ? x / 32 : -((-x + 31) / 32); }
@@ -289,7 +279,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
   __shared__ uint64_t s_lohi[2];
-  __shared__ int64_t s_follow;
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   FM_STAMP(v, 0);
   // Materialise every kernel-argument field used later now, so their scalar
@@ -338,7 +327,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
       }
     }
   }
-  FM_STAMP(v, 2);
   // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
   // (all 64 lanes), published with the range by a single barrier.
   if (threadIdx.x < 64) {
@@ -355,6 +343,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
         if (l == 0 && h >= v.n) follow = t + shift;
         lf_step_w2(v, t + shift, l, h);
         if (l >= h) follow = -1;
+        FM_STAMP(v, 2);
       }
       if (slice == 0 && threadIdx.x == 0) {
         lo_out[row] = l;
@@ -368,10 +357,22 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
     if (threadIdx.x == 0) {
       s_lohi[0] = l;
       s_lohi[1] = h;
-      s_follow = follow;
       plan.nb = 0;
+      plan.a0 = plan.b0 = plan.a1 = plan.b1 = 0;
     }
-    if (l < h) plan_range_wave(v, l, h, follow, plan);
+    if (l < h) {
+      // a wide range is looked up in the range-bitmap cache first (one
+      // bitmap, nothing streamed); otherwise the aligned-bitmap plan
+      const uint32_t* cb = cache_find(v, l, h);
+      if (cb) {
+        if (threadIdx.x == 0) {
+          plan.nb = 1;
+          plan.ptr[0] = cb;
+        }
+      } else {
+        plan_range_wave(v, l, h, follow, plan);
+      }
+    }
   }
   // LDS window over symbol space, 128-bit aligned: words [w_lo, w_lo + nwin)
   const int64_t w_lo = floor_div32((int64_t)t0 + shift) & ~(int64_t)3;
@@ -398,11 +399,9 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t qq = g + (uint32_t)u * G;
-      x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(v.bm + plan.off[qq] + gwb) : make_uint4(0, 0, 0, 0);
+      x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
     }
-    uint64_t a0, b0, a1, b1;
-    stream_parts(v, lo, hi, s_follow, a0, b0, a1, b1);
-    stream_symbols(v.bwt, make_parts(a0, b0, a1, b1), base_bit, lim, win);
+    stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win);
     FM_STAMP(v, 4);
     // G groups split the bitmaps, each thread owns one uint4 of the window
     // (several when the window is wider than the workgroup); partial ORs
@@ -416,7 +415,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const uint32_t qq = q + (uint32_t)u * G;
-              x[u] = qq < nb ? *reinterpret_cast<const uint4*>(v.bm + plan.off[qq] + gwb) : make_uint4(0, 0, 0, 0);
+              x[u] = qq < nb ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
             }
           }
           first = false;
@@ -469,6 +468,17 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
     }
   }
   FM_STAMP(v, 7);
+}
+
+// cache probe per row (one wave each): 1 if [lo, hi) has a cached bitmap
+__global__ void __launch_bounds__(256) k_cache_probe(DevView v, const uint64_t* __restrict__ lo,
+                                                    const uint64_t* __restrict__ hi, uint64_t m,
+                                                    uint8_t* __restrict__ out) {
+  const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (i >= m) return;
+  const uint64_t l = lo[i], h = min(hi[i], v.n);
+  const bool hit = l < h && cache_find(v, l, h) != nullptr;
+  if ((threadIdx.x & 63u) == 0) out[i] = hit ? 1 : 0;
 }
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -539,6 +549,14 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     else FM_LAUNCH(false, false);
   }
 #undef FM_LAUNCH
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_cache_probe(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m, uint8_t* out,
+                       hipStream_t s) {
+  if (m == 0) return 0;
+  k_cache_probe<<<(unsigned)((m * 64 + 255) / 256), 256, 0, s>>>(v, lo, hi, m, out);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -76,6 +76,12 @@ struct DevView {
   const uint32_t* bm_follow;  // per symbol c: bitmap of BWT[C[c], C[c+1]) (follow set), or null
   uint64_t bm_off[kMaxBmLevels];   // word offset of each bitmap level
   uint64_t bm_count[kMaxBmLevels]; // bitmaps per level
+  // range-bitmap cache: the bitmap of every SA range reachable from the root
+  // by LF steps with width >= cache_min (suffix-tree nodes), found by (lo, hi)
+  const uint32_t* cache_bm;   // [nodes][bm_words]
+  const uint64_t* cache_tab;  // [cap][2] = {lo, hi | id << 34}; lo = ~0: empty
+  uint64_t cache_mask;        // cap - 1 (cap a power of 2); 0 = no cache
+  uint64_t cache_min;         // width threshold Wc
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
   uint32_t NL2;               // its levels (0 = not built)
@@ -340,6 +346,46 @@ __device__ __forceinline__ void lf_step_w2(const DevView& v, int64_t sym, uint64
 }
 
 // ---------------------------------------------------------------------------
+// range-bitmap cache lookup
+__host__ __device__ __forceinline__ uint64_t cache_hash(uint64_t lo, uint64_t hi) {
+  uint64_t x = lo * 0x9E3779B97F4A7C15ull ^ (hi + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+  x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ull;
+  return x ^ (x >> 32);
+}
+
+constexpr uint64_t kCacheEmpty = ~0ull;
+constexpr uint32_t kCacheIdShift = 34;
+
+// Bitmap of [lo, hi) if cached, else null.  Called by all 64 lanes of a wave
+// with uniform (lo, hi): lanes 0-15 read 16 consecutive probe slots (256 B) per
+// round; linear probing stops at the first empty slot.
+__device__ __forceinline__ const uint32_t* cache_find(const DevView& v, uint64_t lo, uint64_t hi) {
+  if (!v.cache_mask || hi - lo < v.cache_min) return nullptr;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t slot = cache_hash(lo, hi) & v.cache_mask;
+  for (int round = 0; round < 64; ++round) {
+    uint64_t klo = kCacheEmpty, khi = 0;
+    if (lane < 16) {
+      const uint64_t* e = v.cache_tab + 2 * ((slot + lane) & v.cache_mask);
+      klo = e[0];
+      khi = e[1];
+    }
+    const bool hit = lane < 16 && klo == lo && (khi & ((1ull << kCacheIdShift) - 1)) == hi;
+    const bool empty = lane < 16 && klo == kCacheEmpty;
+    const uint64_t bh = __ballot(hit), be = __ballot(empty);
+    if (bh && (!be || __ffsll((long long)bh) < __ffsll((long long)be))) {
+      const uint32_t src = (uint32_t)__ffsll((long long)bh) - 1;
+      const uint64_t id = __shfl(khi, (int)src, 64) >> kCacheIdShift;
+      return v.cache_bm + id * v.bm_words;
+    }
+    if (be) return nullptr;
+    slot += 16;
+  }
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------
 // host-side owner of the device structures
 struct Index {
   int device = 0;
@@ -363,6 +409,9 @@ struct Index {
   uint8_t* w2_blocks[kW2MaxLevels] = {nullptr, nullptr, nullptr};
   uint64_t* w2_sb[kW2MaxLevels] = {nullptr, nullptr, nullptr};
   uint64_t* w2_Z = nullptr;
+  uint32_t* cache_bm = nullptr;
+  uint64_t* cache_tab = nullptr;
+  uint64_t cache_nodes = 0, cache_bytes = 0;
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;
   uint32_t* text = nullptr;
@@ -377,6 +426,7 @@ struct Index {
 // build.hip
 int device_build_from_bwt(Index* h, const uint32_t* d_bwt_owned, uint64_t n, hipStream_t s);
 int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
+int device_build_cache(Index* h, hipStream_t s);   // cache.hip
 int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s,
                        uint64_t* d_total);
 
@@ -397,11 +447,14 @@ int launch_mask(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64
 int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                   const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                   uint64_t m, uint8_t* mask, uint64_t ld, uint64_t vocab, int packed, hipStream_t s);
+int launch_cache_probe(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m, uint8_t* out,
+                       hipStream_t s);
 int launch_follow_bitmaps(const DevView& v, const uint64_t* C, uint64_t nsym, uint32_t* out,
                           hipStream_t s);
 int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
-                    void* ws, uint64_t total_cap, hipStream_t s);
+                    void* ws, uint64_t total_cap, hipStream_t s, uint64_t min_count = 1,
+                    uint64_t* child_lo = nullptr);
 size_t distinct_ws_bytes(uint64_t total_cap);
 
 // epilogue.hip

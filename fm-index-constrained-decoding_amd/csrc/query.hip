@@ -162,12 +162,17 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[
 // interval_symbols with counts: level-synchronous BFS over the 16-ary
 // wavelet matrix, one workgroup per row; children are appended in digit
 // order so the final frontier is in ascending symbol order.
+// min_count > 1 prunes every prefix node holding fewer occurrences (so only
+// symbols occurring >= min_count times are reported, in O(width / min_count)
+// space); child_lo, when given, receives LF(lo, c) = C[c] + rank_c(lo) of
+// every reported symbol (the child range is [child_lo, child_lo + count)).
 __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __restrict__ lo_a,
                                                  const uint64_t* __restrict__ hi_a, uint64_t m,
                                                  const uint64_t* __restrict__ cap_off,
                                                  uint64_t* __restrict__ syms,
                                                  uint64_t* __restrict__ counts,
-                                                 uint64_t* __restrict__ k_out, Frontier fr) {
+                                                 uint64_t* __restrict__ k_out, Frontier fr,
+                                                 uint64_t min_count, uint64_t* __restrict__ child_lo) {
   __shared__ uint32_t wave_tot[4];
   const uint64_t row = blockIdx.x;
   if (row >= m) return;
@@ -208,7 +213,7 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
         digit_counts(v, lev, alo[i], cl);
         digit_counts(v, lev, ahi[i], ch);
 #pragma unroll
-        for (int d = 0; d < 16; ++d) nchild += (ch[d] > cl[d]) ? 1u : 0u;
+        for (int d = 0; d < 16; ++d) nchild += (ch[d] >= cl[d] + min_count) ? 1u : 0u;
       }
       uint32_t tot;
       const uint64_t pos0 = out + block_scan_u32(nchild, wave_tot, tot);
@@ -216,7 +221,7 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
         uint64_t pos = pos0;
 #pragma unroll
         for (uint32_t d = 0; d < 16; ++d) {
-          if (ch[d] > cl[d]) {
+          if (ch[d] >= cl[d] + min_count) {
             if (pos < cap) {
               blo[pos] = Z[d] + cl[d];
               bhi[pos] = Z[d] + ch[d];
@@ -247,6 +252,7 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
   for (uint64_t i = threadIdx.x; i < fc; i += 256) {
     syms[base + i] = apre[i];
     counts[base + i] = ahi[i] - alo[i];
+    if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
   }
   if (threadIdx.x == 0) k_out[row] = fc;
 }
@@ -298,7 +304,7 @@ size_t distinct_ws_bytes(uint64_t total_cap) { return (size_t)total_cap * 40 + 2
 
 int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
-                    void* ws, uint64_t total_cap, hipStream_t s) {
+                    void* ws, uint64_t total_cap, hipStream_t s, uint64_t min_count, uint64_t* child_lo) {
   if (m == 0) return 0;
   Frontier fr;
   char* p = reinterpret_cast<char*>(ws);
@@ -309,7 +315,8 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
   fr.hi[1] = fr.lo[1] + T;
   fr.pre[0] = reinterpret_cast<uint32_t*>(fr.hi[1] + T);
   fr.pre[1] = fr.pre[0] + T;
-  k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr);
+  k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr,
+                                         min_count ? min_count : 1, child_lo);
   FM_HIP(hipGetLastError());
   return 0;
 }

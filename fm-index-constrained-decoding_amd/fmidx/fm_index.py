@@ -236,7 +236,20 @@ class FMIndex:
         check(lib().fm_stats(self._h, *[byref(v) for v in vals]), "stats")
         keys = ["levels", "wm_bytes", "bwt_bytes", "bitmap_bytes", "bitmap_block"]
         out = {k: int(v.value) for k, v in zip(keys, vals)}
-        out["follow_bytes"] = int(os.environ.get("FMIDX_FOLLOW_BITMAPS", "1") != "0" and out["bitmap_block"] > 0)
+        out["follow_bytes"] = int(os.environ.get("FMIDX_FOLLOW_BITMAPS", "0") != "0" and out["bitmap_block"] > 0)
+        ex = [c_uint64() for _ in range(5)]
+        check(lib().fm_stats_ex(self._h, *[byref(v) for v in ex]), "stats_ex")
+        for k, v in zip(["lf_levels", "lf_wm_bytes", "cache_nodes", "cache_bytes", "cache_min"], ex):
+            out[k] = int(v.value)
+        return out
+
+    def cache_contains(self, lo, hi):
+        """uint8 device tensor: 1 where [lo, hi) has a cached range bitmap."""
+        import torch
+
+        out = torch.empty(lo.numel(), dtype=torch.uint8, device=lo.device)
+        check(lib().fm_cache_lookup_batch(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), lo.numel(),
+                                          c_void_p(out.data_ptr()), c_void_p(_stream_of(lo))), "cache_lookup_batch")
         return out
 
     def get_range_batch(self, patterns: Sequence[Sequence[int]], shift: int = 0,

@@ -234,6 +234,17 @@ int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, ui
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
              uint64_t* bitmap_bytes, uint64_t* bitmap_block);
 
+/* Bytes of the LF path's 2-level wavelet matrix and its level count, and the
+ * range-bitmap cache: cached ranges (every SA range reachable from the root
+ * with width >= cache_min), their bytes, and cache_min (0 = no cache). */
+int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint64_t* cache_nodes,
+                uint64_t* cache_bytes, uint64_t* cache_min);
+
+/* For m device ranges, out[i] = 1 if [lo[i], hi[i]) has a cached bitmap
+ * (accounting / tests; stream-ordered). */
+int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
+                          void* stream);
+
 /* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces. */
 int fm_device_bwt(const fm_index* h, const uint32_t** out);
 

@@ -19,21 +19,23 @@ def dev():
     return torch.device("cuda:0")
 
 
-def ours_index(docs, bm_log2=None):
+def ours_index(docs, bm_log2=None, cache_min=None):
     from fmidx.index import FMIndex
 
-    old = os.environ.get("FMIDX_BM_LOG2")
-    if bm_log2 is not None:
-        os.environ["FMIDX_BM_LOG2"] = str(bm_log2)
+    env = {"FMIDX_BM_LOG2": bm_log2, "FMIDX_CACHE_MIN": cache_min}
+    old = {k: os.environ.get(k) for k in env}
+    for k, val in env.items():
+        if val is not None:
+            os.environ[k] = str(val)
     try:
         idx = FMIndex(device=0)
         idx.initialize(docs, in_memory=True)
     finally:
-        if bm_log2 is not None:
-            if old is None:
-                del os.environ["FMIDX_BM_LOG2"]
+        for k, val in old.items():
+            if val is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["FMIDX_BM_LOG2"] = old
+                os.environ[k] = val
     return idx
 
 
@@ -125,11 +127,16 @@ def test_swig_surface_errors(dev):
     (6, 150, 1 << 20, 60, 6),     # 21-bit symbols: 3-level LF wavelet matrix
     (7, 300, 246, 90, 6),         # 8-bit symbols: one uint8 LF level
 ])
-def test_random_corpora_vs_oracle(dev, seed, n_docs, vocab, max_len, bm):
+@pytest.mark.parametrize("cache_min", [None, 8])
+def test_random_corpora_vs_oracle(dev, seed, n_docs, vocab, max_len, bm, cache_min):
+    """cache_min=8: the range-bitmap cache holds every reachable range of width
+    >= 8, so masks of wide ranges come from cached bitmaps."""
     import torch
 
     docs = markov_docs(seed, n_docs, vocab, max_len)
-    ours = ours_index(docs, bm_log2=bm)
+    ours = ours_index(docs, bm_log2=bm, cache_min=cache_min)
+    if cache_min is not None and bm is not None and vocab < 10000:
+        assert ours.stats()["cache_nodes"] > 1
     ora = OracleIndex()
     ora.initialize(docs, in_memory=True)
     n = ora.size()
@@ -210,11 +217,12 @@ def test_incremental_lf_equals_full_research(dev):
         assert got == want, s
 
 
-def test_decode_step_fused_and_reset(dev):
+@pytest.mark.parametrize("cache_min", [None, 4])
+def test_decode_step_fused_and_reset(dev, cache_min):
     import torch
 
     docs = markov_docs(11, 80, 40, 90)
-    ours = ours_index(docs, bm_log2=5)
+    ours = ours_index(docs, bm_log2=5, cache_min=cache_min)
     ora = OracleIndex()
     ora.initialize(docs, in_memory=True)
     n = ora.size()

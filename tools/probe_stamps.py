@@ -35,7 +35,7 @@ grid = (B + 7) // 8 * 8 * S
 stamps = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
 lo_o = torch.empty(B, dtype=torch.int64, device=dev)
 hi_o = torch.empty(B, dtype=torch.int64, device=dev)
-names = ["lohi", "zero", "lf+plan", "stream", "bitmap", "barrier", "emit"]
+names = ["lohi", "lf", "plan+bar", "stream", "bitmap", "barrier", "emit"]
 summary = []
 for s in range(W, W + 12):
     lo_i, hi_i = lo_hist[s - 1].clone(), hi_hist[s - 1].clone()
