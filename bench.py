@@ -209,6 +209,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=600)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--packed", action="store_true",
+                    help="bit-packed masks (uint32[B, ceil(V/32)]) instead of uint8[B, V] (not the headline)")
     ap.add_argument("--dump-trace", default="", help="write the timed trace states to this .npz")
     ap.add_argument("--eager-replay", action="store_true",
                     help="after the timed region, launch the K timed steps once more eagerly (no graph) "
@@ -236,7 +238,9 @@ def main():
     S_trace = S + (args.cpu_steps if cpu_leg else 0)
     tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
     del text
-    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    PK = bool(args.packed)
+    mask = (torch.empty((B, (V + 31) // 32), dtype=torch.int32, device=dev) if PK
+            else torch.empty((B, V), dtype=torch.uint8, device=dev))
     lo = init[0].clone()
     hi = init[1].clone()
     dummy = torch.empty((1, 1), dtype=torch.uint8, device=dev)
@@ -248,7 +252,7 @@ def main():
             dist.barrier()
 
     for s in range(W):
-        fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
+        fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0, packed=PK)
     torch.cuda.synchronize()
     state_lo, state_hi = lo.clone(), hi.clone()
 
@@ -267,14 +271,14 @@ def main():
         for i in range(K):
             src, dst = bufs[i % 2], bufs[(i + 1) % 2]
             fm.decode_step(tokens[W + i], src[0], src[1], mask, V, SHIFT, reset_below=0,
-                           lo_out=dst[0], hi_out=dst[1])
+                           lo_out=dst[0], hi_out=dst[1], packed=PK)
     with torch.cuda.graph(g_lf):
         for i in range(K):
             fm.lf_step_batch(tokens[W + i], lo_hist[W + i - 1], hi_hist[W + i - 1], SHIFT,
                              lo_out=lo_scr, hi_out=hi_scr, reset_below=0)
     with torch.cuda.graph(g_mask):
         for i in range(K):
-            fm.allowed_mask(lo_hist[W + i], hi_hist[W + i], V, SHIFT, out=mask)
+            fm.allowed_mask(lo_hist[W + i], hi_hist[W + i], V, SHIFT, out=mask, packed=PK)
 
     def timed(graph, reps=1, reset=False):
         ts = []
@@ -328,7 +332,7 @@ def main():
         for i in range(K):
             src, dst = bufs[i % 2], bufs[(i + 1) % 2]
             fm.decode_step(tokens[W + i], src[0], src[1], mask, V, SHIFT, reset_below=0,
-                           lo_out=dst[0], hi_out=dst[1])
+                           lo_out=dst[0], hi_out=dst[1], packed=PK)
         torch.cuda.synchronize()
     if args.dump_trace and rank == 0:
         np.savez_compressed(args.dump_trace, tokens=tokens[:S].cpu().numpy(), lo=lo_hist[:S].cpu().numpy(),
@@ -354,7 +358,7 @@ def main():
                                hi_hist[W:S].reshape(-1).contiguous()).view(K, B).cpu().numpy()
     read_bytes = np.stack([plan_bytes(lo_np[i], hi_np[i], n, b0_log2, bm_levels, words * 4, follow[i], cached[i])
                            for i in range(K)])
-    mask_bytes_per_launch = float((read_bytes.sum(1) + B * V).mean())
+    mask_bytes_per_launch = float((read_bytes.sum(1) + (B * ((V + 31) // 32) * 4 if PK else B * V)).mean())
     mask_us = float(np.median(mask_ms)) * 1e3
     NL = st["levels"]
     # LF: per digit level and endpoint one 128-B rank block + one 8-B
@@ -397,7 +401,7 @@ def main():
             "vocab": V,
             "wavelet_digit_levels": NL,
             "parallelism": f"replicas{world}",
-            "mask": "uint8[B,V]",
+            "mask": "uint32[B,ceil(V/32)] bit-packed" if PK else "uint8[B,V]",
         },
         "roofline": {
             "bound": "hbm",

@@ -198,8 +198,9 @@ __device__ __forceinline__ void set_u4(uint32_t* win, const uint4& q, int64_t ba
   set_bit(win, q.w, base_bit, lim);
 }
 
+// by threads [0, nthr) of the workgroup
 __device__ void stream_symbols(const uint32_t* __restrict__ bwt, const StreamParts& sp, int64_t base_bit,
-                               int64_t lim, uint32_t* win) {
+                               int64_t lim, uint32_t* win, uint32_t nthr) {
   const uint64_t ntot = sp.n0 + sp.n1;
   const uint4* src = reinterpret_cast<const uint4*>(bwt);
   uint32_t hsym = ~0u;          // head/tail symbols: threads 0..11, loaded with the first round
@@ -207,11 +208,11 @@ __device__ void stream_symbols(const uint32_t* __restrict__ bwt, const StreamPar
     const uint32_t pc = threadIdx.x / 3, k = threadIdx.x % 3;
     if (k < sp.plen[pc]) hsym = bwt[sp.piece[pc] + k];
   }
-  for (uint64_t base = threadIdx.x; base < ntot; base += (uint64_t)kDecThreads * kUnroll) {
+  for (uint64_t base = threadIdx.x; base < ntot; base += (uint64_t)nthr * kUnroll) {
     uint4 q[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t j = base + (uint64_t)u * kDecThreads;
+      const uint64_t j = base + (uint64_t)u * nthr;
       q[u] = (j < ntot) ? part_u4(src, sp, j) : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #pragma unroll
@@ -281,12 +282,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   __shared__ uint64_t s_lohi[2];
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   FM_STAMP(v, 0);
-  // Materialise every kernel-argument field used later now, so their scalar
-  // loads issue together at entry instead of one cache-missing round trip
-  // per first use deep inside the dependent chain.
-  asm volatile("" ::"s"(v.n), "s"(v.nblk), "s"(v.nsb), "s"(v.wm), "s"(v.sb), "s"(v.Z), "s"(v.D), "s"(v.C));
-  asm volatile("" ::"s"(v.bwt), "s"(v.bm), "s"(v.bm_full), "s"(v.bm_follow), "s"(v.bm_count[0]),
-               "s"(v.L), "s"(v.NL), "s"(v.max_sym), "s"(v.bm_words), "s"(v.bm_levels), "s"(v.bm_log2));
+  FM_PRELOAD_VIEW(v);
   uint64_t row;
   uint32_t slice;
   map_block(blockIdx.x, S, row, slice);
@@ -382,70 +378,98 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   lds_barrier();
   const uint64_t lo = s_lohi[0], hi = s_lohi[1];
   FM_STAMP(v, 3);
+  // Roles.  A wave with stores in flight cannot wait on a load without
+  // waiting for its stores too (shared vmcnt), so loads go to store-free waves:
+  //   early zero  (narrow input): waves 1.. have zero-filled; wave 0 streams
+  //   late zero   (output streamed only, wide input): waves 0-3 stream while
+  //               waves 4.. zero-fill now, overlapping the stream round trip
+  //   otherwise   every wave gathers (bitmaps + partial ends), every wave emits
+  // The zero-filling waves own their chunks in the final emit (program order).
+  const bool late_zero = kDecThreads >= 512 && !early_zero && lo < hi && plan.nb == 0;
+  const uint32_t e_first = early_zero ? 64u : (late_zero ? 256u : 0u);   // emit/zero owners: tid >= e_first
+  if (late_zero && threadIdx.x >= e_first) {
+    for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
+      const uint64_t t = t0 + k * CH;
+      if (PACKED) {
+        store4(orsrc, (uint32_t)(k * 4), 0u);
+      } else if (aligned16 && t + CH <= t1) {
+        store16(orsrc, (uint32_t)(k * 16), make_uint4(0, 0, 0, 0));
+      } else {
+        for (uint64_t j = t; j < min(t1, t + CH); ++j) out_row[j] = 0;
+      }
+    }
+  }
   if (lo < hi) {
-    // streamed partial ends, then bitmap ORs; one barrier after
     const int64_t base_bit = w_lo * 32;
     const int64_t lim = (int64_t)nwin * 32;
-    // The first batch of bitmap words (<= 8 per thread) is loaded before the
-    // partial ends are streamed, so both are in flight in one round trip.
     const uint32_t nb = plan.nb;
-    const uint32_t nw4 = nwin / 4;
-    const uint32_t G = max(1u, (uint32_t)kDecThreads / nw4);   // thread groups splitting the bitmaps
-    const uint32_t g = threadIdx.x / nw4;
-    uint32_t w4b = threadIdx.x % nw4;
-    int64_t gwb = w_lo + 4 * (int64_t)w4b;
-    bool own = nb && g < G && w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
-    uint4 x[8];
+    if (nb == 0) {
+      // streamed only
+      const uint32_t nthr = early_zero ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
+      if (threadIdx.x < nthr)
+        stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win, nthr);
+      FM_STAMP(v, 4);
+    } else {
+      // The first batch of bitmap words (<= 8 per thread) is loaded before the
+      // partial ends are streamed, so both are in flight in one round trip.
+      const uint32_t nw4 = nwin / 4;
+      const uint32_t G = max(1u, (uint32_t)kDecThreads / nw4);   // thread groups splitting the bitmaps
+      const uint32_t g = threadIdx.x / nw4;
+      uint32_t w4b = threadIdx.x % nw4;
+      int64_t gwb = w_lo + 4 * (int64_t)w4b;
+      bool own = g < G && w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
+      uint4 x[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t qq = g + (uint32_t)u * G;
-      x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
-    }
-    stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win);
-    FM_STAMP(v, 4);
-    // G groups split the bitmaps, each thread owns one uint4 of the window
-    // (several when the window is wider than the workgroup); partial ORs
-    // merge with LDS atomics.
-    bool first = true;
-    while (nb && g < G && w4b < nw4) {
-      if (own) {
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        for (uint32_t q = g; q < nb; q += G * 8) {
-          if (!first) {
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t qq = g + (uint32_t)u * G;
+        x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
+      }
+      stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win, kDecThreads);
+      FM_STAMP(v, 4);
+      // G groups split the bitmaps, each thread owns one uint4 of the window
+      // (several when the window is wider than the workgroup); partial ORs
+      // merge with LDS atomics.
+      bool first = true;
+      while (g < G && w4b < nw4) {
+        if (own) {
+          uint4 acc = make_uint4(0, 0, 0, 0);
+          for (uint32_t q = g; q < nb; q += G * 8) {
+            if (!first) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const uint32_t qq = q + (uint32_t)u * G;
+                x[u] = qq < nb ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
+              }
+            }
+            first = false;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-              const uint32_t qq = q + (uint32_t)u * G;
-              x[u] = qq < nb ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
+              acc.x |= x[u].x;
+              acc.y |= x[u].y;
+              acc.z |= x[u].z;
+              acc.w |= x[u].w;
             }
           }
-          first = false;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            acc.x |= x[u].x;
-            acc.y |= x[u].y;
-            acc.z |= x[u].z;
-            acc.w |= x[u].w;
-          }
+          if (acc.x) atomicOr(&win[4 * w4b + 0], acc.x);
+          if (acc.y) atomicOr(&win[4 * w4b + 1], acc.y);
+          if (acc.z) atomicOr(&win[4 * w4b + 2], acc.z);
+          if (acc.w) atomicOr(&win[4 * w4b + 3], acc.w);
         }
-        if (acc.x) atomicOr(&win[4 * w4b + 0], acc.x);
-        if (acc.y) atomicOr(&win[4 * w4b + 1], acc.y);
-        if (acc.z) atomicOr(&win[4 * w4b + 2], acc.z);
-        if (acc.w) atomicOr(&win[4 * w4b + 3], acc.w);
+        first = false;
+        w4b += kDecThreads;
+        gwb = w_lo + 4 * (int64_t)w4b;
+        own = w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
       }
-      first = false;
-      w4b += kDecThreads;
-      gwb = w_lo + 4 * (int64_t)w4b;
-      own = w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
     }
     FM_STAMP(v, 5);
     lds_barrier();
   }
   FM_STAMP(v, 6);
-  // the final stores to an early-zeroed chunk must land after its zero store
-  // (same thread, same address): drain this wave's outstanding stores first
-  if (early_zero) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the final stores to a zeroed chunk must land after its zero store (same
+  // thread, same address): drain this wave's outstanding stores first
+  const bool zeroed = early_zero || late_zero;
+  if (zeroed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
-  const uint32_t e_first = early_zero ? 64u : 0u;
   if (threadIdx.x >= e_first) {
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
       const int64_t rel = rel0 + (int64_t)k * CH;
@@ -457,7 +481,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
       const uint64_t cnt = min((uint64_t)CH, t1 - t);
       if (CH == 16) bits &= 0xFFFFu;
       if (cnt < CH) bits &= (1u << cnt) - 1u;
-      if (early_zero && bits == 0) continue;
+      if (zeroed && bits == 0) continue;
       if (PACKED) {
         store4(orsrc, (uint32_t)(k * 4), bits);   // t0 and t are multiples of 32
       } else if (aligned16 && cnt == 16) {

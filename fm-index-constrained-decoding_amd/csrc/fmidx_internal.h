@@ -109,6 +109,25 @@ struct DevView {
   } while (0)
 #endif
 
+// Kernel arguments live in memory and reach the wave through the scalar cache:
+// a field first touched deep inside a dependent chain costs a scalar-load
+// round trip there (measured ~1 us under load per phase).  Materialising every
+// hot field at kernel entry issues all those loads together, up front.
+#define FM_PRELOAD_VIEW(v)                                                                                 \
+  do {                                                                                                     \
+    asm volatile("" ::"s"((v).n), "s"((v).nblk), "s"((v).nsb), "s"((v).wm), "s"((v).sb), "s"((v).Z),      \
+                 "s"((v).D), "s"((v).C));                                                                  \
+    asm volatile("" ::"s"((v).bwt), "s"((v).bm), "s"((v).bm_full), "s"((v).bm_follow),                     \
+                 "s"((v).bm_count[0]), "s"((v).L), "s"((v).NL), "s"((v).max_sym), "s"((v).bm_words),       \
+                 "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
+    asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
+                 "s"((v).cache_mask), "s"((v).cache_min));                                                 \
+    asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
+                 "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
+    asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
+                 "s"((v).w2[1].bits), "s"((v).w2[1].shift));                                               \
+  } while (0)
+
 // ---------------------------------------------------------------------------
 // occurrences of digit d among the first m (<= 16) nibbles of w
 __device__ __forceinline__ uint32_t nib_count(uint64_t w, uint32_t d, uint32_t m) {

@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
                                                   int64_t shift, int64_t reset_below,
                                                   const uint64_t* lo_in, const uint64_t* hi_in,
                                                   uint64_t* lo_out, uint64_t* hi_out, uint64_t m) {
+  FM_PRELOAD_VIEW(v);
   const uint64_t i = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63u;
   if (i >= m) return;
