@@ -41,6 +41,8 @@ void Index::release() {
     w2_sb[l] = nullptr;
   }
   if (w2_Z) (void)hipFree(w2_Z);
+  if (E) (void)hipFree(E);
+  E = nullptr;
   if (cache_bm) (void)hipFree(cache_bm);
   if (cache_tab) (void)hipFree(cache_tab);
   cache_bm = nullptr;

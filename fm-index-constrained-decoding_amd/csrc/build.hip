@@ -11,6 +11,9 @@
 #include "fmidx_internal.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -339,6 +342,27 @@ __global__ void k_w2_sbscan(const uint32_t* __restrict__ sbtot, uint64_t nsb, ui
   total[d] = acc;
 }
 
+// ---- E array: LF(i) | BWT[i] << 36 ----------------------------------------
+struct InSymRange {
+  uint32_t c0, c1;
+  __host__ __device__ bool operator()(uint32_t x) const { return x >= c0 && x < c1; }
+};
+
+__global__ void __launch_bounds__(kThreads) k_gather_keys(const uint32_t* __restrict__ bwt,
+                                                         const uint64_t* __restrict__ pos, uint64_t m,
+                                                         uint32_t c0, uint32_t* __restrict__ key) {
+  for (uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x; k < m; k += (uint64_t)gridDim.x * kThreads)
+    key[k] = bwt[pos[k]] - c0;
+}
+
+// k-th position in (symbol, position) order has LF = base + k
+__global__ void __launch_bounds__(kThreads) k_write_e(const uint64_t* __restrict__ pos,
+                                                     const uint32_t* __restrict__ key, uint64_t m, uint64_t base,
+                                                     uint32_t c0, uint64_t* __restrict__ E) {
+  for (uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x; k < m; k += (uint64_t)gridDim.x * kThreads)
+    E[pos[k]] = (base + k) | ((uint64_t)(key[k] + c0) << kESymShift);
+}
+
 template <typename T>
 int dmalloc(T** p, size_t count) {
   *p = nullptr;
@@ -558,6 +582,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     v.bm_follow = fb;
   }
   if (device_build_w2(h, d_bwt, n, s)) return -1;
+  if (device_build_lfe(h, d_bwt, n, s)) return -1;
   if (device_build_cache(h, s)) return -1;
   h->built = true;
   return 0;
@@ -654,6 +679,70 @@ int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) 
   h->view.D2 = h->D2;
   h->view.NL2 = NL2;
   h->w2_bytes = bytes;
+  return 0;
+}
+
+// E[i] = LF(i) | BWT[i] << kESymShift.  LF(i) = C[c] + rank_c(i) is the index
+// of position i in the (symbol, position) order, so symbols are processed in
+// chunks of <= 2^29 occurrences (cut at C boundaries): select the chunk's
+// positions (ascending), stable radix sort them by symbol, write base + k.
+int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
+  if (env_u32("FMIDX_LF_E", 1) == 0) return 0;
+  if (n >= (1ull << kESymShift) || h->max_sym >= (1ull << (64 - kESymShift))) return 0;
+  const uint64_t K = (uint64_t)h->max_sym + 1;
+  std::vector<uint64_t> C(K + 1);
+  FM_HIP(hipMemcpyAsync(C.data(), h->C, (K + 1) * 8, hipMemcpyDeviceToHost, s));
+  FM_HIP(hipStreamSynchronize(s));
+  const uint64_t kChunk = 1ull << 29;
+  uint64_t maxm = 0;
+  std::vector<uint32_t> cuts{0};
+  while (cuts.back() < K) {
+    uint32_t c = cuts.back();
+    const uint64_t start = C[c];
+    uint32_t e = c + 1;
+    while (e < K && C[e + 1] - start <= kChunk) ++e;
+    cuts.push_back(e);
+    maxm = std::max(maxm, C[e] - start);
+  }
+  if (dmalloc(&h->E, n)) return -1;
+  uint64_t *pos = nullptr, *pos2 = nullptr, *d_cnt = nullptr;
+  uint32_t *key = nullptr, *key2 = nullptr;
+  if (dmalloc(&pos, maxm) || dmalloc(&pos2, maxm) || dmalloc(&key, maxm) || dmalloc(&key2, maxm) ||
+      dmalloc(&d_cnt, 1))
+    return -1;
+  rocprim::counting_iterator<uint64_t> iota(0);
+  size_t t1 = 0, t2 = 0;
+  auto flags0 = rocprim::make_transform_iterator(d_bwt, InSymRange{0, 1});
+  FM_HIP(rocprim::select(nullptr, t1, iota, flags0, pos, d_cnt, (size_t)n, s));
+  FM_HIP(rocprim::radix_sort_pairs(nullptr, t2, key, key2, pos, pos2, (size_t)maxm, 0, 32, s));
+  uint8_t* tmp = nullptr;
+  const size_t tb = std::max(t1, t2);
+  if (dmalloc(&tmp, tb)) return -1;
+  const unsigned g = (unsigned)std::min<uint64_t>((maxm + kThreads - 1) / kThreads, 1u << 18);
+  for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+    const uint32_t c0 = cuts[ci], c1 = cuts[ci + 1];
+    const uint64_t m = C[c1] - C[c0];
+    if (m == 0) continue;
+    size_t need = tb;
+    auto flags = rocprim::make_transform_iterator(d_bwt, InSymRange{c0, c1});
+    FM_HIP(rocprim::select(tmp, need, iota, flags, pos, d_cnt, (size_t)n, s));
+    k_gather_keys<<<g, kThreads, 0, s>>>(d_bwt, pos, m, c0, key);
+    FM_HIP(hipGetLastError());
+    uint32_t bits = 1;
+    while (bits < 32 && ((uint64_t)(c1 - c0 - 1) >> bits) != 0) ++bits;
+    need = tb;
+    FM_HIP(rocprim::radix_sort_pairs(tmp, need, key, key2, pos, pos2, (size_t)m, 0, bits, s));
+    k_write_e<<<g, kThreads, 0, s>>>(pos2, key2, m, C[c0], c0, h->E);
+    FM_HIP(hipGetLastError());
+  }
+  FM_HIP(hipStreamSynchronize(s));
+  FM_HIP(hipFree(tmp));
+  FM_HIP(hipFree(pos));
+  FM_HIP(hipFree(pos2));
+  FM_HIP(hipFree(key));
+  FM_HIP(hipFree(key2));
+  FM_HIP(hipFree(d_cnt));
+  h->view.E = h->E;
   return 0;
 }
 

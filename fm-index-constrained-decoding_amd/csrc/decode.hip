@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
         // from the full range the LF step lands on symbol c's C-block, whose
         // allowed set is c's precomputed follow-set bitmap
         if (l == 0 && h >= v.n) follow = t + shift;
-        lf_step_w2(v, t + shift, l, h);
+        lf_step_fast(v, t + shift, l, h);
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }
@@ -399,7 +399,10 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
       }
     }
   }
-  if (lo < hi) {
+  // One whole bitmap and nothing streamed (a cached range, the full range or a
+  // follow set): emitted straight from the bitmap in memory, no LDS pass.
+  const bool direct = lo < hi && plan.nb == 1 && plan.a0 >= plan.b0 && plan.a1 >= plan.b1;
+  if (lo < hi && !direct) {
     const int64_t base_bit = w_lo * 32;
     const int64_t lim = (int64_t)nwin * 32;
     const uint32_t nb = plan.nb;
@@ -470,7 +473,44 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   const bool zeroed = early_zero || late_zero;
   if (zeroed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
-  if (threadIdx.x >= e_first) {
+  if (direct) {
+    // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH); 4 chunks' words
+    // are loaded before any is converted and stored.  Chunk ownership as in
+    // the zero-fill (threads >= e_first) when the row was zeroed early.
+    const uint32_t* bm = plan.ptr[0];
+    const int64_t wlim = (int64_t)v.bm_words;
+    const uint32_t nt = kDecThreads - e_first;
+    for (uint64_t k0 = threadIdx.x - e_first; threadIdx.x >= e_first && k0 < nch; k0 += (uint64_t)nt * 4) {
+      uint64_t w2[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t k = k0 + (uint64_t)u * nt;
+        const int64_t bit = (int64_t)t0 + shift + (int64_t)k * CH;
+        const int64_t wi = bit >> 5;
+        const uint32_t a = (k < nch && wi < wlim) ? bm[wi] : 0u;
+        const uint32_t b = (k < nch && wi + 1 < wlim) ? bm[wi + 1] : 0u;
+        w2[u] = ((uint64_t)a | ((uint64_t)b << 32)) >> (bit & 31);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t k = k0 + (uint64_t)u * nt;
+        if (k >= nch) break;
+        const uint64_t t = t0 + k * CH;
+        const uint64_t cnt = min((uint64_t)CH, t1 - t);
+        uint32_t bits = (uint32_t)w2[u];
+        if (CH == 16) bits &= 0xFFFFu;
+        if (cnt < CH) bits &= (1u << cnt) - 1u;
+        if (zeroed && bits == 0) continue;
+        if (PACKED) {
+          store4(orsrc, (uint32_t)(k * 4), bits);
+        } else if (aligned16 && cnt == 16) {
+          store16(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits));
+        } else {
+          for (uint64_t j = 0; j < cnt; ++j) out_row[t + j] = (uint8_t)((bits >> j) & 1u);
+        }
+      }
+    }
+  } else if (threadIdx.x >= e_first) {
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
       const int64_t rel = rel0 + (int64_t)k * CH;
       const uint32_t wi = (uint32_t)(rel >> 5);

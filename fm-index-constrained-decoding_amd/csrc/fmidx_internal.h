@@ -46,6 +46,10 @@ constexpr int kW2MaxLevels = 3;
 constexpr int kW2BlkLog2 = 10;                 // 1024 digits per rank block
 constexpr int kW2Blk = 1 << kW2BlkLog2;
 constexpr int kW2SbLog2 = 16;                  // 64 blocks per superblock (u16 block headers)
+// E[i] = LF(i) | BWT[i] << 36: a narrow range's LF step reads E[lo, hi) once.
+constexpr uint32_t kESymShift = 36;
+constexpr uint64_t kELfMask = (1ull << kESymShift) - 1;
+constexpr uint32_t kENarrow = 512;             // widest range whose LF step scans E (8 entries per lane)
 
 // One level of the 2-level wavelet matrix.  Block b (digits [1024 b, 1024 b +
 // 1024)) = [R x uint16 count of each digit before the block, relative to its
@@ -82,6 +86,7 @@ struct DevView {
   const uint64_t* cache_tab;  // [cap][2] = {lo, hi | id << 34}; lo = ~0: empty
   uint64_t cache_mask;        // cap - 1 (cap a power of 2); 0 = no cache
   uint64_t cache_min;         // width threshold Wc
+  const uint64_t* E;          // [n] LF(i) | BWT[i] << kESymShift (narrow-range LF + streaming), or null
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
   uint32_t NL2;               // its levels (0 = not built)
@@ -121,7 +126,7 @@ struct DevView {
                  "s"((v).bm_count[0]), "s"((v).L), "s"((v).NL), "s"((v).max_sym), "s"((v).bm_words),       \
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
-                 "s"((v).cache_mask), "s"((v).cache_min));                                                 \
+                 "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E));                                     \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -364,6 +369,63 @@ __device__ __forceinline__ void lf_step_w2(const DevView& v, int64_t sym, uint64
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
+// LF step by a whole wave, choosing the path by the input width: a range of
+// at most kENarrow rows scans E[lo, hi) (8 entries per lane, ONE round trip --
+// and the entries are the ones the previous decode step streamed for its mask,
+// so they are usually still in L2 / the Infinity Cache): the occurrences of c
+// map to consecutive LF values, so the new range is [LF(first c), LF(last c)+1).
+// Wider ranges descend the 2-level wavelet matrix (2 round trips).
+__device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
+  if (hi > v.n) hi = v.n;
+  if (!v.E || lo >= hi || hi - lo > kENarrow || sym < 0 || (uint64_t)sym > v.max_sym) {
+    lf_step_w2(v, sym, lo, hi);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t c = (uint64_t)sym;
+  uint64_t e[kENarrow / 64];
+#pragma unroll
+  for (uint32_t j = 0; j < kENarrow / 64; ++j) {
+    const uint64_t idx = lo + lane + 64 * j;
+    e[j] = idx < hi ? v.E[idx] : ~0ull;
+  }
+  uint64_t fmin = ~0ull, fmax = 0, lfmin = 0, lfmax = 0;   // first / last match (relative index + 1)
+#pragma unroll
+  for (uint32_t j = 0; j < kENarrow / 64; ++j) {
+    if (e[j] != ~0ull && (e[j] >> kESymShift) == c) {
+      const uint64_t r = lane + 64 * j + 1;
+      if (r < fmin) {
+        fmin = r;
+        lfmin = e[j] & kELfMask;
+      }
+      if (r > fmax) {
+        fmax = r;
+        lfmax = e[j] & kELfMask;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t om = __shfl_xor(fmin, d, 64), ol = __shfl_xor(lfmin, d, 64);
+    const uint64_t xm = __shfl_xor(fmax, d, 64), xl = __shfl_xor(lfmax, d, 64);
+    if (om < fmin) {
+      fmin = om;
+      lfmin = ol;
+    }
+    if (xm > fmax) {
+      fmax = xm;
+      lfmax = xl;
+    }
+  }
+  if (fmax == 0) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = lfmin;
+  hi = lfmax + 1;
+}
+
 // ---------------------------------------------------------------------------
 // range-bitmap cache lookup
 __host__ __device__ __forceinline__ uint64_t cache_hash(uint64_t lo, uint64_t hi) {
@@ -428,6 +490,7 @@ struct Index {
   uint8_t* w2_blocks[kW2MaxLevels] = {nullptr, nullptr, nullptr};
   uint64_t* w2_sb[kW2MaxLevels] = {nullptr, nullptr, nullptr};
   uint64_t* w2_Z = nullptr;
+  uint64_t* E = nullptr;
   uint32_t* cache_bm = nullptr;
   uint64_t* cache_tab = nullptr;
   uint64_t cache_nodes = 0, cache_bytes = 0;
@@ -446,6 +509,7 @@ struct Index {
 int device_build_from_bwt(Index* h, const uint32_t* d_bwt_owned, uint64_t n, hipStream_t s);
 int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
 int device_build_cache(Index* h, hipStream_t s);   // cache.hip
+int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
 int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s,
                        uint64_t* d_total);
 
