@@ -45,6 +45,9 @@ void Index::release() {
   E = nullptr;
   if (cache_bm) (void)hipFree(cache_bm);
   if (cache_tab) (void)hipFree(cache_tab);
+  if (trans_tab) (void)hipFree(trans_tab);
+  trans_tab = nullptr;
+  trans_entries = 0;
   cache_bm = nullptr;
   cache_tab = nullptr;
   cache_nodes = cache_bytes = 0;

@@ -23,7 +23,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <unordered_set>
+#include <unordered_map>
 #include <vector>
 
 namespace fmidx {
@@ -71,10 +71,14 @@ int device_build_cache(Index* h, hipStream_t s) {
 
   // ---- breadth-first enumeration of the ranges with width >= Wc
   std::vector<std::pair<uint64_t, uint64_t>> nodes;
-  std::unordered_set<std::pair<uint64_t, uint64_t>, PairHash> seen;
+  std::unordered_map<std::pair<uint64_t, uint64_t>, uint64_t, PairHash> seen;   // range -> id
   std::vector<std::pair<uint64_t, uint64_t>> frontier{{0, n}}, next;
   nodes.push_back({0, n});
-  seen.insert({0, n});
+  seen.emplace(std::make_pair(uint64_t(0), n), 0);
+  struct Edge {
+    uint64_t plo, phi, c, clo, cw, id;
+  };
+  std::vector<Edge> edges;   // parent (not the root) -> cached child
   const uint64_t kChunkCap = 1ull << 24;   // child slots per k_distinct launch
   bool full = false;
   while (!frontier.empty() && !full) {
@@ -104,8 +108,9 @@ int device_build_cache(Index* h, hipStream_t s) {
       if (launch_distinct(v, d_lo.p, d_hi.p, m, d_off.p, d_syms.p, d_cnt.p, d_k.p, d_ws.p, total, s, Wc,
                           d_child.p))
         return -1;
-      std::vector<uint64_t> k(m), cnt(total), child(total);
+      std::vector<uint64_t> k(m), cnt(total), child(total), sym(total);
       FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, s));
+      FM_HIP(hipMemcpyAsync(sym.data(), d_syms.p, total * 8, hipMemcpyDeviceToHost, s));
       FM_HIP(hipMemcpyAsync(cnt.data(), d_cnt.p, total * 8, hipMemcpyDeviceToHost, s));
       FM_HIP(hipMemcpyAsync(child.data(), d_child.p, total * 8, hipMemcpyDeviceToHost, s));
       FM_HIP(hipStreamSynchronize(s));
@@ -117,14 +122,21 @@ int device_build_cache(Index* h, hipStream_t s) {
         }
         for (uint64_t j = 0; j < k[r]; ++j) {
           const uint64_t a = child[off[r] + j], b = a + cnt[off[r] + j];
-          if (seen.insert({a, b}).second) {
+          auto it = seen.find({a, b});
+          uint64_t id;
+          if (it == seen.end()) {
             if (nodes.size() >= max_nodes) {
               full = true;
               break;
             }
+            id = nodes.size();
+            seen.emplace(std::make_pair(a, b), id);
             nodes.push_back({a, b});
             next.push_back({a, b});
+          } else {
+            id = it->second;
           }
+          if (!(lo[r] == 0 && hi[r] == n)) edges.push_back({lo[r], hi[r], sym[off[r] + j], a, b - a, id});
         }
       }
       i0 = i1;
@@ -183,6 +195,43 @@ int device_build_cache(Index* h, hipStream_t s) {
   v.cache_tab = h->cache_tab;
   v.cache_min = Wc;
   v.cache_mask = cap - 1;
+
+  // ---- edge table (cached parent, c) -> cached child: linear probing with
+  //      every key within 16 slots of its home (one 512-B probe round)
+  v.trans_mask = 0;
+  v.trans_tab = nullptr;
+  if (edges.empty() || env_u64("FMIDX_EDGE_TABLE", 1) == 0) return 0;
+  uint64_t tcap = 1024;
+  while (tcap < 4 * edges.size()) tcap <<= 1;
+  std::vector<uint64_t> et;
+  for (;;) {
+    et.assign(4 * tcap, 0);
+    for (uint64_t i = 0; i < tcap; ++i) et[4 * i] = kCacheEmpty;
+    bool ok = true;
+    for (const Edge& e : edges) {
+      const uint64_t home = trans_hash(e.plo, e.phi, e.c) & (tcap - 1);
+      uint64_t d = 0;
+      while (d < 16 && et[4 * ((home + d) & (tcap - 1))] != kCacheEmpty) ++d;
+      if (d == 16) {
+        ok = false;
+        break;
+      }
+      uint64_t* slot = &et[4 * ((home + d) & (tcap - 1))];
+      slot[0] = e.plo;
+      slot[1] = e.phi | (e.c << kCacheIdShift);
+      slot[2] = e.clo;
+      slot[3] = e.cw | ((e.id + 1) << kCacheIdShift);
+    }
+    if (ok) break;
+    tcap <<= 1;
+  }
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&h->trans_tab), tcap * 32));
+  FM_HIP(hipMemcpyAsync(h->trans_tab, et.data(), tcap * 32, hipMemcpyHostToDevice, s));
+  FM_HIP(hipStreamSynchronize(s));
+  h->trans_entries = edges.size();
+  h->cache_bytes += tcap * 32;
+  v.trans_tab = h->trans_tab;
+  v.trans_mask = tcap - 1;
   return 0;
 }
 

@@ -8,9 +8,9 @@
 // index.py:161-174, sentinel dropped) that the processors scatter into their
 // score masks (document_constrained_generation_causal_qwen.py:185-204).
 //
-// Geometry (gfx950): one workgroup of kDecThreads = 512 threads (8 waves)
-// per (row, vocab slice); 2 slices per row at B = 256 (the measured best:
-// 1024 threads x 1 slice and 256 x 4 are 0.3-1.6 us slower per step).
+// Geometry (gfx950): one workgroup of kDecThreads = 1024 threads (16 waves)
+// per (row, vocab slice); 1 slice per row at B = 256 (measured best at C3:
+// 11.7 us/step vs 12.1 for 256 x 4 slices and 13.1 for 512 x 2).
 //   wave 0        LF step (2-level wavelet matrix: 2 dependent round trips),
 //                 then the read plan of the new range
 //   waves 1..15   rows whose incoming range is already narrow stay narrow
@@ -30,7 +30,7 @@ namespace fmidx {
 namespace {
 
 #ifndef FMIDX_DEC_THREADS
-#define FMIDX_DEC_THREADS 512
+#define FMIDX_DEC_THREADS 1024
 #endif
 #ifndef FMIDX_STORE_AUX
 #define FMIDX_STORE_AUX 16
@@ -328,6 +328,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   if (threadIdx.x < 64) {
     uint64_t l = lo_in[row], h = hi_in[row];
     int64_t follow = -1;
+    const uint32_t* tbm = nullptr;   // bitmap of the new range, when the edge table knew it
     if (DO_LF) {
       const int64_t t = tok[row];
       if (t < reset_below) {
@@ -337,7 +338,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
         // from the full range the LF step lands on symbol c's C-block, whose
         // allowed set is c's precomputed follow-set bitmap
         if (l == 0 && h >= v.n) follow = t + shift;
-        lf_step_fast(v, t + shift, l, h);
+        lf_step_decode(v, t + shift, l, h, tbm);
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }
@@ -359,7 +360,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
     if (l < h) {
       // a wide range is looked up in the range-bitmap cache first (one
       // bitmap, nothing streamed); otherwise the aligned-bitmap plan
-      const uint32_t* cb = cache_find(v, l, h);
+      const uint32_t* cb = tbm ? tbm : cache_find(v, l, h);
       if (cb) {
         if (threadIdx.x == 0) {
           plan.nb = 1;

@@ -86,6 +86,10 @@ struct DevView {
   const uint64_t* cache_tab;  // [cap][2] = {lo, hi | id << 34}; lo = ~0: empty
   uint64_t cache_mask;        // cap - 1 (cap a power of 2); 0 = no cache
   uint64_t cache_min;         // width threshold Wc
+  // edges of the cached ranges' LF graph: (cached parent, symbol c) -> the
+  // cached child LF_c(parent) and its bitmap id; 4 words per slot
+  const uint64_t* trans_tab;
+  uint64_t trans_mask;        // cap - 1; 0 = none
   const uint64_t* E;          // [n] LF(i) | BWT[i] << kESymShift (narrow-range LF + streaming), or null
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
@@ -126,7 +130,8 @@ struct DevView {
                  "s"((v).bm_count[0]), "s"((v).L), "s"((v).NL), "s"((v).max_sym), "s"((v).bm_words),       \
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
-                 "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E));                                     \
+                 "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
+                 "s"((v).trans_mask));                                                                     \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -466,6 +471,82 @@ __device__ __forceinline__ const uint32_t* cache_find(const DevView& v, uint64_t
   return nullptr;
 }
 
+__host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi, uint64_t c) {
+  return cache_hash(lo ^ (c * 0xD6E8FEB86659FD93ull), hi + c);
+}
+
+// Fused LF step of the decode kernel, by all 64 lanes of a wave.  A range of
+// at most kENarrow rows scans E (one round trip).  A cached range probes the
+// edge table (cached parent, c) -> cached child AND starts the wavelet-matrix
+// descent at once: a hit gives the new range and its bitmap after one round
+// trip (the table is a few MB, Infinity-Cache resident), a miss continues the
+// descent (two round trips, as without the table).  *cbm = the new range's
+// cached bitmap when the table knew it, else null.
+__device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
+                                               const uint32_t*& cbm) {
+  cbm = nullptr;
+  if (hi > v.n) hi = v.n;
+  if (!v.trans_mask || lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym || hi - lo < v.cache_min ||
+      (lo == 0 && hi == v.n)) {
+    lf_step_fast(v, sym, lo, hi);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t c = (uint64_t)sym;
+  // (1) the edge probe: 16 slots of 32 B by lanes 0-15 (one 512-B round)
+  const uint64_t k1 = hi | (c << kCacheIdShift);
+  const uint64_t slot = trans_hash(lo, hi, c) & v.trans_mask;
+  uint4 ta = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0), tb = make_uint4(0, 0, 0, 0);
+  if (lane < 16) {
+    const uint4* e = reinterpret_cast<const uint4*>(v.trans_tab + 4 * ((slot + lane) & v.trans_mask));
+    ta = e[0];
+    tb = e[1];
+  }
+  // (2) the wavelet-matrix descent's first level, issued before the probe is inspected
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
+  const uint32_t c32 = (uint32_t)c;
+  const int64_t dd = v.D2[c32];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  const uint64_t pos0 = side ? hi : lo;
+  const uint32_t d0 = (c32 >> v.w2[0].shift) & ((1u << v.w2[0].bits) - 1u);
+  const uint64_t r0 = rank_w2(v.w2[0], pos0, d0, q);
+  const uint64_t w0 = (uint64_t)ta.x | ((uint64_t)ta.y << 32), w1 = (uint64_t)ta.z | ((uint64_t)ta.w << 32);
+  const uint64_t bh = __ballot(lane < 16 && w0 == lo && w1 == k1);
+  const uint64_t be = __ballot(lane < 16 && w0 == kCacheEmpty);
+  if (bh && (!be || __ffsll((long long)bh) < __ffsll((long long)be))) {
+    const int src = __ffsll((long long)bh) - 1;
+    const uint64_t w2 = (uint64_t)tb.x | ((uint64_t)tb.y << 32), w3 = (uint64_t)tb.z | ((uint64_t)tb.w << 32);
+    const uint64_t clo = __shfl(w2, src, 64);
+    const uint64_t x = __shfl(w3, src, 64);
+    lo = clo;
+    hi = clo + (x & ((1ull << kCacheIdShift) - 1));
+    cbm = v.cache_bm + ((x >> kCacheIdShift) - 1) * v.bm_words;
+    return;
+  }
+  // miss (the table is built with >= 16 free slots after every cluster head it
+  // holds, so no key lies past the first 16): finish the descent
+  uint64_t pos = z[0] + r0;
+#pragma unroll
+  for (int l = 1; l < kW2MaxLevels; ++l) {
+    if (l >= (int)v.NL2) break;
+    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    pos = z[l] + rank_w2(v.w2[l], pos, d, q);
+  }
+  const uint64_t other = __shfl_xor(pos, 32, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
 // ---------------------------------------------------------------------------
 // host-side owner of the device structures
 struct Index {
@@ -493,7 +574,8 @@ struct Index {
   uint64_t* E = nullptr;
   uint32_t* cache_bm = nullptr;
   uint64_t* cache_tab = nullptr;
-  uint64_t cache_nodes = 0, cache_bytes = 0;
+  uint64_t* trans_tab = nullptr;
+  uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0;
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;
   uint32_t* text = nullptr;

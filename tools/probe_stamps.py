@@ -24,7 +24,7 @@ tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, W + 12, 2025090
 dl = lib()
 dl.fm_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
-T = 512                        # kDecThreads (decode.hip)
+T = 1024                       # kDecThreads (decode.hip)
 S = int(os.environ.get("FMIDX_MASK_SLICES", "0"))
 if S == 0:                     # mirrors mask_geometry() in decode.hip
     want = max(1, int(os.environ.get("FMIDX_WAVE_BUDGET", "4096")) // (((B + 7) // 8 * 8) * (T // 64)))
