@@ -376,6 +376,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   const int64_t sym_end = (int64_t)t1 + shift + 64;
   const uint32_t nwin = (uint32_t)(((sym_end - w_lo * 32 + 31) / 32 + 3) & ~3ll);
   for (uint32_t w = threadIdx.x; w < nwin; w += kDecThreads) win[w] = 0;
+  FM_STAMP_T(v, 5, kDecThreads - 64);   // diagnostic: the last wave's arrival at the plan barrier
   lds_barrier();
   const uint64_t lo = s_lohi[0], hi = s_lohi[1];
   FM_STAMP(v, 3);
@@ -465,7 +466,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
         own = w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
       }
     }
-    FM_STAMP(v, 5);
     lds_barrier();
   }
   FM_STAMP(v, 6);

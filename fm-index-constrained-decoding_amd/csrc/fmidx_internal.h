@@ -112,7 +112,15 @@ struct DevView {
     if (threadIdx.x == 0 && (v).stamps)                                                \
       (v).stamps[(uint64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define FM_STAMP_T(v, slot, tid)                                                         \
+  do {                                                                                 \
+    if (threadIdx.x == (tid) && (v).stamps)                                            \
+      (v).stamps[(uint64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define FM_STAMP_T(v, slot, tid) \
+  do {                           \
+  } while (0)
 #define FM_STAMP(v, slot) \
   do {                    \
   } while (0)
@@ -193,62 +201,6 @@ __device__ __forceinline__ uint64_t rank16(const DevView& v, uint32_t lev, uint6
   return cnt;
 }
 
-// rank_d(i) by an aligned group of 8 lanes (q = lane & 7): one uint4 each,
-// summed with three xor-shuffles.  Every lane of the group gets the result.
-__device__ __forceinline__ uint64_t rank16_coop(const DevView& v, uint32_t lev, uint64_t i, uint32_t d,
-                                                uint32_t q) {
-  const uint64_t b = i / kBlkDigits;
-  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
-  const uint4 x = rank_block(v, lev, b)[q];
-  const uint64_t base = sb_row(v, lev, b)[d];
-  uint32_t part = block_part(x, q, d, k);
-  part += __shfl_xor(part, 1, 64);
-  part += __shfl_xor(part, 2, 64);
-  part += __shfl_xor(part, 4, 64);
-  return base + part;
-}
-
-// One reference backward_search_step on a half-open state (fm_index.cpp:67-97
-// as driven by index.py:110), computed by an aligned group of 16 lanes:
-// lanes 0-7 rank the low end, lanes 8-15 the high end, NL dependent rounds.
-// (0,0) = empty in and out.  All 16 lanes receive the result.
-__device__ __forceinline__ void lf_step16(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
-                                          uint32_t lane16) {
-  if (hi > v.n) hi = v.n;                    // high clamp (fm_index.cpp:74-76)
-  if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {  // low > high / unknown symbol
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  const uint32_t c = (uint32_t)sym;
-  if (lo == 0 && hi == v.n) {                // [sdsl] backward_search full-range case
-    const uint64_t a = v.C[c], b = v.C[c + 1];
-    lo = a < b ? a : 0;
-    hi = a < b ? b : 0;
-    return;
-  }
-  const uint32_t q = lane16 & 7u;
-  const bool side = lane16 >= 8;
-  uint64_t l = lo, r = hi;
-  for (uint32_t lev = 0; lev < v.NL; ++lev) {
-    const uint32_t d = digit_of(c, v.NL, lev);
-    const uint64_t z = v.Z[lev * kRadix + d];
-    const uint64_t mine = rank16_coop(v, lev, side ? r : l, d, q);
-    const uint64_t other = __shfl_xor(mine, 8, 64);
-    l = z + (side ? other : mine);
-    r = z + (side ? mine : other);
-    if (l >= r) break;
-  }
-  if (l >= r) {
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  const int64_t dd = v.D[c];
-  lo = (uint64_t)((int64_t)l + dd);
-  hi = (uint64_t)((int64_t)r + dd);
-}
-
 // Full NL-level descent of both endpoints by one thread (no early exit).
 __device__ __forceinline__ void descend_full(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
   for (uint32_t lev = 0; lev < v.NL; ++lev) {
@@ -278,16 +230,17 @@ __device__ __forceinline__ uint32_t eq8_count(uint32_t w, uint32_t dd, uint32_t 
   return c;
 }
 
-__device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
+__device__ __forceinline__ uint64_t rank_w2_at(const uint8_t* blocks, const uint64_t* sbp, uint64_t blk_bytes,
+                                            uint32_t bits, uint64_t i, uint32_t d, uint32_t q) {
   const uint64_t b = i >> kW2BlkLog2;
   const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
-  const uint8_t* base = L.blocks + b * L.blk_bytes;
-  const uint32_t R = 1u << L.bits;
-  const uint64_t sbv = L.sb[(i >> kW2SbLog2) * R + d];
+  const uint8_t* base = blocks + b * blk_bytes;
+  const uint32_t R = 1u << bits;
+  const uint64_t sbv = sbp[(i >> kW2SbLog2) * R + d];
   const uint32_t hdr = reinterpret_cast<const uint16_t*>(base)[d];
   const uint32_t first = 32 * q;   // first digit of this lane
   uint32_t cnt = 0;
-  if (L.bits > 8) {
+  if (bits > 8) {
     const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
     uint4 x[4];
 #pragma unroll
@@ -328,64 +281,16 @@ __device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32
   return sbv + hdr + cnt;
 }
 
-// One reference backward_search_step on a half-open state (fm_index.cpp:67-97
-// as driven by index.py:110) over the 2-level wavelet matrix, by all 64 lanes
-// of a wave (lanes 0-31 rank the low end, 32-63 the high end): NL2 (= 2 for
-// a 128k vocabulary) dependent round trips.  (0,0) = empty in and out; every
-// lane receives the result.
-__device__ __forceinline__ void lf_step_w2(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
-  if (hi > v.n) hi = v.n;                    // high clamp (fm_index.cpp:74-76)
-  if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {  // low > high / unknown symbol
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  const uint32_t c = (uint32_t)sym;
-  if (lo == 0 && hi == v.n) {                // [sdsl] backward_search full-range case
-    const uint64_t a = v.C[c], b = v.C[c + 1];
-    lo = a < b ? a : 0;
-    hi = a < b ? b : 0;
-    return;
-  }
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t q = lane & 31u;
-  const bool side = lane >= 32;
-  // level-independent loads first: all in flight with the first rank
-  const int64_t dd = v.D2[c];
-  uint64_t z[kW2MaxLevels];
-#pragma unroll
-  for (int l = 0; l < kW2MaxLevels; ++l)
-    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
-  uint64_t pos = side ? hi : lo;
-#pragma unroll
-  for (int l = 0; l < kW2MaxLevels; ++l) {
-    if (l >= (int)v.NL2) break;
-    const uint32_t d = (c >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    pos = z[l] + rank_w2(v.w2[l], pos, d, q);
-  }
-  const uint64_t other = __shfl_xor(pos, 32, 64);
-  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
-  if (l2 >= h2) {
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  lo = (uint64_t)((int64_t)l2 + dd);
-  hi = (uint64_t)((int64_t)h2 + dd);
+__device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
+  return rank_w2_at(L.blocks, L.sb, L.blk_bytes, L.bits, i, d, q);
 }
 
-// LF step by a whole wave, choosing the path by the input width: a range of
-// at most kENarrow rows scans E[lo, hi) (8 entries per lane, ONE round trip --
-// and the entries are the ones the previous decode step streamed for its mask,
-// so they are usually still in L2 / the Infinity Cache): the occurrences of c
-// map to consecutive LF values, so the new range is [LF(first c), LF(last c)+1).
-// Wider ranges descend the 2-level wavelet matrix (2 round trips).
+// LF step of a narrow range by a whole wave: E[lo, hi) is scanned (8 entries
+// per lane, ONE round trip -- and usually L2 / Infinity-Cache hits, the rows
+// the previous decode step streamed): the occurrences of c map to consecutive
+// LF values, so the new range is [LF(first c), LF(last c) + 1).
+// (precondition: v.E, 0 < hi - lo <= kENarrow, hi <= n, 0 <= sym <= max_sym)
 __device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
-  if (hi > v.n) hi = v.n;
-  if (!v.E || lo >= hi || hi - lo > kENarrow || sym < 0 || (uint64_t)sym > v.max_sym) {
-    lf_step_w2(v, sym, lo, hi);
-    return;
-  }
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t c = (uint64_t)sym;
   uint64_t e[kENarrow / 64];
@@ -475,66 +380,76 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
   return cache_hash(lo ^ (c * 0xD6E8FEB86659FD93ull), hi + c);
 }
 
-// Fused LF step of the decode kernel, by all 64 lanes of a wave.  A range of
-// at most kENarrow rows scans E (one round trip).  A cached range probes the
-// edge table (cached parent, c) -> cached child AND starts the wavelet-matrix
-// descent at once: a hit gives the new range and its bitmap after one round
-// trip (the table is a few MB, Infinity-Cache resident), a miss continues the
-// descent (two round trips, as without the table).  *cbm = the new range's
-// cached bitmap when the table knew it, else null.
+// The LF step of the batched kernels, by all 64 lanes of a wave (uniform
+// inputs), with exactly one inlined copy of each path (a kernel's code is
+// fetched cold into the instruction cache at every launch, so duplicated
+// inlined paths cost fetch latency on the dependent chain):
+//   * full range: [C[c], C[c+1]) ([sdsl] backward_search shortcut);
+//   * <= kENarrow rows: one scan of E[lo, hi) (lf_step_fast);
+//   * otherwise the wavelet-matrix descent (NL2 round trips); a cached range
+//     also probes the edge table (cached parent, c) -> cached child, issued
+//     with the first descent level -- a hit ends the step after one round
+//     trip and names the child's bitmap in *cbm (else null).
 __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
                                                const uint32_t*& cbm) {
   cbm = nullptr;
   if (hi > v.n) hi = v.n;
-  if (!v.trans_mask || lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym || hi - lo < v.cache_min ||
-      (lo == 0 && hi == v.n)) {
+  if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  const uint32_t c32 = (uint32_t)sym;
+  if (lo == 0 && hi == v.n) {
+    const uint64_t a = v.C[c32], b = v.C[c32 + 1];
+    lo = a < b ? a : 0;
+    hi = a < b ? b : 0;
+    return;
+  }
+  if (v.E && hi - lo <= kENarrow) {
     lf_step_fast(v, sym, lo, hi);
     return;
   }
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
   const uint64_t c = (uint64_t)sym;
-  // (1) the edge probe: 16 slots of 32 B by lanes 0-15 (one 512-B round)
+  // (1) edge probe of a cached range: 16 slots of 32 B by lanes 0-15
+  const bool probe = v.trans_mask && hi - lo >= v.cache_min;
   const uint64_t k1 = hi | (c << kCacheIdShift);
-  const uint64_t slot = trans_hash(lo, hi, c) & v.trans_mask;
   uint4 ta = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0), tb = make_uint4(0, 0, 0, 0);
-  if (lane < 16) {
+  if (probe && lane < 16) {
+    const uint64_t slot = trans_hash(lo, hi, c) & v.trans_mask;
     const uint4* e = reinterpret_cast<const uint4*>(v.trans_tab + 4 * ((slot + lane) & v.trans_mask));
     ta = e[0];
     tb = e[1];
   }
-  // (2) the wavelet-matrix descent's first level, issued before the probe is inspected
-  const uint32_t q = lane & 31u;
-  const bool side = lane >= 32;
-  const uint32_t c32 = (uint32_t)c;
+  // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
   uint64_t z[kW2MaxLevels];
 #pragma unroll
   for (int l = 0; l < kW2MaxLevels; ++l)
     z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
-  const uint64_t pos0 = side ? hi : lo;
-  const uint32_t d0 = (c32 >> v.w2[0].shift) & ((1u << v.w2[0].bits) - 1u);
-  const uint64_t r0 = rank_w2(v.w2[0], pos0, d0, q);
-  const uint64_t w0 = (uint64_t)ta.x | ((uint64_t)ta.y << 32), w1 = (uint64_t)ta.z | ((uint64_t)ta.w << 32);
-  const uint64_t bh = __ballot(lane < 16 && w0 == lo && w1 == k1);
-  const uint64_t be = __ballot(lane < 16 && w0 == kCacheEmpty);
-  if (bh && (!be || __ffsll((long long)bh) < __ffsll((long long)be))) {
-    const int src = __ffsll((long long)bh) - 1;
-    const uint64_t w2 = (uint64_t)tb.x | ((uint64_t)tb.y << 32), w3 = (uint64_t)tb.z | ((uint64_t)tb.w << 32);
-    const uint64_t clo = __shfl(w2, src, 64);
-    const uint64_t x = __shfl(w3, src, 64);
-    lo = clo;
-    hi = clo + (x & ((1ull << kCacheIdShift) - 1));
-    cbm = v.cache_bm + ((x >> kCacheIdShift) - 1) * v.bm_words;
-    return;
-  }
-  // miss (the table is built with >= 16 free slots after every cluster head it
-  // holds, so no key lies past the first 16): finish the descent
-  uint64_t pos = z[0] + r0;
-#pragma unroll
-  for (int l = 1; l < kW2MaxLevels; ++l) {
-    if (l >= (int)v.NL2) break;
+  uint64_t pos = side ? hi : lo;
+#pragma unroll 1
+  for (int l = 0; l < (int)v.NL2; ++l) {
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    pos = z[l] + rank_w2(v.w2[l], pos, d, q);
+    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
+    if (l == 0 && probe) {   // the probe's loads were issued before this level's
+      const uint64_t w0 = (uint64_t)ta.x | ((uint64_t)ta.y << 32), w1 = (uint64_t)ta.z | ((uint64_t)ta.w << 32);
+      const uint64_t bh = __ballot(lane < 16 && w0 == lo && w1 == k1);
+      if (bh) {   // keys lie within 16 slots of their home (build invariant)
+        const int src = __ffsll((long long)bh) - 1;
+        const uint64_t w2 = (uint64_t)tb.x | ((uint64_t)tb.y << 32), w3 = (uint64_t)tb.z | ((uint64_t)tb.w << 32);
+        const uint64_t clo = __shfl(w2, src, 64);
+        const uint64_t x = __shfl(w3, src, 64);
+        lo = clo;
+        hi = clo + (x & ((1ull << kCacheIdShift) - 1));
+        cbm = v.cache_bm + ((x >> kCacheIdShift) - 1) * v.bm_words;
+        return;
+      }
+    }
+    pos = z[l] + r;
   }
   const uint64_t other = __shfl_xor(pos, 32, 64);
   const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;

@@ -39,7 +39,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
     l = 0;
     h = v.n;
   } else {
-    lf_step_fast(v, t + shift, l, h);
+    const uint32_t* cbm;
+    lf_step_decode(v, t + shift, l, h, cbm);
   }
   if (lane == 0) {
     lo_out[i] = l;
@@ -59,7 +60,8 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
   uint64_t h = hi_in ? hi_in[i] : v.n;
   const int64_t a = off[i], b = off[i + 1];
   for (int64_t j = a; j < b; ++j) {
-    lf_step_fast(v, tok[j] + shift, l, h);
+    const uint32_t* cbm;
+    lf_step_decode(v, tok[j] + shift, l, h, cbm);
     if (l == 0 && h == 0) break;       // index.py:111-112
   }
   if (lane == 0) {

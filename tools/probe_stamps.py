@@ -35,7 +35,7 @@ grid = (B + 7) // 8 * 8 * S
 stamps = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
 lo_o = torch.empty(B, dtype=torch.int64, device=dev)
 hi_o = torch.empty(B, dtype=torch.int64, device=dev)
-names = ["lohi", "lf", "plan+bar", "stream", "bitmap", "barrier", "emit"]
+names = ["lohi", "lf", "plan+bar", "stream", "(w15arr-s4)", "bar2", "emit"]
 summary = []
 for s in range(W, W + 12):
     lo_i, hi_i = lo_hist[s - 1].clone(), hi_hist[s - 1].clone()
@@ -65,9 +65,14 @@ for s in range(W, W + 12):
     print(f"step {s}: kernel span {span:.1f}us, dispatch spread {start_spread:.1f}us, "
           f"median WG {np.median(tot):.1f}us, mean phases " +
           " ".join(f"{nm}={ph[:, i].mean():.2f}" for i, nm in enumerate(names)))
+    w15 = (st[:, 5] - st[:, 0]) * 10 / 1000
+    t2 = (st[:, 2] - st[:, 0]) * 10 / 1000
+    print(f"   last-wave arrival at plan barrier (from WG start): median {np.median(w15):.2f} us, "
+          f"max {w15.max():.2f}; wave-0 LF done median {np.median(t2[st[:, 2] > 0]):.2f} us")
     for j in np.argsort(-end_rel)[:4]:
         print(f"   slowest-ending WG row {rows[j]} width {w_old[j]}->{w_new[j]} start "
               f"{(st[j, 0] - t0) * 10 / 1000:.1f} end {end_rel[j]:.1f}: " +
-              " ".join(f"{nm}={ph[j, i]:.2f}" for i, nm in enumerate(names)))
+              " ".join(f"{nm}={ph[j, i]:.2f}" for i, nm in enumerate(names)) +
+              f" | lf_done@{t2[j]:.2f} w15_at_bar@{w15[j]:.2f} bar_passed@{(st[j, 3] - st[j, 0]) * 10 / 1000:.2f}")
 print(f"SUMMARY lib={os.environ.get('STAMPS_LIB')} SW={SW} S={S} grid={grid}: mean span "
       f"{np.mean([a for a, _ in summary]):.1f}us, mean dispatch spread {np.mean([b for _, b in summary]):.1f}us")
