@@ -220,12 +220,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU: bind the device BEFORE the RCCL communicator exists
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
     n_tokens = int(args.tokens)
     B, V, K, W = args.batch, args.vocab, args.steps, max(1, args.warmup)
 

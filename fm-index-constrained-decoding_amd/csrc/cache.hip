@@ -21,6 +21,7 @@
 #include "fmidx_internal.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
@@ -144,6 +145,51 @@ int device_build_cache(Index* h, hipStream_t s) {
     frontier.swap(next);
   }
   seen.clear();
+
+  if (env_u64("FMIDX_CACHE_STATS", 0)) {
+    // diagnostic: distinct symbols summed over the cached ranges, and their width histogram
+    uint64_t sum = 0, maxk = 0, hist[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t sigma = (uint64_t)h->max_sym + 1;
+    for (size_t i0 = 1; i0 < nodes.size();) {
+      std::vector<uint64_t> lo, hi, off{0};
+      size_t i1 = i0;
+      while (i1 < nodes.size()) {
+        const uint64_t cap = std::min<uint64_t>(nodes[i1].second - nodes[i1].first, sigma);
+        if (i1 > i0 && off.back() + cap > (1ull << 25)) break;
+        lo.push_back(nodes[i1].first);
+        hi.push_back(nodes[i1].second);
+        off.push_back(off.back() + cap);
+        ++i1;
+      }
+      const uint64_t m = i1 - i0, total = off.back();
+      DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_k;
+      DBuf<uint8_t> d_ws;
+      if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(total) || d_cnt.alloc(total) ||
+          d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(total)))
+        return -1;
+      FM_HIP(hipMemcpyAsync(d_lo.p, lo.data(), m * 8, hipMemcpyHostToDevice, s));
+      FM_HIP(hipMemcpyAsync(d_hi.p, hi.data(), m * 8, hipMemcpyHostToDevice, s));
+      FM_HIP(hipMemcpyAsync(d_off.p, off.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+      if (launch_distinct(v, d_lo.p, d_hi.p, m, d_off.p, d_syms.p, d_cnt.p, d_k.p, d_ws.p, total, s)) return -1;
+      std::vector<uint64_t> k(m);
+      FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, s));
+      FM_HIP(hipStreamSynchronize(s));
+      for (uint64_t r = 0; r < m; ++r) {
+        sum += k[r];
+        maxk = std::max(maxk, k[r]);
+        int b = 0;
+        while (b < 7 && k[r] >= (16ull << (2 * b))) ++b;
+        hist[b]++;
+      }
+      i0 = i1;
+    }
+    fprintf(stderr, "[fmidx] cache: %zu ranges >= %llu, distinct symbols summed %llu (max %llu); "
+            "distinct-count histogram <16,<64,<256,<1K,<4K,<16K,<64K,>=: %llu %llu %llu %llu %llu %llu %llu %llu; "
+            "edges between cached ranges %zu\n", nodes.size(), (unsigned long long)Wc, (unsigned long long)sum,
+            (unsigned long long)maxk, (unsigned long long)hist[0], (unsigned long long)hist[1],
+            (unsigned long long)hist[2], (unsigned long long)hist[3], (unsigned long long)hist[4],
+            (unsigned long long)hist[5], (unsigned long long)hist[6], (unsigned long long)hist[7], edges.size());
+  }
 
   // ---- bitmaps (packed masks in symbol space, exactly the hierarchy layout)
   const uint64_t N = nodes.size();

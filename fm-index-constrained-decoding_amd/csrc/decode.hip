@@ -268,24 +268,40 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // (packed, one uint32 store); chunk k of a slice is owned by one thread in
 // both the early zero-fill and the final emit.
 template <bool PACKED, bool DO_LF>
-__global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t* __restrict__ tok,
-                                                       int64_t shift, int64_t reset_below,
+// Argument order: the per-row state pointers and the slice geometry come first
+// so that, with kernel-argument preloading (Makefile: -amdgpu-kernarg-preload-
+// count), they arrive in SGPRs at dispatch and the row-state loads issue
+// before any kernel-argument memory load; the large DevView comes last.
+__global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restrict__ tok,
                                                        const uint64_t* __restrict__ lo_in,
-                                                       const uint64_t* __restrict__ hi_in,
+                                                       const uint64_t* __restrict__ hi_in, uint64_t m,
+                                                       uint32_t S, uint32_t SW, uint64_t vocab,
                                                        uint64_t* __restrict__ lo_out,
-                                                       uint64_t* __restrict__ hi_out, uint64_t m,
+                                                       uint64_t* __restrict__ hi_out,
+                                                       int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
-                                                       uint64_t vocab, uint32_t S, uint32_t SW,
-                                                       uint64_t early_width) {
+                                                       uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
   __shared__ uint64_t s_lohi[2];
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
-  FM_STAMP(v, 0);
-  FM_PRELOAD_VIEW(v);
   uint64_t row;
   uint32_t slice;
   map_block(blockIdx.x, S, row, slice);
+  // The row state first, as VECTOR loads (vmcnt) through the preloaded
+  // pointers: FM_PRELOAD_VIEW's scalar loads then wait on lgkmcnt alone and do
+  // not serialise behind (or in front of) the state's round trip.
+  const uint32_t srow = (uint32_t)(row < m ? row : 0);
+  const __amdgpu_buffer_rsrc_t r_lo = make_rsrc(lo_in, (uint32_t)(m * 8));
+  const __amdgpu_buffer_rsrc_t r_hi = make_rsrc(hi_in, (uint32_t)(m * 8));
+  typedef unsigned v2u __attribute__((ext_vector_type(2)));
+  const v2u ql = __builtin_amdgcn_raw_buffer_load_b64(r_lo, srow * 8, 0, 0);
+  const v2u qh = __builtin_amdgcn_raw_buffer_load_b64(r_hi, srow * 8, 0, 0);
+  v2u qt = {0u, 0u};
+  if (DO_LF) qt = __builtin_amdgcn_raw_buffer_load_b64(make_rsrc(tok, (uint32_t)(m * 8)), srow * 8, 0, 0);
+  FM_STAMP(v, 0);
+  const uint64_t st_lo = (uint64_t)ql.x | ((uint64_t)ql.y << 32), st_hi = (uint64_t)qh.x | ((uint64_t)qh.y << 32);
+  const int64_t st_tok = (int64_t)((uint64_t)qt.x | ((uint64_t)qt.y << 32));
   if (row >= m) return;
   const uint64_t t0 = (uint64_t)slice * SW;
   if (t0 >= vocab) return;
@@ -299,10 +315,11 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   // chunks holding an allowed token.
   bool early_zero;
   {
-    const uint64_t l0 = lo_in[row], h0 = min(hi_in[row], v.n);
-    const bool reset = DO_LF && tok[row] < reset_below;
+    const uint64_t l0 = st_lo, h0 = min(st_hi, v.n);
+    const bool reset = DO_LF && st_tok < reset_below;
     early_zero = !reset && (l0 >= h0 || h0 - l0 <= early_width);
   }
+  FM_PRELOAD_VIEW(v);   // after the state loads are in flight (see above)
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
   // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
   const __amdgpu_buffer_rsrc_t orsrc =
@@ -326,11 +343,11 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(DevView v, const int64_t
   // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
   // (all 64 lanes), published with the range by a single barrier.
   if (threadIdx.x < 64) {
-    uint64_t l = lo_in[row], h = hi_in[row];
+    uint64_t l = st_lo, h = st_hi;
     int64_t follow = -1;
     const uint32_t* tbm = nullptr;   // bitmap of the new range, when the edge table knew it
     if (DO_LF) {
-      const int64_t t = tok[row];
+      const int64_t t = st_tok;
       if (t < reset_below) {
         l = 0;
         h = v.n;
@@ -604,8 +621,8 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
   }();
 #define FM_LAUNCH(P, L)                                                                                       \
-  k_decode<P, L><<<g, kDecThreads, 0, s>>>(v, tok, shift, reset_below, lo_in, hi_in, lo_out, hi_out, m, mask, \
-                                           ld, vocab, S, SW, ew)
+  k_decode<P, L><<<g, kDecThreads, 0, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
+                                           mask, ld, ew, v)
   if (do_lf) {
     if (packed) FM_LAUNCH(true, true);
     else FM_LAUNCH(false, true);
