@@ -53,6 +53,7 @@ class _BatchedCore:
     def __init__(self, index):
         self.index = index
         self._uni_cache = {}
+        self._prev = {}     # pattern tuple -> (lo, hi) from the previous ranges() call
 
     # -- index work ---------------------------------------------------------
     def counts(self, patterns: Sequence[Sequence[int]]) -> List[int]:
@@ -62,10 +63,30 @@ class _BatchedCore:
         return (hi.astype(np.int64) - lo.astype(np.int64)).tolist()
 
     def ranges(self, patterns: Sequence[Sequence[int]]):
+        """get_range of every pattern (index.py:103-114), incrementally: during
+        decoding a row's pattern is usually last step's pattern plus one token,
+        and get_range is a left-to-right loop of LF steps with an early exit at
+        (0, 0), so range(p) == one LF step of range(p[:-1]) by p[-1] -- bit for
+        bit the reference's value.  Rows that do not extend a pattern of the
+        previous call are searched in full; both kinds go in one launch."""
         if not patterns:
+            self._prev = {}
             z = np.zeros(0, dtype=np.uint64)
             return z, z
-        return self.index.get_range_batch(patterns, SHIFT)
+        n = self.index.size()
+        keys = [tuple(int(t) for t in p) for p in patterns]
+        toks, slo, shi = [], np.zeros(len(keys), dtype=np.uint64), np.zeros(len(keys), dtype=np.uint64)
+        for i, k in enumerate(keys):
+            prev = self._prev.get(k[:-1]) if k else None
+            if prev is not None:
+                slo[i], shi[i] = prev
+                toks.append(k[-1:])
+            else:
+                slo[i], shi[i] = 0, n
+                toks.append(k)
+        lo, hi = self.index.get_range_batch(toks, SHIFT, starts=(slo, shi))
+        self._prev = {k: (l, h) for k, l, h in zip(keys, lo.tolist(), hi.tolist())}
+        return lo, hi
 
     def allowed_bits(self, lo: np.ndarray, hi: np.ndarray, vocab: int):
         device = torch.device("cuda", self.index.device)
