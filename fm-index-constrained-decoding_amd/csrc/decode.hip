@@ -151,44 +151,33 @@ __device__ __forceinline__ void set_bit(uint32_t* win, uint32_t sym, int64_t bas
 // unaligned tail.  The first round's loads -- every head/tail symbol (threads
 // 0..11) and kUnroll uint4 per thread of the concatenated middles -- are all
 // issued before any is consumed, so a partial end of up to 16K symbols costs
-// one memory round trip.
-struct StreamParts {
-  uint64_t q0, n0, q1, n1;       // uint4 middles: [q0, q0+n0) and [q1, q1+n1)
-  uint64_t piece[4];             // head/tail start positions
-  uint32_t plen[4];              // head/tail lengths (0..3)
-};
+// one memory round trip.  Everything is computed in registers: an aggregate
+// selected with a lane-varying index lands in scratch, and a scratch store +
+// load ahead of the first BWT load adds a round trip (plus the store's
+// acknowledgement, shared vmcnt) to the chain.
 
-__device__ __forceinline__ void split_part(uint64_t a, uint64_t b, uint64_t& q, uint64_t& nq, uint64_t& h,
-                                           uint32_t& hl, uint64_t& t, uint32_t& tl) {
-  hl = tl = 0;
-  q = nq = 0;
-  h = t = 0;
+// the aligned middle of [a, b) as uint4 indices [q, q + nq)
+__device__ __forceinline__ void middle_of(uint64_t a, uint64_t b, uint64_t& q, uint64_t& nq) {
+  const uint64_t a4 = (a + 3) & ~3ull, b4 = b & ~3ull;
+  const bool has = a < b && a4 < b4;
+  q = has ? a4 / 4 : 0;
+  nq = has ? (b4 - a4) / 4 : 0;
+}
+
+// head (tail = false) or tail piece of [a, b): start position and length (0..3)
+__device__ __forceinline__ void piece_of(uint64_t a, uint64_t b, bool tail, uint64_t& pos, uint32_t& len) {
+  pos = 0;
+  len = 0;
   if (a >= b) return;
   const uint64_t a4 = (a + 3) & ~3ull, b4 = b & ~3ull;
-  if (a4 >= b4) {            // fewer than one aligned uint4: up to 6 symbols as head+tail
-    h = a;
-    hl = (uint32_t)min((uint64_t)3, b - a);
-    t = a + hl;
-    tl = (uint32_t)(b - t);
+  if (a4 >= b4) {            // fewer than one aligned uint4: up to 6 symbols as head + tail
+    const uint32_t hl = (uint32_t)min((uint64_t)3, b - a);
+    pos = tail ? a + hl : a;
+    len = tail ? (uint32_t)(b - a - hl) : hl;
     return;
   }
-  h = a;
-  hl = (uint32_t)(a4 - a);
-  t = b4;
-  tl = (uint32_t)(b - b4);
-  q = a4 / 4;
-  nq = (b4 - a4) / 4;
-}
-
-__device__ __forceinline__ StreamParts make_parts(uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1) {
-  StreamParts p;
-  split_part(a0, b0, p.q0, p.n0, p.piece[0], p.plen[0], p.piece[1], p.plen[1]);
-  split_part(a1, b1, p.q1, p.n1, p.piece[2], p.plen[2], p.piece[3], p.plen[3]);
-  return p;
-}
-
-__device__ __forceinline__ uint4 part_u4(const uint4* src, const StreamParts& p, uint64_t j) {
-  return src[j < p.n0 ? p.q0 + j : p.q1 + (j - p.n0)];
+  pos = tail ? b4 : a;
+  len = tail ? (uint32_t)(b - b4) : (uint32_t)(a4 - a);
 }
 
 __device__ __forceinline__ void set_u4(uint32_t* win, const uint4& q, int64_t base_bit, int64_t lim) {
@@ -199,21 +188,28 @@ __device__ __forceinline__ void set_u4(uint32_t* win, const uint4& q, int64_t ba
 }
 
 // by threads [0, nthr) of the workgroup
-__device__ void stream_symbols(const uint32_t* __restrict__ bwt, const StreamParts& sp, int64_t base_bit,
-                               int64_t lim, uint32_t* win, uint32_t nthr) {
-  const uint64_t ntot = sp.n0 + sp.n1;
+__device__ __forceinline__ void stream_symbols(const uint32_t* __restrict__ bwt, uint64_t a0, uint64_t b0,
+                                               uint64_t a1, uint64_t b1, int64_t base_bit, int64_t lim,
+                                               uint32_t* win, uint32_t nthr) {
+  uint64_t q0, n0, q1, n1;
+  middle_of(a0, b0, q0, n0);
+  middle_of(a1, b1, q1, n1);
+  const uint64_t ntot = n0 + n1;
   const uint4* src = reinterpret_cast<const uint4*>(bwt);
   uint32_t hsym = ~0u;          // head/tail symbols: threads 0..11, loaded with the first round
   if (threadIdx.x < 12) {
     const uint32_t pc = threadIdx.x / 3, k = threadIdx.x % 3;
-    if (k < sp.plen[pc]) hsym = bwt[sp.piece[pc] + k];
+    uint64_t pp;
+    uint32_t pl;
+    piece_of(pc < 2 ? a0 : a1, pc < 2 ? b0 : b1, (pc & 1) != 0, pp, pl);
+    if (k < pl) hsym = bwt[pp + k];
   }
   for (uint64_t base = threadIdx.x; base < ntot; base += (uint64_t)nthr * kUnroll) {
     uint4 q[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t j = base + (uint64_t)u * nthr;
-      q[u] = (j < ntot) ? part_u4(src, sp, j) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      q[u] = (j < ntot) ? src[j < n0 ? q0 + j : q1 + (j - n0)] : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -243,6 +239,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
 
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x) {
   v4u v = {x.x, x.y, x.z, x.w};
@@ -284,6 +281,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
   __shared__ uint64_t s_lohi[2];
+  FM_STAMP_DECL;
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   uint64_t row;
   uint32_t slice;
@@ -359,10 +357,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }
-      if (slice == 0 && threadIdx.x == 0) {
-        lo_out[row] = l;
-        hi_out[row] = h;
-      }
     }
     l = __shfl(l, 0, 64);
     h = __shfl(h, 0, 64);
@@ -429,7 +423,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
       // streamed only
       const uint32_t nthr = early_zero ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
       if (threadIdx.x < nthr)
-        stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win, nthr);
+        stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
       FM_STAMP(v, 4);
     } else {
       // The first batch of bitmap words (<= 8 per thread) is loaded before the
@@ -446,7 +440,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
         const uint32_t qq = g + (uint32_t)u * G;
         x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
       }
-      stream_symbols(v.bwt, make_parts(plan.a0, plan.b0, plan.a1, plan.b1), base_bit, lim, win, kDecThreads);
+      stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
       FM_STAMP(v, 4);
       // G groups split the bitmaps, each thread owns one uint4 of the window
       // (several when the window is wider than the workgroup); partial ORs
@@ -549,7 +543,15 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
       }
     }
   }
+  // The new row state is stored last: wave 0 loads after its LF step (cache
+  // probe, partial ends), and with a store ahead of them in the shared vmcnt
+  // queue each of those waits would include the store's acknowledgement.
+  if (DO_LF && slice == 0 && threadIdx.x == 0) {
+    lo_out[row] = lo;
+    hi_out[row] = hi;
+  }
   FM_STAMP(v, 7);
+  FM_STAMP_FLUSH(v);
 }
 
 // cache probe per row (one wave each): 1 if [lo, hi) has a cached bitmap

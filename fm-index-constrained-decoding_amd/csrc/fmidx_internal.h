@@ -105,23 +105,39 @@ struct DevView {
 #endif
 };
 
-// Diagnostic phase stamps (s_memrealtime, 100 MHz), compiled only with -DFMIDX_STAMPS.
+// Diagnostic phase stamps (s_memrealtime, 100 MHz), compiled only with
+// -DFMIDX_STAMPS.  They are kept in LDS and written out once at the end of the
+// workgroup, so the stamped kernel issues no extra global store inside its
+// dependent chain (a store ahead of a load in the shared vmcnt queue would
+// make the load's wait include the store's acknowledgement).
 #ifdef FMIDX_STAMPS
-#define FM_STAMP(v, slot)                                                              \
-  do {                                                                                 \
-    if (threadIdx.x == 0 && (v).stamps)                                                \
-      (v).stamps[(uint64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+#define FM_STAMP_DECL                                                    \
+  __shared__ uint64_t s_stamp_[8];                                       \
+  if (threadIdx.x == 0)                                                  \
+    for (int s_ = 0; s_ < 8; ++s_)                                       \
+      if (s_ != 5) s_stamp_[s_] = 0
+#define FM_STAMP(v, slot)                                                \
+  do {                                                                   \
+    if (threadIdx.x == 0) s_stamp_[(slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-#define FM_STAMP_T(v, slot, tid)                                                         \
-  do {                                                                                 \
-    if (threadIdx.x == (tid) && (v).stamps)                                            \
-      (v).stamps[(uint64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+#define FM_STAMP_T(v, slot, tid)                                         \
+  do {                                                                   \
+    if (threadIdx.x == (tid)) s_stamp_[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define FM_STAMP_FLUSH(v)                                                \
+  do {                                                                   \
+    if (threadIdx.x == 0 && (v).stamps)                                  \
+      for (int s_ = 0; s_ < 8; ++s_) (v).stamps[(uint64_t)blockIdx.x * 8 + s_] = s_stamp_[s_]; \
   } while (0)
 #else
+#define FM_STAMP_DECL
 #define FM_STAMP_T(v, slot, tid) \
   do {                           \
   } while (0)
 #define FM_STAMP(v, slot) \
+  do {                    \
+  } while (0)
+#define FM_STAMP_FLUSH(v) \
   do {                    \
   } while (0)
 #endif

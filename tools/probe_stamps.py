@@ -69,6 +69,15 @@ for s in range(W, W + 12):
     t2 = (st[:, 2] - st[:, 0]) * 10 / 1000
     print(f"   last-wave arrival at plan barrier (from WG start): median {np.median(w15):.2f} us, "
           f"max {w15.max():.2f}; wave-0 LF done median {np.median(t2[st[:, 2] > 0]):.2f} us")
+    def cls(w):
+        return np.select([w == 0, w <= 64, w <= 512, w < 4096], ["0", "<=64", "<=512", "<4096"], ">=4096")
+    key = np.char.add(np.char.add(cls(w_old), "->"), cls(w_new))
+    agg = {}
+    for k, e, l2 in zip(key, end_rel, (st[:, 2] - st[:, 0]) * 10 / 1000):
+        agg.setdefault(k, []).append((e, l2))
+    print("   by class (old->new width): " + "; ".join(
+        f"{k} n={len(v)} end mean {np.mean([a for a, _ in v]):.1f} max {np.max([a for a, _ in v]):.1f}"
+        for k, v in sorted(agg.items(), key=lambda kv: -np.max([a for a, _ in kv[1]]))))
     for j in np.argsort(-end_rel)[:4]:
         print(f"   slowest-ending WG row {rows[j]} width {w_old[j]}->{w_new[j]} start "
               f"{(st[j, 0] - t0) * 10 / 1000:.1f} end {end_rel[j]:.1f}: " +
