@@ -327,6 +327,9 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   // so a wave with stores in flight cannot wait on a load without also
   // waiting for them -- wave 0 (LF + plan) must stay store-free.
   if (early_zero && threadIdx.x >= 64) {
+#ifdef FMIDX_ZERO_DELAY
+    for (int d_ = 0; d_ < FMIDX_ZERO_DELAY; ++d_) __builtin_amdgcn_s_sleep(16);   // experiment: hold the zero-fill back
+#endif
     for (uint64_t k = threadIdx.x - 64; k < nch; k += kDecThreads - 64) {
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
@@ -480,46 +483,65 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
     lds_barrier();
   }
   FM_STAMP(v, 6);
-  // the final stores to a zeroed chunk must land after its zero store (same
-  // thread, same address): drain this wave's outstanding stores first
+  // A zeroed chunk's final store follows its zero store from the same thread
+  // to the same address, in program order: per-location coherence orders the
+  // two, no wait for the zero stores' acknowledgements is needed.
   const bool zeroed = early_zero || late_zero;
+#ifdef FMIDX_ZERO_WAIT
   if (zeroed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
   if (direct) {
-    // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH); 4 chunks' words
-    // are loaded before any is converted and stored.  Chunk ownership as in
-    // the zero-fill (threads >= e_first) when the row was zeroed early.
+    // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH).  All of a
+    // thread's chunks (kDirectU per round, one round for a 128k-152k vocab)
+    // have their words loaded before any is converted and stored: the emit is
+    // one memory round trip.  Chunk ownership as in the zero-fill (threads >=
+    // e_first) when the row was zeroed early.
     const uint32_t* bm = plan.ptr[0];
-    const int64_t wlim = (int64_t)v.bm_words;
+    const uint32_t wlim = v.bm_words;
     const uint32_t nt = kDecThreads - e_first;
-    for (uint64_t k0 = threadIdx.x - e_first; threadIdx.x >= e_first && k0 < nch; k0 += (uint64_t)nt * 4) {
-      uint64_t w2[4];
+    const uint32_t nch32 = (uint32_t)nch;
+    const uint32_t bit0 = (uint32_t)((int64_t)t0 + shift);   // < 2^27: 32-bit chunk arithmetic
+    constexpr int kDirectU = (kDecThreads >= 1024) ? 8 : 4;
+    for (uint32_t k0 = threadIdx.x - e_first; threadIdx.x >= e_first && k0 < nch32; k0 += nt * kDirectU) {
+      uint32_t wa[kDirectU], wb[kDirectU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t k = k0 + (uint64_t)u * nt;
-        const int64_t bit = (int64_t)t0 + shift + (int64_t)k * CH;
-        const int64_t wi = bit >> 5;
-        const uint32_t a = (k < nch && wi < wlim) ? bm[wi] : 0u;
-        const uint32_t b = (k < nch && wi + 1 < wlim) ? bm[wi + 1] : 0u;
-        w2[u] = ((uint64_t)a | ((uint64_t)b << 32)) >> (bit & 31);
+      for (int u = 0; u < kDirectU; ++u) {
+        const uint32_t k = k0 + (uint32_t)u * nt;
+        const uint32_t wi = (bit0 + k * CH) >> 5;
+        wa[u] = (k < nch32 && wi < wlim) ? bm[wi] : 0u;
+        wb[u] = (k < nch32 && wi + 1 < wlim) ? bm[wi + 1] : 0u;
       }
+      uint32_t slow = 0;   // chunks needing byte stores (a short last chunk / unaligned row): after the loop
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t k = k0 + (uint64_t)u * nt;
-        if (k >= nch) break;
-        const uint64_t t = t0 + k * CH;
-        const uint64_t cnt = min((uint64_t)CH, t1 - t);
-        uint32_t bits = (uint32_t)w2[u];
+      for (int u = 0; u < kDirectU; ++u) {
+        const uint32_t k = k0 + (uint32_t)u * nt;
+        if (k >= nch32) break;
+        const uint32_t o = (bit0 + k * CH) & 31u;
+        const uint64_t t = t0 + (uint64_t)k * CH;
+        const bool full = t + CH <= t1;
+        uint32_t bits = (uint32_t)((((uint64_t)wb[u] << 32) | wa[u]) >> o);
         if (CH == 16) bits &= 0xFFFFu;
-        if (cnt < CH) bits &= (1u << cnt) - 1u;
+        if (PACKED && !full) bits &= (1u << (uint32_t)(t1 - t)) - 1u;
         if (zeroed && bits == 0) continue;
         if (PACKED) {
-          store4(orsrc, (uint32_t)(k * 4), bits);
-        } else if (aligned16 && cnt == 16) {
-          store16(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits));
+          store4(orsrc, k * 4, bits);
+        } else if (aligned16 && full) {
+          store16(orsrc, k * 16, bits16_to_bytes(bits));
         } else {
-          for (uint64_t j = 0; j < cnt; ++j) out_row[t + j] = (uint8_t)((bits >> j) & 1u);
+          slow |= 1u << u;
         }
+      }
+#pragma unroll 1
+      for (uint32_t u = 0; !PACKED && slow; ++u, slow >>= 1) {
+        if (!(slow & 1u)) continue;
+        const uint32_t k = k0 + u * nt;
+        const uint32_t wi = (bit0 + k * CH) >> 5, o = (bit0 + k * CH) & 31u;
+        const uint32_t a = wi < wlim ? bm[wi] : 0u, b = wi + 1 < wlim ? bm[wi + 1] : 0u;
+        const uint32_t bits = (uint32_t)((((uint64_t)b << 32) | a) >> o);
+        const uint64_t t = t0 + (uint64_t)k * CH;
+        const uint32_t cnt = (uint32_t)min((uint64_t)CH, t1 - t);
+        for (uint32_t j = 0; j < cnt; ++j) out_row[t + j] = (uint8_t)((bits >> j) & 1u);
       }
     }
   } else if (threadIdx.x >= e_first) {
