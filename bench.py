@@ -378,7 +378,8 @@ def main():
         f"bytes/step {decode_bytes / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
         f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}, "
         f"cached rows {cached.mean():.3f} (cache: {st['cache_nodes']} ranges >= {st['cache_min']}, "
-        f"{st['cache_bytes'] / 2**30:.1f} GiB)")
+        f"{st['cache_bytes'] / 2**30:.1f} GiB; transitions {st['trans_entries']} "
+        f"(+{st['trans_dropped']} left out), {st['trans_bytes'] / 2**30:.1f} GiB)")
 
     result = {
         "metric": METRIC,

@@ -47,7 +47,7 @@ void Index::release() {
   if (cache_tab) (void)hipFree(cache_tab);
   if (trans_tab) (void)hipFree(trans_tab);
   trans_tab = nullptr;
-  trans_entries = 0;
+  trans_entries = trans_dropped = trans_bytes = 0;
   cache_bm = nullptr;
   cache_tab = nullptr;
   cache_nodes = cache_bytes = 0;
@@ -774,6 +774,15 @@ int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint
   if (cache_nodes) *cache_nodes = x.cache_nodes;
   if (cache_bytes) *cache_bytes = x.cache_bytes;
   if (cache_min) *cache_min = x.view.cache_mask ? x.view.cache_min : 0;
+  return 0;
+}
+
+int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes) {
+  FM_CHECK_BUILT(h);
+  const auto& x = h->idx;
+  if (entries) *entries = x.trans_entries;
+  if (dropped) *dropped = x.trans_dropped;
+  if (bytes) *bytes = x.trans_bytes;
   return 0;
 }
 

@@ -21,6 +21,7 @@
 #include "fmidx_internal.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -58,6 +59,166 @@ struct DBuf {
 
 }  // namespace
 
+// Cache id + 1 of [lo, hi), or 0: one thread's linear probe of the cache table.
+__device__ uint64_t cache_id_thread(const DevView& v, uint64_t lo, uint64_t hi) {
+  if (!v.cache_mask || hi - lo < v.cache_min) return 0;
+  uint64_t slot = cache_hash(lo, hi) & v.cache_mask;
+  for (uint64_t i = 0; i <= v.cache_mask; ++i) {
+    const uint64_t e0 = v.cache_tab[2 * slot], e1 = v.cache_tab[2 * slot + 1];
+    if (e0 == kCacheEmpty) return 0;
+    if (e0 == lo && (e1 & kMask34) == hi) return (e1 >> kCacheIdShift) + 1;
+    slot = (slot + 1) & v.cache_mask;
+  }
+  return 0;
+}
+
+// Insert the children of a batch of cached parents (k_distinct output: row r's
+// k[r] symbols, counts and child starts at off[r]) into the transition table.
+// One workgroup per parent; a slot is claimed by CAS on its first word; a key
+// whose home run of kTransProbe slots is full is left out (the decode step then
+// takes the wavelet-matrix descent for it).
+__global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t* __restrict__ plo,
+                                                      const uint64_t* __restrict__ phi,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ k,
+                                                      const uint64_t* __restrict__ syms,
+                                                      const uint64_t* __restrict__ cnt,
+                                                      const uint64_t* __restrict__ child, uint64_t m,
+                                                      uint64_t* __restrict__ tab, uint64_t cap,
+                                                      unsigned long long* __restrict__ stats) {
+  const uint64_t r = blockIdx.x;
+  if (r >= m) return;
+  const uint64_t kr = k[r];
+  if (kr == ~0ull) return;
+  const uint64_t lo = plo[r], hi = phi[r], base = off[r];
+  unsigned long long ins = 0, drop = 0;
+  for (uint64_t j = threadIdx.x; j < kr; j += 256) {
+    const uint64_t c = syms[base + j], cw = cnt[base + j], clo = child[base + j];
+    uint64_t aux = 0;
+    if (cw >= v.cache_min) {
+      aux = cache_id_thread(v, clo, clo + cw);
+    } else if (cw == 1) {
+      const uint64_t sym = v.bwt[clo];
+      if (sym < kTransOne) aux = kTransOne | sym;
+    }
+    const uint64_t w0 = lo | (c << kTransSymShift);
+    const uint64_t w1 = hi | ((clo & ((1ull << 30) - 1)) << kTransSymShift);
+    const uint64_t w2 = (clo >> 30) | (cw << 4) | (aux << 38);
+    uint64_t slot = trans_home(lo, hi, c, cap);
+    bool done = false;
+    for (uint32_t d = 0; d < kTransProbe && !done; ++d) {
+      unsigned long long* p = reinterpret_cast<unsigned long long*>(tab + 3 * slot);
+      if (atomicCAS(p, (unsigned long long)kTransEmpty, (unsigned long long)w0) == kTransEmpty) {
+        tab[3 * slot + 1] = w1;
+        tab[3 * slot + 2] = w2;
+        done = true;
+      }
+      if (++slot == cap) slot = 0;
+    }
+    if (done) ++ins; else ++drop;
+  }
+  if (ins) atomicAdd(&stats[0], ins);
+  if (drop) atomicAdd(&stats[1], drop);
+}
+
+// Transition table of the cached ranges (all their children, or -- when that
+// would exceed FMIDX_TRANS_MB -- only the cached ones), built on the GPU from
+// two k_distinct passes over the cached parents: one to count the entries,
+// one to insert them.
+int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>& nodes, hipStream_t s) {
+  DevView& v = h->view;
+  v.trans_cap = 0;
+  v.trans_tab = nullptr;
+  if (h->trans_tab) (void)hipFree(h->trans_tab);
+  h->trans_tab = nullptr;
+  h->trans_entries = h->trans_dropped = h->trans_bytes = 0;
+  const uint64_t mode = env_u64("FMIDX_TRANS", 2);   // 2 = every child, 1 = cached children only, 0 = none
+  if (mode == 0 || nodes.size() < 2 || !v.cache_mask) return 0;
+  const uint64_t budget = env_u64("FMIDX_TRANS_MB", 72ull << 10) << 20;
+  const uint64_t sigma = (uint64_t)h->max_sym + 1;
+  const uint64_t kChunkCap = 1ull << 25;
+  // parents: every cached range but the root (whose LF step is the C lookup)
+  auto pass = [&](uint64_t min_count, uint64_t* tab, uint64_t cap, uint64_t& total,
+                  unsigned long long* d_stats) -> int {
+    total = 0;
+    for (size_t i0 = 1; i0 < nodes.size();) {
+      std::vector<uint64_t> lo, hi, off{0};
+      size_t i1 = i0;
+      while (i1 < nodes.size()) {
+        const uint64_t w = nodes[i1].second - nodes[i1].first;
+        const uint64_t c = std::min<uint64_t>(min_count > 1 ? w / min_count + 1 : w, sigma);
+        if (i1 > i0 && off.back() + c > kChunkCap) break;
+        lo.push_back(nodes[i1].first);
+        hi.push_back(nodes[i1].second);
+        off.push_back(off.back() + c);
+        ++i1;
+      }
+      const uint64_t m = i1 - i0, tot = off.back();
+      DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_child, d_k;
+      DBuf<uint8_t> d_ws;
+      if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(tot) || d_cnt.alloc(tot) ||
+          d_child.alloc(tot) || d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(tot)))
+        return -1;
+      FM_HIP(hipMemcpyAsync(d_lo.p, lo.data(), m * 8, hipMemcpyHostToDevice, s));
+      FM_HIP(hipMemcpyAsync(d_hi.p, hi.data(), m * 8, hipMemcpyHostToDevice, s));
+      FM_HIP(hipMemcpyAsync(d_off.p, off.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
+      if (launch_distinct(v, d_lo.p, d_hi.p, m, d_off.p, d_syms.p, d_cnt.p, d_k.p, d_ws.p, tot, s, min_count,
+                          d_child.p))
+        return -1;
+      if (tab) {
+        k_trans_insert<<<(unsigned)m, 256, 0, s>>>(v, d_lo.p, d_hi.p, d_off.p, d_k.p, d_syms.p, d_cnt.p,
+                                                   d_child.p, m, tab, cap, d_stats);
+        FM_HIP(hipGetLastError());
+        FM_HIP(hipStreamSynchronize(s));   // chunk buffers are freed on scope exit
+      } else {
+        std::vector<uint64_t> k(m);
+        FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, s));
+        FM_HIP(hipStreamSynchronize(s));
+        for (uint64_t r = 0; r < m; ++r) total += (k[r] == ~0ull) ? 0 : k[r];
+      }
+      i0 = i1;
+    }
+    return 0;
+  };
+  uint64_t min_count = mode >= 2 ? 1 : v.cache_min;
+  uint64_t entries = 0;
+  if (pass(min_count, nullptr, 0, entries, nullptr)) return -1;
+  uint64_t cap = std::max<uint64_t>(1024, entries + entries / 2 + entries / 4);   // load <= 0.57
+  if (cap * 24 > budget && min_count == 1) {   // over budget: the cached children only
+    min_count = v.cache_min;
+    if (pass(min_count, nullptr, 0, entries, nullptr)) return -1;
+    cap = std::max<uint64_t>(1024, 2 * entries);
+  }
+  if (entries == 0 || cap * 24 > budget) return 0;
+  uint64_t* tab = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&tab), cap * 24) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;   // no room: the descent serves every step
+  }
+  FM_HIP(hipMemsetAsync(tab, 0xFF, cap * 24, s));
+  DBuf<unsigned long long> d_stats;
+  if (d_stats.alloc(2)) {
+    (void)hipFree(tab);
+    return -1;
+  }
+  FM_HIP(hipMemsetAsync(d_stats.p, 0, 16, s));
+  uint64_t dummy = 0;
+  if (pass(min_count, tab, cap, dummy, d_stats.p)) {
+    (void)hipFree(tab);
+    return -1;
+  }
+  unsigned long long st[2] = {0, 0};
+  FM_HIP(hipMemcpy(st, d_stats.p, 16, hipMemcpyDeviceToHost));
+  h->trans_tab = tab;
+  h->trans_entries = st[0];
+  h->trans_dropped = st[1];
+  h->trans_bytes = cap * 24;
+  h->cache_bytes += cap * 24;
+  v.trans_tab = tab;
+  v.trans_cap = cap;
+  return 0;
+}
+
 int device_build_cache(Index* h, hipStream_t s) {
   DevView& v = h->view;
   v.cache_mask = 0;
@@ -76,10 +237,6 @@ int device_build_cache(Index* h, hipStream_t s) {
   std::vector<std::pair<uint64_t, uint64_t>> frontier{{0, n}}, next;
   nodes.push_back({0, n});
   seen.emplace(std::make_pair(uint64_t(0), n), 0);
-  struct Edge {
-    uint64_t plo, phi, c, clo, cw, id;
-  };
-  std::vector<Edge> edges;   // parent (not the root) -> cached child
   const uint64_t kChunkCap = 1ull << 24;   // child slots per k_distinct launch
   bool full = false;
   while (!frontier.empty() && !full) {
@@ -124,20 +281,16 @@ int device_build_cache(Index* h, hipStream_t s) {
         for (uint64_t j = 0; j < k[r]; ++j) {
           const uint64_t a = child[off[r] + j], b = a + cnt[off[r] + j];
           auto it = seen.find({a, b});
-          uint64_t id;
           if (it == seen.end()) {
             if (nodes.size() >= max_nodes) {
               full = true;
               break;
             }
-            id = nodes.size();
+            const uint64_t id = nodes.size();
             seen.emplace(std::make_pair(a, b), id);
             nodes.push_back({a, b});
             next.push_back({a, b});
-          } else {
-            id = it->second;
           }
-          if (!(lo[r] == 0 && hi[r] == n)) edges.push_back({lo[r], hi[r], sym[off[r] + j], a, b - a, id});
         }
       }
       i0 = i1;
@@ -149,6 +302,9 @@ int device_build_cache(Index* h, hipStream_t s) {
   if (env_u64("FMIDX_CACHE_STATS", 0)) {
     // diagnostic: distinct symbols summed over the cached ranges, and their width histogram
     uint64_t sum = 0, maxk = 0, hist[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t wsum = 0, ksum_w[6] = {0, 0, 0, 0, 0, 0};   // distinct summed over parents of width < 8K,32K,128K,512K,2M,inf
+    for (size_t i = 1; i < nodes.size(); ++i) wsum += nodes[i].second - nodes[i].first;
+    const auto t_stats = std::chrono::steady_clock::now();
     const uint64_t sigma = (uint64_t)h->max_sym + 1;
     for (size_t i0 = 1; i0 < nodes.size();) {
       std::vector<uint64_t> lo, hi, off{0};
@@ -177,6 +333,12 @@ int device_build_cache(Index* h, hipStream_t s) {
       for (uint64_t r = 0; r < m; ++r) {
         sum += k[r];
         maxk = std::max(maxk, k[r]);
+        {
+          const uint64_t w = hi[r] - lo[r];
+          int c = 0;
+          while (c < 5 && w >= (8192ull << (2 * c))) ++c;
+          ksum_w[c] += k[r];
+        }
         int b = 0;
         while (b < 7 && k[r] >= (16ull << (2 * b))) ++b;
         hist[b]++;
@@ -185,10 +347,15 @@ int device_build_cache(Index* h, hipStream_t s) {
     }
     fprintf(stderr, "[fmidx] cache: %zu ranges >= %llu, distinct symbols summed %llu (max %llu); "
             "distinct-count histogram <16,<64,<256,<1K,<4K,<16K,<64K,>=: %llu %llu %llu %llu %llu %llu %llu %llu; "
-            "edges between cached ranges %zu\n", nodes.size(), (unsigned long long)Wc, (unsigned long long)sum,
+            "\n", nodes.size(), (unsigned long long)Wc, (unsigned long long)sum,
             (unsigned long long)maxk, (unsigned long long)hist[0], (unsigned long long)hist[1],
             (unsigned long long)hist[2], (unsigned long long)hist[3], (unsigned long long)hist[4],
-            (unsigned long long)hist[5], (unsigned long long)hist[6], (unsigned long long)hist[7], edges.size());
+            (unsigned long long)hist[5], (unsigned long long)hist[6], (unsigned long long)hist[7]);
+    fprintf(stderr, "[fmidx] cache: widths summed %llu; distinct summed by parent width <8K,<32K,<128K,<512K,<2M,>=: "
+            "%llu %llu %llu %llu %llu %llu; stats pass %.1f s\n", (unsigned long long)wsum,
+            (unsigned long long)ksum_w[0], (unsigned long long)ksum_w[1], (unsigned long long)ksum_w[2],
+            (unsigned long long)ksum_w[3], (unsigned long long)ksum_w[4], (unsigned long long)ksum_w[5],
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_stats).count());
   }
 
   // ---- bitmaps (packed masks in symbol space, exactly the hierarchy layout)
@@ -242,43 +409,7 @@ int device_build_cache(Index* h, hipStream_t s) {
   v.cache_min = Wc;
   v.cache_mask = cap - 1;
 
-  // ---- edge table (cached parent, c) -> cached child: linear probing with
-  //      every key within 16 slots of its home (one 512-B probe round)
-  v.trans_mask = 0;
-  v.trans_tab = nullptr;
-  if (edges.empty() || env_u64("FMIDX_EDGE_TABLE", 1) == 0) return 0;
-  uint64_t tcap = 1024;
-  while (tcap < 4 * edges.size()) tcap <<= 1;
-  std::vector<uint64_t> et;
-  for (;;) {
-    et.assign(4 * tcap, 0);
-    for (uint64_t i = 0; i < tcap; ++i) et[4 * i] = kCacheEmpty;
-    bool ok = true;
-    for (const Edge& e : edges) {
-      const uint64_t home = trans_hash(e.plo, e.phi, e.c) & (tcap - 1);
-      uint64_t d = 0;
-      while (d < 16 && et[4 * ((home + d) & (tcap - 1))] != kCacheEmpty) ++d;
-      if (d == 16) {
-        ok = false;
-        break;
-      }
-      uint64_t* slot = &et[4 * ((home + d) & (tcap - 1))];
-      slot[0] = e.plo;
-      slot[1] = e.phi | (e.c << kCacheIdShift);
-      slot[2] = e.clo;
-      slot[3] = e.cw | ((e.id + 1) << kCacheIdShift);
-    }
-    if (ok) break;
-    tcap <<= 1;
-  }
-  FM_HIP(hipMalloc(reinterpret_cast<void**>(&h->trans_tab), tcap * 32));
-  FM_HIP(hipMemcpyAsync(h->trans_tab, et.data(), tcap * 32, hipMemcpyHostToDevice, s));
-  FM_HIP(hipStreamSynchronize(s));
-  h->trans_entries = edges.size();
-  h->cache_bytes += tcap * 32;
-  v.trans_tab = h->trans_tab;
-  v.trans_mask = tcap - 1;
-  return 0;
+  return build_transitions(h, nodes, s);
 }
 
 }  // namespace fmidx

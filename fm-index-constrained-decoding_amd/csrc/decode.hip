@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
                                                        uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
-  __shared__ uint64_t s_lohi[2];
+  __shared__ uint64_t s_lohi[3];   // new range + its only symbol when the transition table knew it (else ~0)
   FM_STAMP_DECL;
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   uint64_t row;
@@ -346,7 +346,8 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   if (threadIdx.x < 64) {
     uint64_t l = st_lo, h = st_hi;
     int64_t follow = -1;
-    const uint32_t* tbm = nullptr;   // bitmap of the new range, when the edge table knew it
+    const uint32_t* tbm = nullptr;   // bitmap of the new range, when the transition table knew it
+    int64_t one = -1;                // the new range's only symbol, when the transition table knew it
     if (DO_LF) {
       const int64_t t = st_tok;
       if (t < reset_below) {
@@ -356,7 +357,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
         // from the full range the LF step lands on symbol c's C-block, whose
         // allowed set is c's precomputed follow-set bitmap
         if (l == 0 && h >= v.n) follow = t + shift;
-        lf_step_decode(v, t + shift, l, h, tbm);
+        lf_step_decode(v, t + shift, l, h, tbm, one);
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }
@@ -364,14 +365,16 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
     l = __shfl(l, 0, 64);
     h = __shfl(h, 0, 64);
     follow = __shfl(follow, 0, 64);
+    one = __shfl(one, 0, 64);
     if (h > v.n) h = v.n;
     if (threadIdx.x == 0) {
       s_lohi[0] = l;
       s_lohi[1] = h;
+      s_lohi[2] = (uint64_t)one;
       plan.nb = 0;
       plan.a0 = plan.b0 = plan.a1 = plan.b1 = 0;
     }
-    if (l < h) {
+    if (l < h && one < 0) {
       // a wide range is looked up in the range-bitmap cache first (one
       // bitmap, nothing streamed); otherwise the aligned-bitmap plan
       const uint32_t* cb = tbm ? tbm : cache_find(v, l, h);
@@ -427,6 +430,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
       const uint32_t nthr = early_zero ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
       if (threadIdx.x < nthr)
         stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
+      if (threadIdx.x == 0 && (int64_t)s_lohi[2] >= 0) set_bit(win, (uint32_t)s_lohi[2], base_bit, lim);   // one-row range
       FM_STAMP(v, 4);
     } else {
       // The first batch of bitmap words (<= 8 per thread) is loaded before the

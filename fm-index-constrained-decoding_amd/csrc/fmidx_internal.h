@@ -86,10 +86,12 @@ struct DevView {
   const uint64_t* cache_tab;  // [cap][2] = {lo, hi | id << 34}; lo = ~0: empty
   uint64_t cache_mask;        // cap - 1 (cap a power of 2); 0 = no cache
   uint64_t cache_min;         // width threshold Wc
-  // edges of the cached ranges' LF graph: (cached parent, symbol c) -> the
-  // cached child LF_c(parent) and its bitmap id; 4 words per slot
+  // transition table of the cached ranges: (cached parent P, symbol c) ->
+  // LF_c(P) for every symbol c occurring in P (or, under a memory budget, only
+  // the cached children), with the child's bitmap id or, for a one-row child,
+  // its only symbol; 3 words per slot (layout at kTransSymShift below)
   const uint64_t* trans_tab;
-  uint64_t trans_mask;        // cap - 1; 0 = none
+  uint64_t trans_cap;         // slots; 0 = none
   const uint64_t* E;          // [n] LF(i) | BWT[i] << kESymShift (narrow-range LF + streaming), or null
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
@@ -155,7 +157,7 @@ struct DevView {
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
                  "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
-                 "s"((v).trans_mask));                                                                     \
+                 "s"((v).trans_cap));                                                                     \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -396,6 +398,26 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
   return cache_hash(lo ^ (c * 0xD6E8FEB86659FD93ull), hi + c);
 }
 
+// Transition slot (24 B, linear probing, every key within kTransProbe slots
+// of its home; keys that do not fit are left out and take the descent):
+//   w0 = plo | c << 34                       (empty: ~0)
+//   w1 = phi | (clo & (2^30 - 1)) << 34
+//   w2 = clo >> 30 | cw << 4 | aux << 38      aux: 0, cache id + 1 of the child,
+//                                             or kTransOne | the child's only symbol
+constexpr uint32_t kTransSymShift = 34;
+constexpr uint64_t kMask34 = (1ull << 34) - 1;
+constexpr uint64_t kTransOne = 1ull << 25;
+constexpr uint32_t kTransProbe = 16;
+constexpr uint64_t kTransEmpty = ~0ull;
+
+__host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi, uint64_t c, uint64_t cap) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __umul64hi(trans_hash(lo, hi, c), cap);
+#else
+  return (uint64_t)(((unsigned __int128)trans_hash(lo, hi, c) * cap) >> 64);
+#endif
+}
+
 // The LF step of the batched kernels, by all 64 lanes of a wave (uniform
 // inputs), with exactly one inlined copy of each path (a kernel's code is
 // fetched cold into the instruction cache at every launch, so duplicated
@@ -403,12 +425,14 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
 //   * full range: [C[c], C[c+1]) ([sdsl] backward_search shortcut);
 //   * <= kENarrow rows: one scan of E[lo, hi) (lf_step_fast);
 //   * otherwise the wavelet-matrix descent (NL2 round trips); a cached range
-//     also probes the edge table (cached parent, c) -> cached child, issued
-//     with the first descent level -- a hit ends the step after one round
-//     trip and names the child's bitmap in *cbm (else null).
+//     also probes the transition table, issued with the first descent level
+//     -- a hit ends the step after one round trip and names the child's
+//     bitmap in *cbm (else null) or, for a one-row child, its only symbol in
+//     *one (else -1).
 __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
-                                               const uint32_t*& cbm) {
+                                               const uint32_t*& cbm, int64_t& one) {
   cbm = nullptr;
+  one = -1;
   if (hi > v.n) hi = v.n;
   if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {
     lo = 0;
@@ -430,15 +454,14 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   const uint32_t q = lane & 31u;
   const bool side = lane >= 32;
   const uint64_t c = (uint64_t)sym;
-  // (1) edge probe of a cached range: 16 slots of 32 B by lanes 0-15
-  const bool probe = v.trans_mask && hi - lo >= v.cache_min;
-  const uint64_t k1 = hi | (c << kCacheIdShift);
-  uint4 ta = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0), tb = make_uint4(0, 0, 0, 0);
-  if (probe && lane < 16) {
-    const uint64_t slot = trans_hash(lo, hi, c) & v.trans_mask;
-    const uint4* e = reinterpret_cast<const uint4*>(v.trans_tab + 4 * ((slot + lane) & v.trans_mask));
-    ta = e[0];
-    tb = e[1];
+  // (1) transition probe of a cached range: 16 slots x 3 words, one word per lane 0-47
+  const bool probe = v.trans_cap && hi - lo >= v.cache_min;
+  const uint64_t key0 = lo | (c << kTransSymShift);
+  uint64_t tw = kTransEmpty;
+  if (probe && lane < 3 * kTransProbe) {
+    uint64_t slot = trans_home(lo, hi, c, v.trans_cap) + lane / 3;
+    if (slot >= v.trans_cap) slot -= v.trans_cap;
+    tw = v.trans_tab[3 * slot + lane % 3];
   }
   // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
@@ -452,16 +475,19 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
     const uint64_t r = rank_w2(v.w2[l], pos, d, q);
     if (l == 0 && probe) {   // the probe's loads were issued before this level's
-      const uint64_t w0 = (uint64_t)ta.x | ((uint64_t)ta.y << 32), w1 = (uint64_t)ta.z | ((uint64_t)ta.w << 32);
-      const uint64_t bh = __ballot(lane < 16 && w0 == lo && w1 == k1);
-      if (bh) {   // keys lie within 16 slots of their home (build invariant)
+      const uint64_t w1n = __shfl_down(tw, 1, 64);
+      const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
+      if (bh) {
         const int src = __ffsll((long long)bh) - 1;
-        const uint64_t w2 = (uint64_t)tb.x | ((uint64_t)tb.y << 32), w3 = (uint64_t)tb.z | ((uint64_t)tb.w << 32);
-        const uint64_t clo = __shfl(w2, src, 64);
-        const uint64_t x = __shfl(w3, src, 64);
+        const uint64_t w1 = __shfl(tw, src + 1, 64), w2 = __shfl(tw, src + 2, 64);
+        const uint64_t clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
+        const uint64_t aux = w2 >> 38;
         lo = clo;
-        hi = clo + (x & ((1ull << kCacheIdShift) - 1));
-        cbm = v.cache_bm + ((x >> kCacheIdShift) - 1) * v.bm_words;
+        hi = clo + ((w2 >> 4) & kMask34);
+        if (aux & kTransOne)
+          one = (int64_t)(aux & (kTransOne - 1));
+        else if (aux)
+          cbm = v.cache_bm + (aux - 1) * v.bm_words;
         return;
       }
     }
@@ -506,7 +532,7 @@ struct Index {
   uint32_t* cache_bm = nullptr;
   uint64_t* cache_tab = nullptr;
   uint64_t* trans_tab = nullptr;
-  uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0;
+  uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0, trans_dropped = 0, trans_bytes = 0;
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;
   uint32_t* text = nullptr;

@@ -40,7 +40,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
     h = v.n;
   } else {
     const uint32_t* cbm;
-    lf_step_decode(v, t + shift, l, h, cbm);
+    int64_t one;
+    lf_step_decode(v, t + shift, l, h, cbm, one);
   }
   if (lane == 0) {
     lo_out[i] = l;
@@ -61,7 +62,8 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
   const int64_t a = off[i], b = off[i + 1];
   for (int64_t j = a; j < b; ++j) {
     const uint32_t* cbm;
-    lf_step_decode(v, tok[j] + shift, l, h, cbm);
+    int64_t one;
+    lf_step_decode(v, tok[j] + shift, l, h, cbm, one);
     if (l == 0 && h == 0) break;       // index.py:111-112
   }
   if (lane == 0) {

@@ -241,6 +241,10 @@ class FMIndex:
         check(lib().fm_stats_ex(self._h, *[byref(v) for v in ex]), "stats_ex")
         for k, v in zip(["lf_levels", "lf_wm_bytes", "cache_nodes", "cache_bytes", "cache_min"], ex):
             out[k] = int(v.value)
+        tr = [c_uint64() for _ in range(3)]
+        check(lib().fm_stats_trans(self._h, *[byref(v) for v in tr]), "stats_trans")
+        for k, v in zip(["trans_entries", "trans_dropped", "trans_bytes"], tr):
+            out[k] = int(v.value)
         return out
 
     def cache_contains(self, lo, hi):

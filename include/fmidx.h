@@ -240,6 +240,11 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
 int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint64_t* cache_nodes,
                 uint64_t* cache_bytes, uint64_t* cache_min);
 
+/* Transition table of the cached ranges (cached parent, symbol) -> child range:
+ * entries inserted, entries left out (probe window full; those steps take the
+ * wavelet-matrix descent) and bytes in HBM. */
+int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes);
+
 /* For m device ranges, out[i] = 1 if [lo[i], hi[i]) has a cached bitmap
  * (accounting / tests; stream-ordered). */
 int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
