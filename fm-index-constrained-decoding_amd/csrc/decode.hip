@@ -280,7 +280,8 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
                                                        uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
-  __shared__ uint64_t s_lohi[3];   // new range + its only symbol when the transition table knew it (else ~0)
+  __shared__ uint64_t s_lohi[3];
+  __shared__ unsigned long long s_scan[2];   // workgroup E scan: first / last occurrence   // new range + its only symbol when the transition table knew it (else ~0)
   FM_STAMP_DECL;
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   uint64_t row;
@@ -311,12 +312,17 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   // can only shrink a range), so their slice is zero-filled right away --
   // the stores overlap the LF chain -- and the final pass rewrites only the
   // chunks holding an allowed token.
-  bool early_zero;
-  {
-    const uint64_t l0 = st_lo, h0 = min(st_hi, v.n);
-    const bool reset = DO_LF && st_tok < reset_below;
-    early_zero = !reset && (l0 >= h0 || h0 - l0 <= early_width);
-  }
+  const bool reset = DO_LF && st_tok < reset_below;
+  const uint64_t in_lo = st_lo, in_hi = min(st_hi, v.n);
+  const bool early_zero = !reset && (in_lo >= in_hi || in_hi - in_lo <= early_width);
+  // Incoming ranges of kENarrow+1 .. kEWide rows that the transition table does
+  // not serve take their LF step as ONE scan of E[lo, hi) by the whole
+  // workgroup (<= kEWide / kDecThreads entries per thread, one round trip)
+  // instead of the two-level descent; the other waves are idle until the plan
+  // anyway (such rows are not zero-filled early).
+  const bool wg_scan = DO_LF && !reset && v.E && in_lo < in_hi && in_hi - in_lo > kENarrow &&
+                       in_hi - in_lo <= kEWide && !(in_lo == 0 && in_hi == v.n) &&
+                       (in_hi - in_lo < v.cache_min || !v.trans_cap);
   FM_PRELOAD_VIEW(v);   // after the state loads are in flight (see above)
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
   // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
@@ -341,6 +347,41 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
       }
     }
   }
+  if (wg_scan) {
+    const uint64_t c = (uint64_t)(st_tok + shift);
+    constexpr int kU = (kEWide + kDecThreads - 1) / kDecThreads;
+    uint64_t e[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t idx = in_lo + threadIdx.x + (uint64_t)u * kDecThreads;
+      e[u] = idx < in_hi ? v.E[idx] : ~0ull;
+    }
+    if (threadIdx.x == 0) {
+      s_scan[0] = ~0ull;
+      s_scan[1] = 0;
+    }
+    lds_barrier();
+    // first / last occurrence of c as (relative row + 1) << 36 | LF: min / max
+    uint64_t fmin = ~0ull, fmax = 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (e[u] != ~0ull && (e[u] >> kESymShift) == c) {
+        const uint64_t pk = ((uint64_t)(threadIdx.x + u * kDecThreads + 1) << kESymShift) | (e[u] & kELfMask);
+        fmin = min(fmin, pk);
+        fmax = max(fmax, pk);
+      }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      fmin = min(fmin, (uint64_t)__shfl_xor(fmin, d, 64));
+      fmax = max(fmax, (uint64_t)__shfl_xor(fmax, d, 64));
+    }
+    if ((threadIdx.x & 63u) == 0 && fmax) {
+      atomicMin(&s_scan[0], fmin);
+      atomicMax(&s_scan[1], fmax);
+    }
+    lds_barrier();
+  }
   // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
   // (all 64 lanes), published with the range by a single barrier.
   if (threadIdx.x < 64) {
@@ -357,7 +398,13 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
         // from the full range the LF step lands on symbol c's C-block, whose
         // allowed set is c's precomputed follow-set bitmap
         if (l == 0 && h >= v.n) follow = t + shift;
-        lf_step_decode(v, t + shift, l, h, tbm, one);
+        if (wg_scan) {
+          const uint64_t a = s_scan[0], b = s_scan[1];
+          l = b ? (a & kELfMask) : 0;
+          h = b ? (b & kELfMask) + 1 : 0;
+        } else {
+          lf_step_decode(v, t + shift, l, h, tbm, one);
+        }
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }

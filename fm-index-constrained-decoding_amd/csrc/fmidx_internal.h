@@ -50,6 +50,7 @@ constexpr int kW2SbLog2 = 16;                  // 64 blocks per superblock (u16 
 constexpr uint32_t kESymShift = 36;
 constexpr uint64_t kELfMask = (1ull << kESymShift) - 1;
 constexpr uint32_t kENarrow = 512;             // widest range whose LF step scans E (8 entries per lane)
+constexpr uint32_t kEWide = 4096;              // widest range the decode kernel's workgroup scans E for
 
 // One level of the 2-level wavelet matrix.  Block b (digits [1024 b, 1024 b +
 // 1024)) = [R x uint16 count of each digit before the block, relative to its

@@ -19,10 +19,10 @@ def dev():
     return torch.device("cuda:0")
 
 
-def ours_index(docs, bm_log2=None, cache_min=None):
+def ours_index(docs, bm_log2=None, cache_min=None, trans=None):
     from fmidx.index import FMIndex
 
-    env = {"FMIDX_BM_LOG2": bm_log2, "FMIDX_CACHE_MIN": cache_min}
+    env = {"FMIDX_BM_LOG2": bm_log2, "FMIDX_CACHE_MIN": cache_min, "FMIDX_TRANS": trans}
     old = {k: os.environ.get(k) for k in env}
     for k, val in env.items():
         if val is not None:
@@ -247,6 +247,47 @@ def test_decode_step_fused_and_reset(dev, cache_min):
         assert list(zip(lo.cpu().tolist(), hi.cpu().tolist())) == state
         ref = allowed_mask(ora, [s[0] for s in state], [s[1] for s in state], V, 10)
         assert np.array_equal(mask.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("cache_min,trans", [(None, None), (None, 0), (256, None), (64, 1), (600, None)])
+def test_decode_step_wide_ranges(dev, cache_min, trans):
+    """Decode steps through every LF path of the fused kernel: the workgroup
+    E scan (uncached ranges of 513..4096 rows), the transition table (cached
+    parents -> any child, incl. one-row children and cached children), the
+    table restricted to cached children (trans=1), the two-level descent
+    (trans=0), the wave E scan (<= 512 rows) and early zero-filled rows."""
+    import torch
+
+    docs = markov_docs(31, 400, 8, 200, sticky=0.5)     # ~40K tokens over 8 symbols
+    ours = ours_index(docs, bm_log2=6, cache_min=cache_min, trans=trans)
+    st = ours.stats()
+    if trans != 0 and st["cache_nodes"] > 1:
+        assert st["trans_entries"] > 0
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    F = [t for d in reversed(docs) for t in d]
+    rng = np.random.default_rng(5)
+    B, V, S = 96, 12, 9
+    starts = rng.integers(0, len(F) - S - 1, size=B)
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.full((B,), n, dtype=torch.int64, device=dev)
+    state = [(0, n)] * B
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    seen_wg = 0
+    for step in range(S):
+        tk = np.array([F[starts[b] + step] if rng.random() < 0.9 else int(rng.integers(0, 10)) for b in range(B)])
+        seen_wg += sum(1 for a, b in state if 512 < b - a <= 4096)
+        ours.decode_step(torch.tensor(tk, device=dev), lo, hi, mask, V, 10, reset_below=0)
+        new = []
+        for b in range(B):
+            l, h = state[b]
+            new.append((0, 0) if l >= h else ora.backward_search_step(int(tk[b]) + 10, l, h - 1))
+        state = new
+        assert list(zip(lo.cpu().tolist(), hi.cpu().tolist())) == state, step
+        ref = allowed_mask(ora, [s_[0] for s_ in state], [s_[1] for s_ in state], V, 10)
+        assert np.array_equal(mask.cpu().numpy(), ref), step
+    assert seen_wg > 0
 
 
 def test_device_build_matches_host_build(dev):
