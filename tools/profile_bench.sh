@@ -1,6 +1,8 @@
 #!/bin/bash
-# rocprofv3 kernel-trace + stats of one bench run (GPU box).  Keeps only the
-# stats CSVs (the full per-dispatch trace can exceed gpurun's 64 MiB merge cap).
+# rocprofv3 kernel-trace + stats of one bench run (GPU box).  Keeps the stats
+# CSV and a summary of the fused decode kernel's dispatches (all, and the last
+# --steps ones = the timed graph replay); the full per-dispatch trace can
+# exceed gpurun's 64 MiB merge cap, so it is dropped.
 # usage: tools/profile_bench.sh <outdir> [bench args...]
 set -euo pipefail
 OUT=$1; shift
@@ -8,4 +10,24 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o run -- python3 bench.py --no-cpu "$@" > "$OUT/bench.json" 2> "$OUT/bench.log"
 find "$OUT/raw" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+TRACE=$(find "$OUT/raw" -name "*kernel_trace.csv" | head -1)
+python3 - "$TRACE" "$OUT/decode_dispatches.json" "$@" <<'PY'
+import csv, json, sys
+trace, out, args = sys.argv[1], sys.argv[2], sys.argv[3:]
+steps = int(args[args.index("--steps") + 1]) if "--steps" in args else 20
+d = []
+with open(trace) as f:
+    for r in csv.DictReader(f):
+        if "k_decode<false, true>" in r.get("Kernel_Name", ""):
+            d.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+d.sort()
+dur = [x[1] / 1e3 for x in d]
+t = dur[-steps:]
+res = {"kernel": "k_decode<false, true>", "dispatches": len(dur), "avg_us_all": sum(dur) / len(dur),
+       "timed_dispatches": len(t), "avg_us_timed": sum(t) / len(t), "min_us_timed": min(t), "max_us_timed": max(t),
+       "note": "timed = the last --steps dispatches (the bench's timed graph replay); all includes warmup, "
+               "the three replays used for the step estimate and the standalone mask-only graphs' k_decode<false,false> excluded"}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
+PY
 rm -rf "$OUT/raw"
