@@ -8,9 +8,10 @@
 // index.py:161-174, sentinel dropped) that the processors scatter into their
 // score masks (document_constrained_generation_causal_qwen.py:185-204).
 //
-// Geometry (gfx950): one workgroup of kDecThreads = 1024 threads (16 waves)
-// per (row, vocab slice); 1 slice per row at B = 256 (measured best at C3:
-// 11.7 us/step vs 12.1 for 256 x 4 slices and 13.1 for 512 x 2).
+// Geometry (gfx950): one workgroup of kDecThreads threads per (row, vocab
+// slice): 1024 (16 waves) and 1 slice per row at B = 256 (measured best at
+// C3: 11.7 us/step vs 12.1 for 256 x 4 slices and 13.1 for 512 x 2); 512 or
+// 256 threads for larger batches (decode_threads).
 //   wave 0        LF step (2-level wavelet matrix: 2 dependent round trips),
 //                 then the read plan of the new range
 //   waves 1..15   rows whose incoming range is already narrow stay narrow
@@ -29,13 +30,9 @@ namespace fmidx {
 
 namespace {
 
-#ifndef FMIDX_DEC_THREADS
-#define FMIDX_DEC_THREADS 1024
-#endif
 #ifndef FMIDX_STORE_AUX
 #define FMIDX_STORE_AUX 16
 #endif
-constexpr int kDecThreads = FMIDX_DEC_THREADS;
 // cache policy of the mask stores (buffer-store aux bits): 16 = sc1, i.e.
 // write-through -- the 33 MB of mask a step writes leaves no dirty L2 lines
 // for the kernel-end writeback to flush (MI355X_MICROARCH.md "boundary":
@@ -264,7 +261,7 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // Mask chunks: CH = 16 tokens (uint8 mask, one uint4 store) or 32 tokens
 // (packed, one uint32 store); chunk k of a slice is owned by one thread in
 // both the early zero-fill and the final emit.
-template <bool PACKED, bool DO_LF>
+template <bool PACKED, bool DO_LF, int kDecThreads>
 // Argument order: the per-row state pointers and the slice geometry come first
 // so that, with kernel-argument preloading (Makefile: -amdgpu-kernarg-preload-
 // count), they arrive in SGPRs at dispatch and the row-state loads issue
@@ -467,8 +464,31 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   }
   // One whole bitmap and nothing streamed (a cached range, the full range or a
   // follow set): emitted straight from the bitmap in memory, no LDS pass.
-  const bool direct = lo < hi && plan.nb == 1 && plan.a0 >= plan.b0 && plan.a1 >= plan.b1;
-  if (lo < hi && !direct) {
+  const bool single = lo < hi && plan.nb == 1 && plan.a0 >= plan.b0 && plan.a1 >= plan.b1;
+  const bool direct = single && kDecThreads >= 1024;
+  if (single && !direct) {
+    // smaller workgroups: the one bitmap is staged into the LDS window with
+    // every load of a batch in flight together (one round trip for a 128k
+    // vocabulary at 256 threads), then emitted like any gathered window
+    const uint32_t* bm = plan.ptr[0];
+    const uint32_t nw4 = nwin / 4;
+    for (uint32_t j0 = threadIdx.x; j0 < nw4; j0 += 4 * kDecThreads) {
+      uint4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w4b = j0 + (uint32_t)u * kDecThreads;
+        const int64_t gwb = w_lo + 4 * (int64_t)w4b;
+        x[u] = (w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words)
+                   ? *reinterpret_cast<const uint4*>(bm + gwb) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w4b = j0 + (uint32_t)u * kDecThreads;
+        if (w4b < nw4) *reinterpret_cast<uint4*>(&win[4 * w4b]) = x[u];
+      }
+    }
+    lds_barrier();
+  } else if (lo < hi && !direct) {
     const int64_t base_bit = w_lo * 32;
     const int64_t lim = (int64_t)nwin * 32;
     const uint32_t nb = plan.nb;
@@ -646,18 +666,31 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 
 }  // namespace
 
+// Workgroup size by batch: one 1024-thread workgroup per row while the rows
+// fit one per CU (the emit of a row's 128 KB wants all 16 waves' store
+// issue); beyond that smaller workgroups, so that several rows' dependent
+// chains overlap on each CU (measured at B = 2048: 49.6 us/step with 256
+// threads, 60.1 with 512, 79.1 with 1024, 71.4 with 128; B = 512: 15.2 /
+// 17.6 / 18.1 / 22.4; B = 256: 1024 and 256 threads x 4 slices tie at 10.4).
+// FMIDX_DEC_THREADS overrides.
+static uint32_t decode_threads(uint64_t m) {
+  const uint32_t e = env_u32("FMIDX_DEC_THREADS", 0);
+  if (e == 256 || e == 512 || e == 1024) return e;
+  return m <= 256 ? 1024 : 256;
+}
+
 // Slice geometry.  Residency budget: kernels of this shape keep about 16 waves
 // per CU resident (measured, profiles/r01_tuning); a launch of more waves than
 // budget dispatches its tail only as earlier workgroups retire.  So the slices
-// per row are chosen to keep rows * S * 16 waves within the budget (default
-// one slice per row at B >= 256), slices a multiple of 64 tokens.
-static void mask_geometry(uint64_t m, uint64_t vocab, uint32_t& S, uint32_t& SW) {
+// per row are chosen to keep rows * S * (threads / 64) waves within the
+// budget (default one slice per row at B >= 256), slices a multiple of 64 tokens.
+static void mask_geometry(uint64_t m, uint64_t vocab, uint32_t threads, uint32_t& S, uint32_t& SW) {
   uint32_t s = env_u32("FMIDX_MASK_SLICES", 0);
   const uint64_t s_min = (vocab + kMaxSliceTokens - 1) / kMaxSliceTokens;
   if (s == 0) {
     const uint64_t rows = (m + 7) / 8 * 8;
     const uint64_t budget = env_u32("FMIDX_WAVE_BUDGET", 4096);
-    const uint64_t want = std::max<uint64_t>(1, budget / (rows * (kDecThreads / 64)));
+    const uint64_t want = std::max<uint64_t>(1, budget / (rows * (threads / 64)));
     const uint64_t max_s = std::max<uint64_t>(1, (vocab + 8191) / 8192);
     s = (uint32_t)std::min(want, max_s);
   }
@@ -683,10 +716,11 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
               (unsigned long long)vocab);
     return -1;
   }
+  const uint32_t T = decode_threads(m);
   uint32_t S, SW;
-  mask_geometry(m, vocab, S, SW);
+  mask_geometry(m, vocab, T, S, SW);
   const uint64_t grid = (m + 7) / 8 * 8 * S;
-  if (grid > 0x7fffffffull / kDecThreads) {
+  if (grid > 0x7fffffffull / T) {
     set_error("too many rows for one launch");
     return -1;
   }
@@ -695,16 +729,26 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     const char* e = std::getenv("FMIDX_EARLY_ZERO_WIDTH");
     return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
   }();
-#define FM_LAUNCH(P, L)                                                                                       \
-  k_decode<P, L><<<g, kDecThreads, 0, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                           mask, ld, ew, v)
+#define FM_LAUNCH(P, L, TT)                                                                                  \
+  k_decode<P, L, TT><<<g, TT, 0, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
+                                      mask, ld, ew, v)
+#define FM_LAUNCH_T(P, L)          \
+  do {                             \
+    if (T == 1024)                 \
+      FM_LAUNCH(P, L, 1024);       \
+    else if (T == 512)             \
+      FM_LAUNCH(P, L, 512);        \
+    else                           \
+      FM_LAUNCH(P, L, 256);        \
+  } while (0)
   if (do_lf) {
-    if (packed) FM_LAUNCH(true, true);
-    else FM_LAUNCH(false, true);
+    if (packed) FM_LAUNCH_T(true, true);
+    else FM_LAUNCH_T(false, true);
   } else {
-    if (packed) FM_LAUNCH(true, false);
-    else FM_LAUNCH(false, false);
+    if (packed) FM_LAUNCH_T(true, false);
+    else FM_LAUNCH_T(false, false);
   }
+#undef FM_LAUNCH_T
 #undef FM_LAUNCH
   FM_HIP(hipGetLastError());
   return 0;

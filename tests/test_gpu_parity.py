@@ -249,8 +249,10 @@ def test_decode_step_fused_and_reset(dev, cache_min):
         assert np.array_equal(mask.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("cache_min,trans", [(None, None), (None, 0), (256, None), (64, 1), (600, None)])
-def test_decode_step_wide_ranges(dev, cache_min, trans):
+@pytest.mark.parametrize("cache_min,trans,threads", [(None, None, None), (None, 0, None), (256, None, None),
+                                                     (64, 1, None), (600, None, None), (None, None, 256),
+                                                     (256, None, 512), (64, None, 256)])
+def test_decode_step_wide_ranges(dev, cache_min, trans, threads, monkeypatch):
     """Decode steps through every LF path of the fused kernel: the workgroup
     E scan (uncached ranges of 513..4096 rows), the transition table (cached
     parents -> any child, incl. one-row children and cached children), the
@@ -260,6 +262,8 @@ def test_decode_step_wide_ranges(dev, cache_min, trans):
 
     docs = markov_docs(31, 400, 8, 200, sticky=0.5)     # ~40K tokens over 8 symbols
     ours = ours_index(docs, bm_log2=6, cache_min=cache_min, trans=trans)
+    if threads is not None:     # workgroup size of the decode kernel (default by batch)
+        monkeypatch.setenv("FMIDX_DEC_THREADS", str(threads))
     st = ours.stats()
     if trans != 0 and st["cache_nodes"] > 1:
         assert st["trans_entries"] > 0
