@@ -10,6 +10,10 @@
 // Every pass is a coalesced stream over n symbols.
 #include "fmidx_internal.h"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -21,6 +25,20 @@
 #include <vector>
 
 namespace fmidx {
+
+double build_clock() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void build_phase(const char* name, double t0, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("FMIDX_BUILD_TIMES");
+    return e && *e && *e != '0';
+  }();
+  if (!on) return;
+  (void)hipStreamSynchronize(s);
+  std::fprintf(stderr, "[fmidx] build: %s %.2f s\n", name, build_clock() - t0);
+}
 
 namespace {
 
@@ -581,9 +599,15 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     h->follow_bytes = nsym * words * 4;
     v.bm_follow = fb;
   }
+  double t = build_clock();
   if (device_build_w2(h, d_bwt, n, s)) return -1;
+  build_phase("2-level wavelet matrix", t, s);
+  t = build_clock();
   if (device_build_lfe(h, d_bwt, n, s)) return -1;
+  build_phase("E array", t, s);
+  t = build_clock();
   if (device_build_cache(h, s)) return -1;
+  build_phase("range cache + transitions", t, s);
   h->built = true;
   return 0;
 }

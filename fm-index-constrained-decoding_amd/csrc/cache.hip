@@ -136,15 +136,29 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   if (mode == 0 || nodes.size() < 2 || !v.cache_mask) return 0;
   const uint64_t budget = env_u64("FMIDX_TRANS_MB", 72ull << 10) << 20;
   const uint64_t sigma = (uint64_t)h->max_sym + 1;
-  const uint64_t kChunkCap = 1ull << 25;
+  const uint64_t kChunkCap = 1ull << 26;   // child slots per k_distinct launch
+  const uint64_t kChunkRows = 1ull << 20;
+  // chunk buffers, allocated once and reused by every chunk of both passes
+  DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_child, d_k;
+  DBuf<uint8_t> d_ws;
+  if (d_lo.alloc(kChunkRows) || d_hi.alloc(kChunkRows) || d_off.alloc(kChunkRows + 1) || d_syms.alloc(kChunkCap) ||
+      d_cnt.alloc(kChunkCap) || d_child.alloc(kChunkCap) || d_k.alloc(kChunkRows) ||
+      d_ws.alloc(distinct_ws_bytes(kChunkCap)))
+    return -1;
+  std::vector<uint64_t> lo, hi, off, k;
+  lo.reserve(kChunkRows);
+  hi.reserve(kChunkRows);
+  off.reserve(kChunkRows + 1);
   // parents: every cached range but the root (whose LF step is the C lookup)
   auto pass = [&](uint64_t min_count, uint64_t* tab, uint64_t cap, uint64_t& total,
                   unsigned long long* d_stats) -> int {
     total = 0;
     for (size_t i0 = 1; i0 < nodes.size();) {
-      std::vector<uint64_t> lo, hi, off{0};
+      lo.clear();
+      hi.clear();
+      off.assign(1, 0);
       size_t i1 = i0;
-      while (i1 < nodes.size()) {
+      while (i1 < nodes.size() && i1 - i0 < kChunkRows) {
         const uint64_t w = nodes[i1].second - nodes[i1].first;
         const uint64_t c = std::min<uint64_t>(min_count > 1 ? w / min_count + 1 : w, sigma);
         if (i1 > i0 && off.back() + c > kChunkCap) break;
@@ -154,11 +168,6 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
         ++i1;
       }
       const uint64_t m = i1 - i0, tot = off.back();
-      DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_child, d_k;
-      DBuf<uint8_t> d_ws;
-      if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(tot) || d_cnt.alloc(tot) ||
-          d_child.alloc(tot) || d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(tot)))
-        return -1;
       FM_HIP(hipMemcpyAsync(d_lo.p, lo.data(), m * 8, hipMemcpyHostToDevice, s));
       FM_HIP(hipMemcpyAsync(d_hi.p, hi.data(), m * 8, hipMemcpyHostToDevice, s));
       FM_HIP(hipMemcpyAsync(d_off.p, off.data(), (m + 1) * 8, hipMemcpyHostToDevice, s));
@@ -169,9 +178,9 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
         k_trans_insert<<<(unsigned)m, 256, 0, s>>>(v, d_lo.p, d_hi.p, d_off.p, d_k.p, d_syms.p, d_cnt.p,
                                                    d_child.p, m, tab, cap, d_stats);
         FM_HIP(hipGetLastError());
-        FM_HIP(hipStreamSynchronize(s));   // chunk buffers are freed on scope exit
+        FM_HIP(hipStreamSynchronize(s));   // the host staging vectors are refilled next chunk
       } else {
-        std::vector<uint64_t> k(m);
+        k.resize(m);
         FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, s));
         FM_HIP(hipStreamSynchronize(s));
         for (uint64_t r = 0; r < m; ++r) total += (k[r] == ~0ull) ? 0 : k[r];
@@ -182,7 +191,9 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   };
   uint64_t min_count = mode >= 2 ? 1 : v.cache_min;
   uint64_t entries = 0;
+  double t = build_clock();
   if (pass(min_count, nullptr, 0, entries, nullptr)) return -1;
+  build_phase("transitions: count pass", t, s);
   uint64_t cap = std::max<uint64_t>(1024, entries + entries / 2 + entries / 4);   // load <= 0.57
   if (cap * 24 > budget && min_count == 1) {   // over budget: the cached children only
     min_count = v.cache_min;
@@ -203,10 +214,12 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   }
   FM_HIP(hipMemsetAsync(d_stats.p, 0, 16, s));
   uint64_t dummy = 0;
+  t = build_clock();
   if (pass(min_count, tab, cap, dummy, d_stats.p)) {
     (void)hipFree(tab);
     return -1;
   }
+  build_phase("transitions: insert pass", t, s);
   unsigned long long st[2] = {0, 0};
   FM_HIP(hipMemcpy(st, d_stats.p, 16, hipMemcpyDeviceToHost));
   h->trans_tab = tab;
@@ -232,6 +245,7 @@ int device_build_cache(Index* h, hipStream_t s) {
   const uint64_t max_nodes = std::max<uint64_t>(1, budget / (words * 4));
 
   // ---- breadth-first enumeration of the ranges with width >= Wc
+  const double t_bfs = build_clock();
   std::vector<std::pair<uint64_t, uint64_t>> nodes;
   std::unordered_map<std::pair<uint64_t, uint64_t>, uint64_t, PairHash> seen;   // range -> id
   std::vector<std::pair<uint64_t, uint64_t>> frontier{{0, n}}, next;
@@ -358,7 +372,9 @@ int device_build_cache(Index* h, hipStream_t s) {
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t_stats).count());
   }
 
+  build_phase("range cache: BFS", t_bfs, s);
   // ---- bitmaps (packed masks in symbol space, exactly the hierarchy layout)
+  const double t_bm = build_clock();
   const uint64_t N = nodes.size();
   if (h->cache_bm) (void)hipFree(h->cache_bm);
   h->cache_bm = nullptr;
@@ -383,6 +399,7 @@ int device_build_cache(Index* h, hipStream_t s) {
     }
   }
 
+  build_phase("range cache: bitmaps", t_bm, s);
   // ---- (lo, hi) -> bitmap id, linear probing, load factor <= 1/2
   uint64_t cap = 1024;
   while (cap < 2 * N) cap <<= 1;

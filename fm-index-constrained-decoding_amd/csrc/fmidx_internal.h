@@ -589,6 +589,10 @@ int launch_epilogue(int dtype, const void* scores, void* out, uint64_t B, uint64
 
 void set_error(const char* fmt, ...);
 
+// FMIDX_BUILD_TIMES=1: construction phases report their wall time on stderr.
+double build_clock();                                   // seconds, monotonic
+void build_phase(const char* name, double t0, hipStream_t s);   // syncs s and prints when enabled
+
 }  // namespace fmidx
 
 #define FM_HIP(expr)                                                                    \

@@ -124,24 +124,6 @@ struct Frontier {
   uint32_t* pre[2];
 };
 
-// per-digit counts before position i at level lev (16 values, one thread)
-__device__ __forceinline__ void digit_counts(const DevView& v, uint32_t lev, uint64_t i, uint64_t* out) {
-  const uint64_t b = i / kBlkDigits;
-  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
-  const uint4* blk = rank_block(v, lev, b);
-  const uint64_t* sbr = sb_row(v, lev, b);
-  uint4 x[kBlkU4];
-#pragma unroll
-  for (int q = 0; q < kBlkU4; ++q) x[q] = blk[q];
-#pragma unroll
-  for (uint32_t d = 0; d < 16; ++d) {
-    uint64_t c = sbr[d];
-#pragma unroll
-    for (uint32_t q = 0; q < kBlkU4; ++q) c += block_part(x[q], q, d, k);
-    out[d] = c;
-  }
-}
-
 __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[4]*/, uint32_t& total) {
   const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   uint32_t x = v;
@@ -166,7 +148,12 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[
 
 // interval_symbols with counts: level-synchronous BFS over the 16-ary
 // wavelet matrix, one workgroup per row; children are appended in digit
-// order so the final frontier is in ascending symbol order.
+// order so the final frontier is in ascending symbol order.  Each frontier
+// node is expanded by 4 lanes, lane j ranking digits 4j..4j+3 at both
+// endpoints (the 4 lanes read the same two rank blocks: one coalesced
+// request), 64 nodes per workgroup round; a thread holds 8 ranks instead of
+// all 32 (no register spills), and a block-wide scan of the per-lane child
+// counts in (node, digit) order gives every child its output slot.
 // min_count > 1 prunes every prefix node holding fewer occurrences (so only
 // symbols occurring >= min_count times are reported, in O(width / min_count)
 // space); child_lo, when given, receives LF(lo, c) = C[c] + rank_c(lo) of
@@ -206,31 +193,56 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
   __syncthreads();
   uint64_t fc = 1;
   bool overflow = false;
+  const uint32_t d0 = 4 * (threadIdx.x & 3u);   // this lane's digits d0 .. d0 + 3
   for (uint32_t lev = 0; lev < v.NL; ++lev) {
-    const uint64_t* Z = v.Z + lev * kRadix;
+    uint64_t zd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zd[j] = v.Z[lev * kRadix + d0 + j];
     uint64_t out = 0;
-    for (uint64_t t0 = 0; t0 < fc; t0 += 256) {
-      const uint64_t i = t0 + threadIdx.x;
-      uint64_t cl[16], ch[16];
+    for (uint64_t t0 = 0; t0 < fc; t0 += 64) {
+      const uint64_t i = t0 + (threadIdx.x >> 2);
+      uint64_t cl[4] = {0, 0, 0, 0}, ch[4] = {0, 0, 0, 0};
       uint32_t p = 0, nchild = 0;
       if (i < fc) {
         p = apre[i];
-        digit_counts(v, lev, alo[i], cl);
-        digit_counts(v, lev, ahi[i], ch);
+        const uint64_t il = alo[i], ih = ahi[i];
+        const uint64_t bl = il / kBlkDigits, bh = ih / kBlkDigits;
+        const uint32_t kl = (uint32_t)(il - bl * kBlkDigits), kh = (uint32_t)(ih - bh * kBlkDigits);
+        const uint4* xl = rank_block(v, lev, bl);
+        const uint4* xh = rank_block(v, lev, bh);
+        uint4 a[kBlkU4], b[kBlkU4];
 #pragma unroll
-        for (int d = 0; d < 16; ++d) nchild += (ch[d] >= cl[d] + min_count) ? 1u : 0u;
+        for (int q = 0; q < kBlkU4; ++q) {
+          a[q] = xl[q];
+          b[q] = xh[q];
+        }
+        const uint64_t* sl = sb_row(v, lev, bl);
+        const uint64_t* sh = sb_row(v, lev, bh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cl[j] = sl[d0 + j];
+          ch[j] = sh[d0 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (uint32_t q = 0; q < kBlkU4; ++q) {
+            cl[j] += block_part(a[q], q, d0 + j, kl);
+            ch[j] += block_part(b[q], q, d0 + j, kh);
+          }
+          nchild += (ch[j] >= cl[j] + min_count) ? 1u : 0u;
+        }
       }
       uint32_t tot;
-      const uint64_t pos0 = out + block_scan_u32(nchild, wave_tot, tot);
+      uint64_t pos = out + block_scan_u32(nchild, wave_tot, tot);
       if (nchild) {
-        uint64_t pos = pos0;
 #pragma unroll
-        for (uint32_t d = 0; d < 16; ++d) {
-          if (ch[d] >= cl[d] + min_count) {
+        for (int j = 0; j < 4; ++j) {
+          if (ch[j] >= cl[j] + min_count) {
             if (pos < cap) {
-              blo[pos] = Z[d] + cl[d];
-              bhi[pos] = Z[d] + ch[d];
-              bpre[pos] = (p << 4) | d;
+              blo[pos] = zd[j] + cl[j];
+              bhi[pos] = zd[j] + ch[j];
+              bpre[pos] = (p << 4) | (d0 + j);
             }
             ++pos;
           }
