@@ -330,9 +330,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   // so a wave with stores in flight cannot wait on a load without also
   // waiting for them -- wave 0 (LF + plan) must stay store-free.
   if (early_zero && threadIdx.x >= 64) {
-#ifdef FMIDX_ZERO_DELAY
-    for (int d_ = 0; d_ < FMIDX_ZERO_DELAY; ++d_) __builtin_amdgcn_s_sleep(16);   // experiment: hold the zero-fill back
-#endif
     for (uint64_t k = threadIdx.x - 64; k < nch; k += kDecThreads - 64) {
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
@@ -558,9 +555,6 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   // to the same address, in program order: per-location coherence orders the
   // two, no wait for the zero stores' acknowledgements is needed.
   const bool zeroed = early_zero || late_zero;
-#ifdef FMIDX_ZERO_WAIT
-  if (zeroed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
   if (direct) {
     // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH).  All of a
