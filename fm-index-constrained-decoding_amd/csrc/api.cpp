@@ -47,6 +47,8 @@ void Index::release() {
   if (cache_tab) (void)hipFree(cache_tab);
   if (trans_tab) (void)hipFree(trans_tab);
   trans_tab = nullptr;
+  if (cblock) (void)hipFree(cblock);
+  cblock = nullptr;
   trans_entries = trans_dropped = trans_bytes = 0;
   cache_bm = nullptr;
   cache_tab = nullptr;

@@ -236,6 +236,7 @@ int device_build_cache(Index* h, hipStream_t s) {
   DevView& v = h->view;
   v.cache_mask = 0;
   v.cache_bm = nullptr;
+  v.cblock = nullptr;
   v.cache_tab = nullptr;
   const uint64_t n = h->n;
   const uint64_t Wc = std::max<uint64_t>(2, env_u64("FMIDX_CACHE_MIN", 4096));
@@ -249,6 +250,7 @@ int device_build_cache(Index* h, hipStream_t s) {
   std::vector<std::pair<uint64_t, uint64_t>> nodes;
   std::unordered_map<std::pair<uint64_t, uint64_t>, uint64_t, PairHash> seen;   // range -> id
   std::vector<std::pair<uint64_t, uint64_t>> frontier{{0, n}}, next;
+  std::vector<std::pair<uint64_t, uint64_t>> root_child;   // (symbol, cache id) of the cached C-blocks
   nodes.push_back({0, n});
   seen.emplace(std::make_pair(uint64_t(0), n), 0);
   const uint64_t kChunkCap = 1ull << 24;   // child slots per k_distinct launch
@@ -295,16 +297,20 @@ int device_build_cache(Index* h, hipStream_t s) {
         for (uint64_t j = 0; j < k[r]; ++j) {
           const uint64_t a = child[off[r] + j], b = a + cnt[off[r] + j];
           auto it = seen.find({a, b});
+          uint64_t id;
           if (it == seen.end()) {
             if (nodes.size() >= max_nodes) {
               full = true;
               break;
             }
-            const uint64_t id = nodes.size();
+            id = nodes.size();
             seen.emplace(std::make_pair(a, b), id);
             nodes.push_back({a, b});
             next.push_back({a, b});
+          } else {
+            id = it->second;
           }
+          if (lo[r] == 0 && hi[r] == n) root_child.push_back({sym[off[r] + j], id});
         }
       }
       i0 = i1;
@@ -425,6 +431,21 @@ int device_build_cache(Index* h, hipStream_t s) {
   v.cache_tab = h->cache_tab;
   v.cache_min = Wc;
   v.cache_mask = cap - 1;
+
+  // ---- per symbol: cache id + 1 of its C-block (the LF step from the full range)
+  v.cblock = nullptr;
+  if (h->cblock) (void)hipFree(h->cblock);
+  h->cblock = nullptr;
+  if (!root_child.empty()) {
+    std::vector<uint32_t> cb((size_t)h->max_sym + 2, 0u);
+    for (const auto& e : root_child)
+      if (e.first < cb.size()) cb[e.first] = (uint32_t)(e.second + 1);
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&h->cblock), cb.size() * 4));
+    FM_HIP(hipMemcpyAsync(h->cblock, cb.data(), cb.size() * 4, hipMemcpyHostToDevice, s));
+    FM_HIP(hipStreamSynchronize(s));
+    v.cblock = h->cblock;
+    h->cache_bytes += cb.size() * 4;
+  }
 
   return build_transitions(h, nodes, s);
 }

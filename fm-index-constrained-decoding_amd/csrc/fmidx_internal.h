@@ -93,6 +93,7 @@ struct DevView {
   // its only symbol; 3 words per slot (layout at kTransSymShift below)
   const uint64_t* trans_tab;
   uint64_t trans_cap;         // slots; 0 = none
+  const uint32_t* cblock;     // per symbol c: cache id + 1 of its C-block [C[c], C[c+1]) (0 = not cached), or null
   const uint64_t* E;          // [n] LF(i) | BWT[i] << kESymShift (narrow-range LF + streaming), or null
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
@@ -158,7 +159,7 @@ struct DevView {
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
                  "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
-                 "s"((v).trans_cap));                                                                     \
+                 "s"((v).trans_cap), "s"((v).cblock));                                                                     \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -423,7 +424,8 @@ __host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi
 // inputs), with exactly one inlined copy of each path (a kernel's code is
 // fetched cold into the instruction cache at every launch, so duplicated
 // inlined paths cost fetch latency on the dependent chain):
-//   * full range: [C[c], C[c+1]) ([sdsl] backward_search shortcut);
+//   * full range: [C[c], C[c+1]) ([sdsl] backward_search shortcut), with the
+//     C-block's cached bitmap (cblock) read in the same round trip;
 //   * <= kENarrow rows: one scan of E[lo, hi) (lf_step_fast);
 //   * otherwise the wavelet-matrix descent (NL2 round trips); a cached range
 //     also probes the transition table, issued with the first descent level
@@ -441,10 +443,12 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     return;
   }
   const uint32_t c32 = (uint32_t)sym;
-  if (lo == 0 && hi == v.n) {
+  if (lo == 0 && hi == v.n) {   // the C-block, and its cached bitmap id in the same round trip
     const uint64_t a = v.C[c32], b = v.C[c32 + 1];
+    const uint32_t cid = v.cblock ? v.cblock[c32] : 0u;
     lo = a < b ? a : 0;
     hi = a < b ? b : 0;
+    if (cid && a < b) cbm = v.cache_bm + (uint64_t)(cid - 1) * v.bm_words;
     return;
   }
   if (v.E && hi - lo <= kENarrow) {
@@ -533,6 +537,7 @@ struct Index {
   uint32_t* cache_bm = nullptr;
   uint64_t* cache_tab = nullptr;
   uint64_t* trans_tab = nullptr;
+  uint32_t* cblock = nullptr;
   uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0, trans_dropped = 0, trans_bytes = 0;
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;
