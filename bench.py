@@ -153,9 +153,11 @@ def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: 
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, warmup, seconds, dev):
+def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, V, warmup, seconds, dev):
     """The sdsl-faithful C++ restatement (oracle/cpu_ref.cpp) on the host
-    cores, replaying the same trace from step `warmup` until ~`seconds`."""
+    cores, replaying the same trace from step `warmup` until ~`seconds`; its
+    final ranges AND its final step's masks are compared with the GPU's (a
+    full-scale bit-exact check against an independent implementation)."""
     from oracle.cpu_ref import CpuRef
 
     n = bwt.numel()
@@ -189,11 +191,21 @@ def cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, warmup, seconds, dev):
         if time.time() - t0 >= seconds:
             break
     el = time.time() - t0
-    ok = bool(np.array_equal(lo, lo_hist[s - 1].cpu().numpy().astype(np.uint64)))
+    ok = bool(np.array_equal(lo, lo_hist[s - 1].cpu().numpy().astype(np.uint64)) and
+              np.array_equal(hi, hi_hist[s - 1].cpu().numpy().astype(np.uint64)))
+    # the GPU's mask of the same step (s - 1), from the same incoming state
+    gmask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    glo = torch.empty(B, dtype=torch.int64, device=dev)
+    ghi = torch.empty(B, dtype=torch.int64, device=dev)
+    fm.decode_step(tokens[s - 1], lo_hist[s - 2], hi_hist[s - 2], gmask, V, SHIFT, reset_below=0,
+                   lo_out=glo, hi_out=ghi)
+    mok = bool(np.array_equal(mask, gmask.cpu().numpy()))
     return {"value": rows / el, "unit": "masks/s", "cores": threads, "kind": "port",
             "sample": f"{steps} decode steps x {B} rows of the same trace (steps {warmup}..{s - 1}), "
                       f"same n={n} index, sdsl-faithful wt_int + rank_support_v restatement, "
-                      f"{threads} threads, {el:.1f}s; final ranges match GPU: {ok}"}
+                      f"{threads} threads, {el:.1f}s; final ranges match GPU: {ok}; "
+                      f"final step's {B}x{V} masks match GPU: {mok}",
+            "ranges_match_gpu": ok, "masks_match_gpu": mok}
 
 
 # ---------------------------------------------------------------------------
@@ -435,7 +447,7 @@ def main():
             pass
     if cpu_leg:
         try:
-            result["cpu_baseline"] = cpu_baseline(bwt, tokens, lo_hist, hi_hist, V, W, args.cpu_seconds, dev)
+            result["cpu_baseline"] = cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, V, W, args.cpu_seconds, dev)
         except Exception as e:  # the GPU line must still print
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
