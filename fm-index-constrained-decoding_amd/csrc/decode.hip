@@ -12,8 +12,11 @@
 // slice): 1024 (16 waves) and 1 slice per row at B = 256 (measured best at
 // C3: 11.7 us/step vs 12.1 for 256 x 4 slices and 13.1 for 512 x 2); 512 or
 // 256 threads for larger batches (decode_threads).
-//   wave 0        LF step (2-level wavelet matrix: 2 dependent round trips),
+//   wave 0        LF step (one round trip for every kind of range: C lookup,
+//                 E scan, transition-table probe of a cached range; the
+//                 two-level descent only for ranges none of those serves),
 //                 then the read plan of the new range
+//   all waves     the E scan of an uncached 513..4096-row range
 //   waves 1..15   rows whose incoming range is already narrow stay narrow
 //                 after the step, so their mask row is zero-filled right away,
 //                 overlapping the LF chain
@@ -277,8 +280,8 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
                                                        uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   __shared__ Plan plan;
-  __shared__ uint64_t s_lohi[3];
-  __shared__ unsigned long long s_scan[2];   // workgroup E scan: first / last occurrence   // new range + its only symbol when the transition table knew it (else ~0)
+  __shared__ uint64_t s_lohi[3];              // new range + its only symbol when the transition table knew it (else ~0)
+  __shared__ unsigned long long s_scan[2];    // workgroup E scan: first / last occurrence
   FM_STAMP_DECL;
   __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
   uint64_t row;
