@@ -249,10 +249,13 @@ def test_decode_step_fused_and_reset(dev, cache_min):
         assert np.array_equal(mask.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("cache_min,trans,threads", [(None, None, None), (None, 0, None), (256, None, None),
-                                                     (64, 1, None), (600, None, None), (None, None, 256),
-                                                     (256, None, 512), (64, None, 256)])
-def test_decode_step_wide_ranges(dev, cache_min, trans, threads, monkeypatch):
+@pytest.mark.parametrize("cache_min,trans,threads,V", [(None, None, None, 12), (None, 0, None, 12),
+                                                       (256, None, None, 12), (64, 1, None, 12),
+                                                       (600, None, None, 12), (None, None, 256, 12),
+                                                       (256, None, 512, 12), (64, None, 256, 12),
+                                                       (64, None, None, 151936), (64, None, 256, 151936),
+                                                       (None, None, None, 128256)])
+def test_decode_step_wide_ranges(dev, cache_min, trans, threads, V, monkeypatch):
     """Decode steps through every LF path of the fused kernel: the workgroup
     E scan (uncached ranges of 513..4096 rows), the transition table (cached
     parents -> any child, incl. one-row children and cached children), the
@@ -261,6 +264,9 @@ def test_decode_step_wide_ranges(dev, cache_min, trans, threads, monkeypatch):
     import torch
 
     docs = markov_docs(31, 400, 8, 200, sticky=0.5)     # ~40K tokens over 8 symbols
+    if V > 1000:   # + rare ids over the whole vocabulary: wide ranges with allowed sets spread over V
+        r2 = np.random.default_rng(7)
+        docs = [[t if r2.random() < 0.7 else int(r2.integers(8, V - 10)) for t in d] for d in docs]
     ours = ours_index(docs, bm_log2=6, cache_min=cache_min, trans=trans)
     if threads is not None:     # workgroup size of the decode kernel (default by batch)
         monkeypatch.setenv("FMIDX_DEC_THREADS", str(threads))
@@ -272,7 +278,7 @@ def test_decode_step_wide_ranges(dev, cache_min, trans, threads, monkeypatch):
     n = ora.size()
     F = [t for d in reversed(docs) for t in d]
     rng = np.random.default_rng(5)
-    B, V, S = 96, 12, 9
+    B, S = 96, 9
     starts = rng.integers(0, len(F) - S - 1, size=B)
     lo = torch.zeros(B, dtype=torch.int64, device=dev)
     hi = torch.full((B,), n, dtype=torch.int64, device=dev)
