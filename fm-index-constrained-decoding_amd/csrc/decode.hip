@@ -43,7 +43,9 @@ namespace {
 constexpr int kStoreAux = FMIDX_STORE_AUX;
 constexpr int kMaxPlan = 160;                 // >= 6 * kMaxBmLevels
 constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
-constexpr int kWinWords = kMaxSliceTokens / 32 + 16;
+// LDS window words for a slice of sw tokens: the window starts at most 127
+// symbols before the slice (128-bit aligned) and ends 64 after it
+__host__ __device__ constexpr uint32_t win_words(uint64_t sw) { return (uint32_t)(sw / 32 + 16); }
 constexpr uint64_t kEarlyZeroWidth = 64;      // rows this narrow get their zeros written up front
 constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
 
@@ -264,12 +266,18 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // Mask chunks: CH = 16 tokens (uint8 mask, one uint4 store) or 32 tokens
 // (packed, one uint32 store); chunk k of a slice is owned by one thread in
 // both the early zero-fill and the final emit.
+#ifndef FMIDX_SMALL_WG_WAVES
+// waves per SIMD asked of the < 1024-thread variants: 6 fits 80 VGPRs only
+// with ~50 B of scratch spills (B = 2048: 46.4 us/step against 48.0), so
+// the compiler's own allocation (92 VGPRs, 5 waves) is kept
+#define FMIDX_SMALL_WG_WAVES 1
+#endif
 template <bool PACKED, bool DO_LF, int kDecThreads>
 // Argument order: the per-row state pointers and the slice geometry come first
 // so that, with kernel-argument preloading (Makefile: -amdgpu-kernarg-preload-
 // count), they arrive in SGPRs at dispatch and the row-state loads issue
 // before any kernel-argument memory load; the large DevView comes last.
-__global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restrict__ tok,
+__global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_SMALL_WG_WAVES) k_decode(const int64_t* __restrict__ tok,
                                                        const uint64_t* __restrict__ lo_in,
                                                        const uint64_t* __restrict__ hi_in, uint64_t m,
                                                        uint32_t S, uint32_t SW, uint64_t vocab,
@@ -286,7 +294,10 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   __shared__ uint64_t s_lohi[3];              // new range + its only symbol when the transition table knew it (else ~0)
   __shared__ unsigned long long s_scan[2];    // workgroup E scan: first / last occurrence
   FM_STAMP_DECL;
-  __shared__ __attribute__((aligned(16))) uint32_t win[kWinWords];
+  // sized at launch to the slice (16 KB at a 128k vocabulary instead of the
+  // 32 KB maximum): LDS is what bounds the workgroups resident per CU at
+  // 256 threads
+  extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   uint64_t row;
   uint32_t slice;
   map_block(blockIdx.x, S, row, slice);
@@ -323,8 +334,11 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   // workgroup (<= kEWide / kDecThreads entries per thread, one round trip)
   // instead of the two-level descent; the other waves are idle until the plan
   // anyway (such rows are not zero-filled early).
+  // (at most 4 entries per thread: smaller workgroups serve large batches,
+  // where chains overlap anyway, and keep their registers for occupancy)
+  constexpr uint32_t kScanMax = kEWide < 4u * kDecThreads ? kEWide : 4u * kDecThreads;
   const bool wg_scan = DO_LF && !reset && v.E && in_lo < in_hi && in_hi - in_lo > kENarrow &&
-                       in_hi - in_lo <= kEWide && !(in_lo == 0 && in_hi == v.n) &&
+                       in_hi - in_lo <= kScanMax && !(in_lo == 0 && in_hi == v.n) &&
                        (in_hi - in_lo < v.cache_min || !v.trans_cap);
   FM_PRELOAD_VIEW(v);   // after the state loads are in flight (see above)
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
@@ -349,7 +363,7 @@ __global__ void __launch_bounds__(kDecThreads) k_decode(const int64_t* __restric
   }
   if (wg_scan) {
     const uint64_t c = (uint64_t)(st_tok + shift);
-    constexpr int kU = (kEWide + kDecThreads - 1) / kDecThreads;
+    constexpr int kU = (kScanMax + kDecThreads - 1) / kDecThreads;
     uint64_t e[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -729,9 +743,10 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     const char* e = std::getenv("FMIDX_EARLY_ZERO_WIDTH");
     return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
   }();
-#define FM_LAUNCH(P, L, TT)                                                                                  \
-  k_decode<P, L, TT><<<g, TT, 0, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                      mask, ld, ew, v)
+  const size_t lds = (size_t)win_words(SW) * 4;
+#define FM_LAUNCH(P, L, TT)                                                                                    \
+  k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
+                                        mask, ld, ew, v)
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
