@@ -42,6 +42,7 @@ from fmidx.synth import markov_corpus_gpu  # noqa: E402
 
 SHIFT = 10
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 measured stream)
+HBM_STREAM_GBS = 6290.0   # measured stream rate (MI355X_MICROARCH.md)
 METRIC = "allowed-token masks/sec @ B=256, 128k vocab"
 
 
@@ -429,6 +430,9 @@ def main():
             "kernel": "k_decode (fused LF step + allowed mask)",
             "alg_bytes_per_launch": decode_bytes,
             "avg_launch_us": decode_us,
+            # also against the measured stream rate of MI355X_MICROARCH.md
+            "peak_stream_measured": HBM_STREAM_GBS,
+            "frac_stream": achieved / HBM_STREAM_GBS,
         },
         "standalone_kernels": {
             "k_lf": {"avg_launch_us": lf_us, "rank_GBps": rank_gbs, "alg_bytes_per_launch": float(lf_bytes.mean())},
