@@ -803,7 +803,7 @@ int fm_device_bwt(const fm_index* h, const uint32_t** out) {
 
 #ifdef FMIDX_STAMPS
 // Diagnostic build only (not part of include/fmidx.h): per-workgroup phase
-// stamps of the decode kernel go to d_buf (8 uint64 per workgroup), or off.
+// stamps of the decode kernel go to d_buf (16 uint64 per workgroup: 8 stamps + the row served), or off.
 int fm_debug_set_stamps(fm_index* h, uint64_t* d_buf) {
   FM_CHECK_BUILT(h);
   h->idx.view.stamps = d_buf;

@@ -303,7 +303,11 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   map_block(blockIdx.x, S, row, slice);
   // The row state first, as VECTOR loads (vmcnt) through the preloaded
   // pointers: FM_PRELOAD_VIEW's scalar loads then wait on lgkmcnt alone and do
-  // not serialise behind (or in front of) the state's round trip.
+  // not serialise behind (or in front of) the state's round trip.  (Serving
+  // the rows in a "long dependent chain first" order -- every workgroup
+  // reading all rows' state and taking the row at its own position -- was
+  // measured: 10.7 us/step either way round against 10.3; the bulk of the
+  // bytes, not the dispatch position of the slow rows, sets the step.)
   const uint32_t srow = (uint32_t)(row < m ? row : 0);
   const __amdgpu_buffer_rsrc_t r_lo = make_rsrc(lo_in, (uint32_t)(m * 8));
   const __amdgpu_buffer_rsrc_t r_hi = make_rsrc(hi_in, (uint32_t)(m * 8));
@@ -658,7 +662,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     hi_out[row] = hi;
   }
   FM_STAMP(v, 7);
-  FM_STAMP_FLUSH(v);
+  FM_STAMP_FLUSH(v, row);
 }
 
 // cache probe per row (one wave each): 1 if [lo, hi) has a cached bitmap

@@ -128,10 +128,12 @@ struct DevView {
   do {                                                                   \
     if (threadIdx.x == (tid)) s_stamp_[(slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-#define FM_STAMP_FLUSH(v)                                                \
+#define FM_STAMP_FLUSH(v, row)                                           \
   do {                                                                   \
-    if (threadIdx.x == 0 && (v).stamps)                                  \
-      for (int s_ = 0; s_ < 8; ++s_) (v).stamps[(uint64_t)blockIdx.x * 8 + s_] = s_stamp_[s_]; \
+    if (threadIdx.x == 0 && (v).stamps) {                                \
+      for (int s_ = 0; s_ < 8; ++s_) (v).stamps[(uint64_t)blockIdx.x * 16 + s_] = s_stamp_[s_]; \
+      (v).stamps[(uint64_t)blockIdx.x * 16 + 8] = (row);                 \
+    }                                                                    \
   } while (0)
 #else
 #define FM_STAMP_DECL
@@ -141,8 +143,8 @@ struct DevView {
 #define FM_STAMP(v, slot) \
   do {                    \
   } while (0)
-#define FM_STAMP_FLUSH(v) \
-  do {                    \
+#define FM_STAMP_FLUSH(v, row) \
+  do {                         \
   } while (0)
 #endif
 

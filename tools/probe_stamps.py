@@ -32,7 +32,7 @@ if S == 0:                     # mirrors mask_geometry() in decode.hip
 SW = min(262144, (((V + S - 1) // S) + 63) & ~63)
 S = (V + SW - 1) // SW
 grid = (B + 7) // 8 * 8 * S
-stamps = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
+stamps = torch.zeros(grid * 16, dtype=torch.int64, device=dev)
 lo_o = torch.empty(B, dtype=torch.int64, device=dev)
 hi_o = torch.empty(B, dtype=torch.int64, device=dev)
 names = ["lohi", "lf", "plan+bar", "stream", "(w15arr-s4)", "bar2", "emit"]
@@ -46,15 +46,15 @@ for s in range(W, W + 12):
     fm.decode_step(tokens[s], lo_i, hi_i, mask, V, SHIFT, reset_below=0, lo_out=lo_o, hi_out=hi_o)
     torch.cuda.synchronize()
     dl.fm_debug_set_stamps(fm._h, None)
-    st = stamps.view(grid, 8).cpu().numpy().astype(np.int64)
+    st16 = stamps.view(grid, 16).cpu().numpy().astype(np.int64)
+    st = st16[:, :8]
     ok = st[:, 0] > 0
     st = st[ok]
     t0 = st[:, 0].min()
     span = (st[:, 7].max() - t0) * 10 / 1000
     start_spread = (st[:, 0].max() - t0) * 10 / 1000
     ph = np.diff(st, axis=1) * 10 / 1000     # us
-    b_ids = np.nonzero(ok)[0]
-    rows = (b_ids // (8 * S)) * 8 + (b_ids % (8 * S)) % 8
+    rows = st16[ok, 8]            # the row each workgroup served (row order may permute them)
     w_new = (hi_hist[s] - lo_hist[s]).cpu().numpy()[rows]
     w_old = (hi_hist[s - 1] - lo_hist[s - 1]).cpu().numpy()[rows]
     tot = (st[:, 7] - st[:, 0]) * 10 / 1000
