@@ -411,7 +411,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
-                        f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else 'C2 simplewiki'} scale), B={B} rows, V={V}, incremental ranges",
+                        f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else ('C5 PAQ' if n > 1e9 else 'C2 simplewiki')} "
+                        f"scale), B={B} rows, V={V}, incremental ranges",
             "corpus_tokens": n,
             "global_batch": world * B,
             "batch_per_gpu": B,

@@ -1,8 +1,9 @@
 // query.hip -- batched hot-path kernels for gfx950.
 //
 //  k_lf          one backward-search (LF) step per row: the loop body of
-//                index.py:109-112 / fm_index.cpp:67-97, L dependent levels of
-//                two 64-B rank-block reads each.
+//                index.py:109-112 / fm_index.cpp:67-97, through the shared
+//                lf_step_decode: C lookup, E scan (<= 512 rows), transition
+//                probe, or the 2-level wavelet-matrix descent.
 //  k_search      get_range over CSR patterns with the reference's early exit.
 //  (the allowed-token mask / fused decode step lives in decode.hip)
 //  k_distinct    interval_symbols with counts ([sdsl] wt_int::interval_symbols)
