@@ -67,9 +67,17 @@ class ShardedDecoder:
     """Incremental constrained decoding over a doc-range shard.
 
     ``index`` is this rank's shard index with the batched API of
-    :class:`fmidx.fm_index.FMIndex` (``get_range_batch``, ``lf_step_batch``,
-    ``allowed_mask``); ``group`` a torch.distributed process group (None =
-    single process, no collective).  State (lo, hi) per row is shard-local.
+    :class:`fmidx.fm_index.FMIndex` (``get_range_batch``, ``decode_step`` or
+    ``lf_step_batch`` + ``allowed_mask``); ``group`` a torch.distributed
+    process group (None = single process, no collective).  State (lo, hi) per
+    row is shard-local.
+
+    With the fused ``decode_step`` a step is ONE launch (LF step + mask)
+    writing into a persistent mask buffer -- bit-packed int32 [B, ceil(V/32)]
+    when ``reduce="gather_bits"``, so the all_gather ships the kernel's own
+    output -- and the (lo, hi) state ping-pongs between two buffers.  The mask
+    ``step`` returns is that buffer (or, for gather_bits, a fresh tensor): it
+    is valid until the next step.
     """
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8"):
@@ -80,8 +88,10 @@ class ShardedDecoder:
         if reduce not in ("max_u8", "gather_bits"):
             raise ValueError(reduce)
         self.reduce = reduce
+        self.fused = hasattr(index, "decode_step")
         self.lo = None
         self.hi = None
+        self._buf = None
 
     def start(self, patterns: Sequence[Sequence[int]], device):
         import torch
@@ -89,35 +99,59 @@ class ShardedDecoder:
         lo, hi = self.index.get_range_batch(patterns, self.shift)
         self.lo = torch.tensor(lo.astype(np.int64), device=device)
         self.hi = torch.tensor(hi.astype(np.int64), device=device)
+        self._buf = None
         return self.mask()
 
     def step(self, tokens):
         """Append one token per row (token < 0: restart with an empty pattern)."""
-        self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
-        return self.mask()
+        if not self.fused:
+            self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
+            return self.mask()
+        import torch
+
+        packed = self.group is not None and self.reduce == "gather_bits"
+        if self._buf is None:
+            B = self.lo.numel()
+            if packed:
+                self._buf = torch.empty((B, (self.vocab + 31) // 32), dtype=torch.int32, device=self.lo.device)
+            else:
+                self._buf = torch.empty((B, self.vocab), dtype=torch.uint8, device=self.lo.device)
+            self._lo2 = torch.empty_like(self.lo)
+            self._hi2 = torch.empty_like(self.hi)
+        self.index.decode_step(tokens, self.lo, self.hi, self._buf, self.vocab, self.shift, reset_below=0,
+                               packed=packed, lo_out=self._lo2, hi_out=self._hi2)
+        self.lo, self._lo2 = self._lo2, self.lo
+        self.hi, self._hi2 = self._hi2, self.hi
+        return self._combine(self._buf, packed)
 
     def local_mask(self):
         return self.index.allowed_mask(self.lo, self.hi, self.vocab, self.shift)
 
     def mask(self):
-        import torch
+        return self._combine(self.local_mask(), False)
 
-        m = self.local_mask()
+    def _combine(self, m, packed: bool):
+        """OR of the ranks' masks: in place for max_u8; all_gather of the
+        bit-packed rows (int32 words, or uint8 [B, V] packed here) otherwise."""
         if self.group is None:
             return m
+        import torch
         import torch.distributed as dist
 
         if self.reduce == "max_u8":
             dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
             return m
-        # bit-pack (8 tokens per byte), all-gather, OR locally, unpack
-        packed = pack_bits(m)
+        # bit-pack (8 tokens per byte) unless the kernel already did, all-gather, OR locally, unpack.
+        # int32 words in little-endian bit order are, byte for byte, pack_bits' layout.
+        pk = m if packed else pack_bits(m)
         world = dist.get_world_size(self.group)
-        parts = [torch.empty_like(packed) for _ in range(world)]
-        dist.all_gather(parts, packed, group=self.group)
-        acc = parts[0]
+        parts = [torch.empty_like(pk) for _ in range(world)]
+        dist.all_gather(parts, pk, group=self.group)
+        acc = parts[0].clone()
         for p in parts[1:]:
-            acc = acc | p
+            acc |= p
+        if packed:
+            acc = acc.view(torch.uint8)
         return unpack_bits(acc, self.vocab)
 
 

@@ -47,6 +47,27 @@ class OracleShard:
         return torch.from_numpy(allowed_mask(self.ix, lo.tolist(), hi.tolist(), vocab, shift))
 
 
+class OracleShardFused(OracleShard):
+    """... plus the fused decode_step (uint8 or int32 bit-packed mask), so the
+    ShardedDecoder's one-launch path and its packed all_gather run on CPU."""
+
+    def decode_step(self, tokens, lo, hi, mask, vocab, shift, reset_below=-(1 << 63), packed=False,
+                    lo_out=None, hi_out=None):
+        if lo_out is None:
+            lo_out, hi_out = lo, hi
+        else:
+            lo_out.copy_(lo)
+            hi_out.copy_(hi)
+        self.lf_step_batch(tokens, lo_out, hi_out, shift, reset_below)
+        m = self.allowed_mask(lo_out, hi_out, vocab, shift).numpy()
+        if packed:
+            a = np.pad(m, ((0, 0), (0, mask.shape[1] * 32 - vocab)))
+            mask.copy_(torch.from_numpy(np.packbits(a, axis=1, bitorder="little").view(np.int32).copy()))
+        else:
+            mask.copy_(torch.from_numpy(m))
+        return mask
+
+
 def make_case(seed=5):
     rng = np.random.default_rng(seed)
     docs = []
@@ -95,7 +116,7 @@ def expected_masks(docs, patterns, steps):
     return out
 
 
-def _worker(rank, world, port, halo, reduce, outdir):
+def _worker(rank, world, port, halo, reduce, outdir, fused=False):
     import torch.distributed as dist
 
     from fmidx.sharding import ShardedDecoder, shard_corpus
@@ -105,7 +126,9 @@ def _worker(rank, world, port, halo, reduce, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     docs, patterns, steps = make_case()
     shard_docs_, _ = shard_corpus(docs, world, rank, halo)
-    dec = ShardedDecoder(OracleShard(shard_docs_), V, SHIFT, group=dist.group.WORLD, reduce=reduce)
+    shard = (OracleShardFused if fused else OracleShard)(shard_docs_)
+    dec = ShardedDecoder(shard, V, SHIFT, group=dist.group.WORLD, reduce=reduce)
+    assert dec.fused == fused
     masks = [dec.start(patterns, "cpu").numpy().copy()]
     for tk in steps:
         masks.append(dec.step(torch.tensor(tk, dtype=torch.int64)).numpy().copy())
@@ -122,17 +145,19 @@ def _free_port():
     return p
 
 
-def _run(world, halo, reduce):
+def _run(world, halo, reduce, fused=False):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d, fused), nprocs=world, join=True)
         return [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("reduce", ["max_u8", "gather_bits"])
-def test_sharded_or_equals_unsharded(reduce):
+def test_sharded_or_equals_unsharded(reduce, fused):
+    """fused: one decode_step per step (the packed all_gather ships int32 words)."""
     docs, patterns, steps = make_case()
     want = np.stack(expected_masks(docs, patterns, steps))
-    got = _run(2, 8 + 8 + 1, reduce)      # halo >= longest pattern (7 + 8 steps) + 1
+    got = _run(2, 8 + 8 + 1, reduce, fused)      # halo >= longest pattern (7 + 8 steps) + 1
     for g in got:                          # every rank holds the reduced mask
         assert np.array_equal(g, want)
 
