@@ -83,6 +83,9 @@ struct fm_index {
   fmidx::Index idx;
   std::mutex mu;            // serialises host-API staging buffers / workspace
   uint64_t* scratch = nullptr;  // small device scratch for scalar results
+  void* stage = nullptr;        // grow-only device staging of the synchronous host-API calls
+  void* hstage = nullptr;       // its pinned host mirror (same layout: one copy each way)
+  size_t stage_bytes = 0;
 };
 
 namespace {
@@ -124,20 +127,52 @@ struct DeviceGuard {
     return -1;                                    \
   }
 
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  DevBuf() = default;
-  DevBuf(const DevBuf&) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  int alloc(size_t count) {
-    if (count == 0) count = 1;
-    FM_HIP(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
-    return 0;
+// Device staging of the synchronous host-API calls (always under h->mu): one
+// grow-only buffer carved into 256-B aligned pieces.  A hipMalloc / hipFree
+// pair per call and argument costs tens of us, and hipFree synchronises the
+// whole device (other streams' decode steps included).
+struct Stage {
+  size_t need = 0;
+  template <typename T>
+  size_t add(size_t count) {
+    const size_t off = need;
+    need += (std::max<size_t>(count, 1) * sizeof(T) + 255) & ~size_t(255);
+    return off;
   }
 };
+
+int stage_reserve(fm_index* h, const Stage& st) {
+  if (h->stage_bytes >= st.need) return 0;
+  if (h->stage) FM_HIP(hipFree(h->stage));
+  if (h->hstage) FM_HIP(hipHostFree(h->hstage));
+  h->stage = h->hstage = nullptr;
+  h->stage_bytes = 0;
+  const size_t bytes = std::max<size_t>(st.need, 1 << 20);
+  FM_HIP(hipMalloc(&h->stage, bytes));
+  FM_HIP(hipHostMalloc(&h->hstage, bytes, hipHostMallocDefault));
+  h->stage_bytes = bytes;
+  return 0;
+}
+
+template <typename T>
+T* stage_at(fm_index* h, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(h->stage) + off);
+}
+
+template <typename T>
+T* hstage_at(fm_index* h, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(h->hstage) + off);
+}
+
+// one copy of the staged span [a, b) each way (pinned: a true async DMA)
+int stage_up(fm_index* h, size_t a, size_t b) {
+  FM_HIP(hipMemcpyAsync(stage_at<char>(h, a), hstage_at<char>(h, a), b - a, hipMemcpyHostToDevice, h->idx.stream));
+  return 0;
+}
+int stage_down(fm_index* h, size_t a, size_t b) {
+  FM_HIP(hipMemcpyAsync(hstage_at<char>(h, a), stage_at<char>(h, a), b - a, hipMemcpyDeviceToHost, h->idx.stream));
+  return 0;
+}
 
 int grow_ws(fm_index* h, size_t bytes) {
   auto& x = h->idx;
@@ -226,22 +261,24 @@ int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint
   for (uint64_t i = 0; i < m; ++i)
     cap_off[i + 1] = cap_off[i] + std::min<uint64_t>(distinct_width(lows[i], highs[i], x.n), x.sigma);
   const uint64_t total = cap_off[m];
-  DevBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_k;
-  if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(total) ||
-      d_cnt.alloc(total) || d_k.alloc(m))
-    return -1;
-  FM_HIP(hipMemcpyAsync(d_lo.p, lows, m * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(d_hi.p, highs, m * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(d_off.p, cap_off.data(), (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
+  Stage st;
+  const size_t o_lo = st.add<uint64_t>(m), o_hi = st.add<uint64_t>(m), o_off = st.add<uint64_t>(m + 1),
+               o_syms = st.add<uint64_t>(total), o_cnt = st.add<uint64_t>(total), o_k = st.add<uint64_t>(m);
+  if (stage_reserve(h, st)) return -1;
+  uint64_t *d_lo = stage_at<uint64_t>(h, o_lo), *d_hi = stage_at<uint64_t>(h, o_hi),
+           *d_off = stage_at<uint64_t>(h, o_off), *d_syms = stage_at<uint64_t>(h, o_syms),
+           *d_cnt = stage_at<uint64_t>(h, o_cnt), *d_k = stage_at<uint64_t>(h, o_k);
+  FM_HIP(hipMemcpyAsync(d_lo, lows, m * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(d_hi, highs, m * 8, hipMemcpyHostToDevice, x.stream));
+  FM_HIP(hipMemcpyAsync(d_off, cap_off.data(), (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
   if (grow_ws(h, fmidx::distinct_ws_bytes(total))) return -1;
-  if (fmidx::launch_distinct(x.view, d_lo.p, d_hi.p, m, d_off.p, d_syms.p, d_cnt.p, d_k.p, x.ws,
-                             total, x.stream))
+  if (fmidx::launch_distinct(x.view, d_lo, d_hi, m, d_off, d_syms, d_cnt, d_k, x.ws, total, x.stream))
     return -1;
   std::vector<uint64_t> k(m), s(total), c(total);
-  FM_HIP(hipMemcpyAsync(k.data(), d_k.p, m * 8, hipMemcpyDeviceToHost, x.stream));
+  FM_HIP(hipMemcpyAsync(k.data(), d_k, m * 8, hipMemcpyDeviceToHost, x.stream));
   if (total) {
-    FM_HIP(hipMemcpyAsync(s.data(), d_syms.p, total * 8, hipMemcpyDeviceToHost, x.stream));
-    FM_HIP(hipMemcpyAsync(c.data(), d_cnt.p, total * 8, hipMemcpyDeviceToHost, x.stream));
+    FM_HIP(hipMemcpyAsync(s.data(), d_syms, total * 8, hipMemcpyDeviceToHost, x.stream));
+    FM_HIP(hipMemcpyAsync(c.data(), d_cnt, total * 8, hipMemcpyDeviceToHost, x.stream));
   }
   FM_HIP(hipStreamSynchronize(x.stream));
   offsets.assign(m + 1, 0);
@@ -312,6 +349,8 @@ void fm_destroy(fm_index* h) {
     (void)hipDeviceSynchronize();
     h->idx.release();
     if (h->scratch) (void)hipFree(h->scratch);
+    if (h->stage) (void)hipFree(h->stage);
+    if (h->hstage) (void)hipHostFree(h->hstage);
     if (h->idx.stream) (void)hipStreamDestroy(h->idx.stream);
   }
   delete h;
@@ -445,10 +484,12 @@ int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, u
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   auto& x = h->idx;
-  DevBuf<uint64_t> q;
-  if (q.alloc(len)) return -1;
-  if (len) FM_HIP(hipMemcpyAsync(q.p, query, len * 8, hipMemcpyHostToDevice, x.stream));
-  if (fmidx::launch_raw_multi(x.view, q.p, len, h->scratch, x.stream)) return -1;
+  Stage st;
+  const size_t o_q = st.add<uint64_t>(len);
+  if (stage_reserve(h, st)) return -1;
+  uint64_t* q = stage_at<uint64_t>(h, o_q);
+  if (len) FM_HIP(hipMemcpyAsync(q, query, len * 8, hipMemcpyHostToDevice, x.stream));
+  if (fmidx::launch_raw_multi(x.view, q, len, h->scratch, x.stream)) return -1;
   FM_HIP(hipMemcpyAsync(out, h->scratch, 16, hipMemcpyDeviceToHost, x.stream));
   FM_HIP(hipStreamSynchronize(x.stream));
   return 0;
@@ -519,22 +560,27 @@ int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offset
   auto& x = h->idx;
   if (m == 0) return 0;
   const uint64_t ntok = (uint64_t)offsets[m];
-  DevBuf<int64_t> d_tok, d_off;
-  DevBuf<uint64_t> d_li, d_hi, d_lo2, d_hi2;
-  if (d_tok.alloc(ntok) || d_off.alloc(m + 1) || d_lo2.alloc(m) || d_hi2.alloc(m)) return -1;
-  if (ntok) FM_HIP(hipMemcpyAsync(d_tok.p, tokens, ntok * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(d_off.p, offsets, (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
-  if (lo_in && hi_in) {
-    if (d_li.alloc(m) || d_hi.alloc(m)) return -1;
-    FM_HIP(hipMemcpyAsync(d_li.p, lo_in, m * 8, hipMemcpyHostToDevice, x.stream));
-    FM_HIP(hipMemcpyAsync(d_hi.p, hi_in, m * 8, hipMemcpyHostToDevice, x.stream));
+  const bool starts = lo_in && hi_in;
+  // inputs first, outputs last: one host->device and one device->host copy
+  Stage st;
+  const size_t o_tok = st.add<int64_t>(ntok), o_off = st.add<int64_t>(m + 1), o_li = st.add<uint64_t>(starts ? m : 0),
+               o_hi = st.add<uint64_t>(starts ? m : 0), o_lo2 = st.add<uint64_t>(m), o_hi2 = st.add<uint64_t>(m);
+  if (stage_reserve(h, st)) return -1;
+  if (ntok) std::memcpy(hstage_at<int64_t>(h, o_tok), tokens, ntok * 8);
+  std::memcpy(hstage_at<int64_t>(h, o_off), offsets, (m + 1) * 8);
+  if (starts) {
+    std::memcpy(hstage_at<uint64_t>(h, o_li), lo_in, m * 8);
+    std::memcpy(hstage_at<uint64_t>(h, o_hi), hi_in, m * 8);
   }
-  if (fmidx::launch_search(x.view, d_tok.p, d_off.p, m, shift, d_li.p, d_hi.p, d_lo2.p, d_hi2.p,
-                           x.stream))
+  if (stage_up(h, 0, o_lo2)) return -1;
+  if (fmidx::launch_search(x.view, stage_at<int64_t>(h, o_tok), stage_at<int64_t>(h, o_off), m, shift,
+                           starts ? stage_at<uint64_t>(h, o_li) : nullptr, starts ? stage_at<uint64_t>(h, o_hi) : nullptr,
+                           stage_at<uint64_t>(h, o_lo2), stage_at<uint64_t>(h, o_hi2), x.stream))
     return -1;
-  FM_HIP(hipMemcpyAsync(lo_out, d_lo2.p, m * 8, hipMemcpyDeviceToHost, x.stream));
-  FM_HIP(hipMemcpyAsync(hi_out, d_hi2.p, m * 8, hipMemcpyDeviceToHost, x.stream));
+  if (stage_down(h, o_lo2, st.need)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
+  std::memcpy(lo_out, hstage_at<uint64_t>(h, o_lo2), m * 8);
+  std::memcpy(hi_out, hstage_at<uint64_t>(h, o_hi2), m * 8);
   return 0;
 }
 
