@@ -7,6 +7,8 @@
 set -euo pipefail
 OUT=$1; shift
 mkdir -p "$OUT"
+# the raw trace can exceed gpurun's merge cap: never leave it behind
+trap 'rm -rf "$OUT/raw"' EXIT
 export TMPDIR=/tmp
 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o run -- python3 bench.py --no-cpu "$@" > "$OUT/bench.json" 2> "$OUT/bench.log"
 find "$OUT/raw" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
@@ -18,12 +20,14 @@ steps = int(args[args.index("--steps") + 1]) if "--steps" in args else 20
 d = []
 with open(trace) as f:
     for r in csv.DictReader(f):
-        if "k_decode<false, true>" in r.get("Kernel_Name", ""):
+        if "k_decode<false, true," in r.get("Kernel_Name", ""):  # <PACKED, DO_LF, threads>
             d.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
 d.sort()
+if not d:
+    sys.exit("no k_decode<false, true, *> dispatches in " + trace)
 dur = [x[1] / 1e3 for x in d]
 t = dur[-steps:]
-res = {"kernel": "k_decode<false, true>", "dispatches": len(dur), "avg_us_all": sum(dur) / len(dur),
+res = {"kernel": "k_decode<false, true, *>", "dispatches": len(dur), "avg_us_all": sum(dur) / len(dur),
        "timed_dispatches": len(t), "avg_us_timed": sum(t) / len(t), "min_us_timed": min(t), "max_us_timed": max(t),
        "note": "timed = the last --steps dispatches (the bench's timed graph replay); all includes warmup, "
                "the three replays used for the step estimate and the standalone mask-only graphs' k_decode<false,false> excluded"}
