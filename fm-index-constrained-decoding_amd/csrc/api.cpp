@@ -261,26 +261,27 @@ int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint
   for (uint64_t i = 0; i < m; ++i)
     cap_off[i + 1] = cap_off[i] + std::min<uint64_t>(distinct_width(lows[i], highs[i], x.n), x.sigma);
   const uint64_t total = cap_off[m];
+  // inputs first, outputs last: one host->device and one device->host copy
   Stage st;
   const size_t o_lo = st.add<uint64_t>(m), o_hi = st.add<uint64_t>(m), o_off = st.add<uint64_t>(m + 1),
-               o_syms = st.add<uint64_t>(total), o_cnt = st.add<uint64_t>(total), o_k = st.add<uint64_t>(m);
+               o_k = st.add<uint64_t>(m), o_syms = st.add<uint64_t>(total), o_cnt = st.add<uint64_t>(total);
   if (stage_reserve(h, st)) return -1;
-  uint64_t *d_lo = stage_at<uint64_t>(h, o_lo), *d_hi = stage_at<uint64_t>(h, o_hi),
-           *d_off = stage_at<uint64_t>(h, o_off), *d_syms = stage_at<uint64_t>(h, o_syms),
-           *d_cnt = stage_at<uint64_t>(h, o_cnt), *d_k = stage_at<uint64_t>(h, o_k);
-  FM_HIP(hipMemcpyAsync(d_lo, lows, m * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(d_hi, highs, m * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(d_off, cap_off.data(), (m + 1) * 8, hipMemcpyHostToDevice, x.stream));
+  std::memcpy(hstage_at<uint64_t>(h, o_lo), lows, m * 8);
+  std::memcpy(hstage_at<uint64_t>(h, o_hi), highs, m * 8);
+  std::memcpy(hstage_at<uint64_t>(h, o_off), cap_off.data(), (m + 1) * 8);
+  if (stage_up(h, 0, o_k)) return -1;
   if (grow_ws(h, fmidx::distinct_ws_bytes(total))) return -1;
-  if (fmidx::launch_distinct(x.view, d_lo, d_hi, m, d_off, d_syms, d_cnt, d_k, x.ws, total, x.stream))
+  if (fmidx::launch_distinct(x.view, stage_at<uint64_t>(h, o_lo), stage_at<uint64_t>(h, o_hi), m,
+                             stage_at<uint64_t>(h, o_off), stage_at<uint64_t>(h, o_syms),
+                             stage_at<uint64_t>(h, o_cnt), stage_at<uint64_t>(h, o_k), x.ws, total, x.stream))
     return -1;
-  std::vector<uint64_t> k(m), s(total), c(total);
-  FM_HIP(hipMemcpyAsync(k.data(), d_k, m * 8, hipMemcpyDeviceToHost, x.stream));
-  if (total) {
-    FM_HIP(hipMemcpyAsync(s.data(), d_syms, total * 8, hipMemcpyDeviceToHost, x.stream));
-    FM_HIP(hipMemcpyAsync(c.data(), d_cnt, total * 8, hipMemcpyDeviceToHost, x.stream));
-  }
+  // only the k[] and the used prefix of each capacity slot matter, but the
+  // slots are contiguous: one copy of [k, syms, counts)
+  if (stage_down(h, o_k, total ? o_cnt + total * 8 : o_k + m * 8)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
+  const uint64_t* k = hstage_at<uint64_t>(h, o_k);
+  const uint64_t* s = hstage_at<uint64_t>(h, o_syms);
+  const uint64_t* c = hstage_at<uint64_t>(h, o_cnt);
   offsets.assign(m + 1, 0);
   syms.clear();
   counts.clear();
@@ -473,9 +474,13 @@ int fm_backward_search_step(fm_index* h, uint64_t symbol, uint64_t low, uint64_t
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   auto& x = h->idx;
-  if (fmidx::launch_step_raw(x.view, symbol, low, high, h->scratch, x.stream)) return -1;
-  FM_HIP(hipMemcpyAsync(out, h->scratch, 16, hipMemcpyDeviceToHost, x.stream));
+  Stage st;
+  const size_t o_out = st.add<uint64_t>(2);
+  if (stage_reserve(h, st)) return -1;
+  if (fmidx::launch_step_raw(x.view, symbol, low, high, stage_at<uint64_t>(h, o_out), x.stream)) return -1;
+  if (stage_down(h, o_out, o_out + 16)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
+  std::memcpy(out, hstage_at<uint64_t>(h, o_out), 16);
   return 0;
 }
 
@@ -486,12 +491,17 @@ int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, u
   auto& x = h->idx;
   Stage st;
   const size_t o_q = st.add<uint64_t>(len);
+  const size_t o_out = st.add<uint64_t>(2);
   if (stage_reserve(h, st)) return -1;
-  uint64_t* q = stage_at<uint64_t>(h, o_q);
-  if (len) FM_HIP(hipMemcpyAsync(q, query, len * 8, hipMemcpyHostToDevice, x.stream));
-  if (fmidx::launch_raw_multi(x.view, q, len, h->scratch, x.stream)) return -1;
-  FM_HIP(hipMemcpyAsync(out, h->scratch, 16, hipMemcpyDeviceToHost, x.stream));
+  if (len) {
+    std::memcpy(hstage_at<uint64_t>(h, o_q), query, len * 8);
+    if (stage_up(h, o_q, o_out)) return -1;
+  }
+  if (fmidx::launch_raw_multi(x.view, stage_at<uint64_t>(h, o_q), len, stage_at<uint64_t>(h, o_out), x.stream))
+    return -1;
+  if (stage_down(h, o_out, o_out + 16)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
+  std::memcpy(out, hstage_at<uint64_t>(h, o_out), 16);
   return 0;
 }
 

@@ -35,4 +35,5 @@ out = {"lib": os.path.basename(os.environ.get("FMIDX_LIB", "libfmidx.so")),
 if raw is not None:
     out["distinct_count_multi_256_us"] = per_call(lambda: raw.distinct_count_multi(lo.tolist(), hi.tolist()), 50)
     out["backward_search_multi_8_us"] = per_call(lambda: raw.backward_search_multi([t + 10 for t in pats[0]]))
+    out["backward_search_step_us"] = per_call(lambda: raw.backward_search_step(pats[0][0] + 10, 0, ix.size() - 1))
 print(out, flush=True)
