@@ -24,6 +24,7 @@ that dtype, so outputs match the reference bit for bit.
 from __future__ import annotations
 
 import ctypes
+import functools
 from ctypes import c_void_p
 from typing import List, Optional, Sequence
 
@@ -39,9 +40,11 @@ ROW_DTYPE = np.dtype([("base", "<f4"), ("v_dist", "<f4"), ("v_uni", "<f4"), ("v_
 _DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
 
+@functools.lru_cache(maxsize=4096)
 def _round(x, dtype) -> float:
     """The value a Python number takes when index-put into a ``dtype`` tensor
-    (the reference's ``mask[row, idx] = boost``), through the same setitem path."""
+    (the reference's ``mask[row, idx] = boost``), through the same setitem path.
+    Memoised: a step asks for a few distinct values, but for every row."""
     t = torch.zeros(1, dtype=dtype)
     t[0] = x
     return float(t[0])
@@ -138,8 +141,11 @@ def _find_marker_rows(input_ids: torch.Tensor, marker: Sequence[int]) -> List[to
         return out
     win = ids.unfold(1, m, 1)                                  # [B, L-m+1, m]
     hit = (win == torch.tensor(marker, dtype=ids.dtype)).all(2)
-    for r, i in zip(*torch.nonzero(hit, as_tuple=True)):
-        out.append(input_ids[int(r), int(i) + m:])
+    # slices of the host copy: the callers only read the ids back as lists
+    # (one device slice per row would be B tiny device ops per step)
+    rr, ii = torch.nonzero(hit, as_tuple=True)
+    for r, i in zip(rr.tolist(), ii.tolist()):
+        out.append(ids[r, i + m:])
     return out
 
 
@@ -237,28 +243,36 @@ class QwenIndexBasedLogitsProcessor:
         eos_val = None
         if self.always_allow_eos and L >= self.min_new_tokens:
             eos_val = _round(boost * (self.length_reward_factor ** L), dt)
+        # per-row fields collected as Python lists and written column-wise
+        # (a field store on a numpy record costs ~1 us; B of them per field)
+        flags, v_uni, v_dist, special_tok = [0] * B, [0.0] * B, [0.0] * B, [0] * B
         for i, s in enumerate(proc):
             if s is None:
                 continue
-            r = rows[i]
             if not s:
-                r["flags"] = FLAG_UNIGRAM
-                r["v_uni"] = _round(boost, dt)
+                f = FLAG_UNIGRAM
+                v_uni[i] = _round(boost, dt)
             else:
                 special = _distinct_rule(self.stop_at_count, cnt.get(i, 0), s[-1], self.eos_token_id,
                                          self.pad_token_id)
-                r["v_dist"] = _round(boost * (self.length_reward_factor ** len(s)), dt)
+                v_dist[i] = _round(boost * (self.length_reward_factor ** len(s)), dt)
                 if special is not None:
-                    r["flags"] = FLAG_SPECIAL | FLAG_UNIGRAM
-                    r["special"] = special
+                    f = FLAG_SPECIAL | FLAG_UNIGRAM
+                    special_tok[i] = special
                     empty = False
                 else:
-                    r["flags"] = FLAG_BITS | FLAG_UNIGRAM
+                    f = FLAG_BITS | FLAG_UNIGRAM
                     empty = not bool(has_bits[i])
-                r["v_uni"] = _round(boost if empty else boost / 2, dt)
+                v_uni[i] = _round(boost if empty else boost / 2, dt)
             if eos_val is not None:
-                r["flags"] |= FLAG_EOS
-                r["v_eos"] = eos_val
+                f |= FLAG_EOS
+            flags[i] = f
+        rows["flags"] = flags
+        rows["v_uni"] = v_uni
+        rows["v_dist"] = v_dist
+        rows["special"] = special_tok
+        if eos_val is not None:
+            rows["v_eos"] = [eos_val if s is not None else 0.0 for s in proc]
         return self._core.epilogue(scores, rows, bits, self.eos_token_id)
 
 
