@@ -340,21 +340,26 @@ class CausalIndexBasedLogitsProcessor:
             for i, l, h in zip(pat_rows, lo.tolist(), hi.tolist()):
                 full_lo[i], full_hi[i] = l, h
             bits = self._core.allowed_bits(full_lo, full_hi, V)
+            # column-wise row fields, as in the Qwen variant
+            flags, v_uni, v_dist, special_tok = [0] * B, [0.0] * B, [0.0] * B, [0] * B
             for i, s in enumerate(proc):
-                r = rows[i]
                 if not s:
-                    r["flags"] = FLAG_UNIGRAM
-                    r["v_uni"] = _round(boost, dt)
+                    flags[i] = FLAG_UNIGRAM
+                    v_uni[i] = _round(boost, dt)
                     continue
                 special = _distinct_rule(self.stop_at_count, cnt.get(i, 0), s[-1], self.eos_token_id,
                                          self.pad_token_id)
-                r["v_dist"] = _round(boost * (self.length_reward_factor ** len(s)), dt)
-                r["v_uni"] = _round(boost / 2, dt)          # always BOOST / 2 in this variant
+                v_dist[i] = _round(boost * (self.length_reward_factor ** len(s)), dt)
+                v_uni[i] = _round(boost / 2, dt)          # always BOOST / 2 in this variant
                 if special is not None:
-                    r["flags"] = FLAG_SPECIAL | FLAG_UNIGRAM
-                    r["special"] = special
+                    flags[i] = FLAG_SPECIAL | FLAG_UNIGRAM
+                    special_tok[i] = special
                 else:
-                    r["flags"] = FLAG_BITS | FLAG_UNIGRAM
+                    flags[i] = FLAG_BITS | FLAG_UNIGRAM
+            rows["flags"] = flags
+            rows["v_uni"] = v_uni
+            rows["v_dist"] = v_dist
+            rows["special"] = special_tok
         if self.always_allow_eos:
             rows["flags"] |= FLAG_EOS
             rows["v_eos"] = _round(boost * (self.length_reward_factor ** L), dt)
