@@ -77,7 +77,7 @@ class _BatchedCore:
             z = np.zeros(0, dtype=np.uint64)
             return z, z
         n = self.index.size()
-        keys = [tuple(int(t) for t in p) for p in patterns]
+        keys = [tuple(map(int, p)) for p in patterns]
         toks, slo, shi = [], np.zeros(len(keys), dtype=np.uint64), np.zeros(len(keys), dtype=np.uint64)
         for i, k in enumerate(keys):
             prev = self._prev.get(k[:-1]) if k else None

@@ -57,6 +57,6 @@ for step in range(WARM + STEPS):
     times.append(time.perf_counter() - t)
 t = np.array(times[WARM:]) * 1e3
 print({"B": B, "V": V, "dtype": str(DT).split(".")[1], "corpus_tokens": len(F), "index_build_s": round(build_s, 2),
-       "steps": STEPS, "ms_per_call_mean": round(float(t.mean()), 3), "ms_per_call_min": round(float(t.min()), 3),
+       "steps": STEPS, "ms_per_call_mean": round(float(t.mean()), 3), "ms_per_call_median": round(float(np.median(t)), 3), "ms_per_call_min": round(float(t.min()), 3),
        "ms_per_call_max": round(float(t.max()), 3), "rows_per_s": round(B / (t.mean() / 1e3)),
        "pattern_len_at_end": len(sents[0])}, flush=True)
