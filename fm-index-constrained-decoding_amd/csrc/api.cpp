@@ -31,6 +31,9 @@ void set_error(const char* fmt, ...) {
 }
 
 void Index::release() {
+  // no kernel on any stream may still read what is freed here (the callers
+  // hold the handle's device)
+  (void)hipDeviceSynchronize();
   void* ptrs[] = {wm, sb, Z, D, C, bwt, bm, bm_full, bm_follow, sa, text, ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -86,6 +89,13 @@ struct fm_index {
   void* stage = nullptr;        // grow-only device staging of the synchronous host-API calls
   void* hstage = nullptr;       // its pinned host mirror (same layout: one copy each way)
   size_t stage_bytes = 0;
+  void* dscratch = nullptr;     // device-only scratch of the host API (distinct capacity slots)
+  size_t dscratch_bytes = 0;
+  // the last use of idx.ws, on whatever stream it ran: every launch that uses
+  // the workspace first waits for it (fm_distinct_count_batch runs on the
+  // caller's stream, the host API on idx.stream)
+  hipEvent_t ws_ev = nullptr;
+  bool ws_ev_pending = false;
 };
 
 namespace {
@@ -174,14 +184,57 @@ int stage_down(fm_index* h, size_t a, size_t b) {
   return 0;
 }
 
-int grow_ws(fm_index* h, size_t bytes) {
+// Staging / scratch above these sizes is released at the end of the call that
+// needed it, so one oversized batch does not pin memory for the handle's life.
+constexpr size_t kStageKeep = 64ull << 20;
+constexpr size_t kScratchKeep = 256ull << 20;
+
+void stage_trim(fm_index* h) {
+  if (h->stage_bytes > kStageKeep) {
+    (void)hipFree(h->stage);
+    (void)hipHostFree(h->hstage);
+    h->stage = h->hstage = nullptr;
+    h->stage_bytes = 0;
+  }
+  if (h->dscratch_bytes > kScratchKeep) {
+    (void)hipFree(h->dscratch);
+    h->dscratch = nullptr;
+    h->dscratch_bytes = 0;
+  }
+}
+
+int grow_dscratch(fm_index* h, size_t bytes) {
+  if (h->dscratch_bytes >= bytes) return 0;
+  if (h->dscratch) FM_HIP(hipFree(h->dscratch));
+  h->dscratch = nullptr;
+  h->dscratch_bytes = 0;
+  FM_HIP(hipMalloc(&h->dscratch, bytes));
+  h->dscratch_bytes = bytes;
+  return 0;
+}
+
+// Workspace of k_distinct (under h->mu): wait for its previous use -- on any
+// stream -- before `s` touches it; growing it waits on the host first.
+int ws_acquire(fm_index* h, hipStream_t s, size_t bytes) {
   auto& x = h->idx;
-  if (x.ws_bytes >= bytes) return 0;
-  if (x.ws) FM_HIP(hipFree(x.ws));
-  x.ws = nullptr;
-  x.ws_bytes = 0;
-  FM_HIP(hipMalloc(&x.ws, bytes));
-  x.ws_bytes = bytes;
+  if (!h->ws_ev) FM_HIP(hipEventCreateWithFlags(&h->ws_ev, hipEventDisableTiming));
+  if (x.ws_bytes < bytes) {
+    if (h->ws_ev_pending) FM_HIP(hipEventSynchronize(h->ws_ev));
+    if (x.ws) FM_HIP(hipFree(x.ws));
+    x.ws = nullptr;
+    x.ws_bytes = 0;
+    FM_HIP(hipMalloc(&x.ws, bytes));
+    x.ws_bytes = bytes;
+  } else if (h->ws_ev_pending) {
+    FM_HIP(hipStreamWaitEvent(s, h->ws_ev, 0));
+  }
+  return 0;
+}
+
+// Marks the end of a workspace use enqueued on `s`.
+int ws_release(fm_index* h, hipStream_t s) {
+  FM_HIP(hipEventRecord(h->ws_ev, s));
+  h->ws_ev_pending = true;
   return 0;
 }
 
@@ -252,49 +305,66 @@ uint64_t distinct_width(uint64_t lo, uint64_t hi, uint64_t n) {
   return hi - lo;
 }
 
-// Host-staged batched interval_symbols: syms/counts per range in CSR form.
+// Pairs copied back in the call's one device->host copy; a batch with more
+// distinct symbols than this takes a second copy for the rest.
+constexpr uint64_t kPairsFirstCopy = 1ull << 16;
+
+// Host-staged batched interval_symbols.  Results are compacted on the device
+// into a dense CSR (offsets[m + 1] + interleaved (symbol, count) pairs), so
+// only the symbols found travel back, not the capacity slots (min(width,
+// sigma) per row, ~2 MB for a wide row at a 128k vocabulary).
 int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint64_t m,
-                  std::vector<uint64_t>& syms, std::vector<uint64_t>& counts,
-                  std::vector<uint64_t>& offsets) {
+                  std::vector<uint64_t>& pairs, std::vector<uint64_t>& offsets) {
   auto& x = h->idx;
   std::vector<uint64_t> cap_off(m + 1, 0);
   for (uint64_t i = 0; i < m; ++i)
     cap_off[i + 1] = cap_off[i] + std::min<uint64_t>(distinct_width(lows[i], highs[i], x.n), x.sigma);
   const uint64_t total = cap_off[m];
-  // inputs first, outputs last: one host->device and one device->host copy
+  const uint64_t first = std::min<uint64_t>(total, kPairsFirstCopy);
+  // staged: inputs first, outputs last (one host->device and one device->host copy)
   Stage st;
-  const size_t o_lo = st.add<uint64_t>(m), o_hi = st.add<uint64_t>(m), o_off = st.add<uint64_t>(m + 1),
-               o_k = st.add<uint64_t>(m), o_syms = st.add<uint64_t>(total), o_cnt = st.add<uint64_t>(total);
+  const size_t o_lo = st.add<uint64_t>(m), o_hi = st.add<uint64_t>(m), o_cap = st.add<uint64_t>(m + 1),
+               o_k = st.add<uint64_t>(m), o_off = st.add<uint64_t>(m + 1), o_pairs = st.add<uint64_t>(2 * first);
   if (stage_reserve(h, st)) return -1;
+  // device only: capacity slots (symbols, counts) and the dense pairs
+  const uint64_t T = std::max<uint64_t>(total, 1);
+  if (grow_dscratch(h, (size_t)T * 32)) return -1;
+  uint64_t* d_syms = static_cast<uint64_t*>(h->dscratch);
+  uint64_t* d_cnt = d_syms + T;
+  uint64_t* d_pairs = d_cnt + T;
   std::memcpy(hstage_at<uint64_t>(h, o_lo), lows, m * 8);
   std::memcpy(hstage_at<uint64_t>(h, o_hi), highs, m * 8);
-  std::memcpy(hstage_at<uint64_t>(h, o_off), cap_off.data(), (m + 1) * 8);
+  std::memcpy(hstage_at<uint64_t>(h, o_cap), cap_off.data(), (m + 1) * 8);
   if (stage_up(h, 0, o_k)) return -1;
-  if (grow_ws(h, fmidx::distinct_ws_bytes(total))) return -1;
+  if (ws_acquire(h, x.stream, fmidx::distinct_ws_bytes(total))) return -1;
   if (fmidx::launch_distinct(x.view, stage_at<uint64_t>(h, o_lo), stage_at<uint64_t>(h, o_hi), m,
-                             stage_at<uint64_t>(h, o_off), stage_at<uint64_t>(h, o_syms),
-                             stage_at<uint64_t>(h, o_cnt), stage_at<uint64_t>(h, o_k), x.ws, total, x.stream))
+                             stage_at<uint64_t>(h, o_cap), d_syms, d_cnt, stage_at<uint64_t>(h, o_k), x.ws, total,
+                             x.stream))
     return -1;
-  // only the k[] and the used prefix of each capacity slot matter, but the
-  // slots are contiguous: one copy of [k, syms, counts)
-  if (stage_down(h, o_k, total ? o_cnt + total * 8 : o_k + m * 8)) return -1;
+  if (ws_release(h, x.stream)) return -1;
+  if (fmidx::launch_distinct_csr(stage_at<uint64_t>(h, o_k), stage_at<uint64_t>(h, o_cap), d_syms, d_cnt, m,
+                                 stage_at<uint64_t>(h, o_off), d_pairs, x.stream))
+    return -1;
+  if (first)
+    FM_HIP(hipMemcpyAsync(stage_at<uint64_t>(h, o_pairs), d_pairs, first * 16, hipMemcpyDeviceToDevice, x.stream));
+  if (stage_down(h, o_k, st.need)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
   const uint64_t* k = hstage_at<uint64_t>(h, o_k);
-  const uint64_t* s = hstage_at<uint64_t>(h, o_syms);
-  const uint64_t* c = hstage_at<uint64_t>(h, o_cnt);
-  offsets.assign(m + 1, 0);
-  syms.clear();
-  counts.clear();
+  const uint64_t* off = hstage_at<uint64_t>(h, o_off);
   for (uint64_t i = 0; i < m; ++i) {
     if (k[i] == ~0ull) {
       set_error("distinct_count capacity overflow on range %llu", (unsigned long long)i);
       return -1;
     }
-    for (uint64_t j = 0; j < k[i]; ++j) {
-      syms.push_back(s[cap_off[i] + j]);
-      counts.push_back(c[cap_off[i] + j]);
-    }
-    offsets[i + 1] = offsets[i] + k[i];
+  }
+  const uint64_t used = off[m];
+  offsets.assign(off, off + m + 1);
+  pairs.resize(2 * used);
+  const uint64_t a = std::min(used, first);
+  if (a) std::memcpy(pairs.data(), hstage_at<uint64_t>(h, o_pairs), a * 16);
+  if (used > a) {
+    FM_HIP(hipMemcpyAsync(pairs.data() + 2 * a, d_pairs + 2 * a, (used - a) * 16, hipMemcpyDeviceToHost, x.stream));
+    FM_HIP(hipStreamSynchronize(x.stream));
   }
   return 0;
 }
@@ -352,6 +422,8 @@ void fm_destroy(fm_index* h) {
     if (h->scratch) (void)hipFree(h->scratch);
     if (h->stage) (void)hipFree(h->stage);
     if (h->hstage) (void)hipHostFree(h->hstage);
+    if (h->dscratch) (void)hipFree(h->dscratch);
+    if (h->ws_ev) (void)hipEventDestroy(h->ws_ev);
     if (h->idx.stream) (void)hipStreamDestroy(h->idx.stream);
   }
   delete h;
@@ -502,6 +574,7 @@ int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, u
   if (stage_down(h, o_out, o_out + 16)) return -1;
   FM_HIP(hipStreamSynchronize(x.stream));
   std::memcpy(out, hstage_at<uint64_t>(h, o_out), 16);
+  stage_trim(h);
   return 0;
 }
 
@@ -510,18 +583,16 @@ int fm_distinct_count_multi(fm_index* h, const uint64_t* lows, const uint64_t* h
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
-  std::vector<uint64_t> s, c, off;
-  if (host_distinct(h, lows, highs, m, s, c, off)) return -1;
+  std::vector<uint64_t> pairs, off;
+  const int rc = host_distinct(h, lows, highs, m, pairs, off);
+  stage_trim(h);
+  if (rc) return -1;
   std::memcpy(offsets, off.data(), (m + 1) * 8);
-  if (2 * s.size() > cap) {
-    set_error("output capacity %llu < %llu", (unsigned long long)cap,
-              (unsigned long long)(2 * s.size()));
+  if (pairs.size() > cap) {
+    set_error("output capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)pairs.size());
     return -2;
   }
-  for (size_t i = 0; i < s.size(); ++i) {
-    out[2 * i] = s[i];
-    out[2 * i + 1] = c[i];
-  }
+  if (!pairs.empty()) std::memcpy(out, pairs.data(), pairs.size() * 8);
   return 0;
 }
 
@@ -591,6 +662,7 @@ int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offset
   FM_HIP(hipStreamSynchronize(x.stream));
   std::memcpy(lo_out, hstage_at<uint64_t>(h, o_lo2), m * 8);
   std::memcpy(hi_out, hstage_at<uint64_t>(h, o_hi2), m * 8);
+  stage_trim(h);
   return 0;
 }
 
@@ -797,9 +869,11 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
-  if (grow_ws(h, fmidx::distinct_ws_bytes(total_cap))) return -1;
-  return fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k,
-                                h->idx.ws, total_cap, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ws_acquire(h, s, fmidx::distinct_ws_bytes(total_cap))) return -1;
+  if (fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k, h->idx.ws, total_cap, s))
+    return -1;
+  return ws_release(h, s);
 }
 
 int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, uint64_t V,

@@ -586,6 +586,9 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
                     void* ws, uint64_t total_cap, hipStream_t s, uint64_t min_count = 1,
                     uint64_t* child_lo = nullptr);
 size_t distinct_ws_bytes(uint64_t total_cap);
+// dense CSR (off[m + 1], interleaved (symbol, count) pairs) of launch_distinct's output
+int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64_t* syms, const uint64_t* counts,
+                        uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s);
 
 // epilogue.hip
 int gpu_suffix_sort(const uint32_t* text, uint64_t n, uint32_t* bwt_out, uint64_t* sa_out, hipStream_t s);

@@ -275,6 +275,46 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
   if (threadIdx.x == 0) k_out[row] = fc;
 }
 
+// Dense CSR of k_distinct's output for the host API: off[i] = sum of k[< i]
+// (an overflowed row, k = ~0, contributes 0), then pairs[2 (off[i] + j)] =
+// (symbol, count) -- the interleaved layout of fm_index.cpp:136-143.  One
+// workgroup scans k (m is a host batch, thousands of rows at most).
+__global__ void __launch_bounds__(1024) k_csr_offsets(const uint64_t* __restrict__ k, uint64_t m,
+                                                      uint64_t* __restrict__ off) {
+  __shared__ uint64_t part[1024];
+  const uint64_t per = (m + 1023) / 1024;
+  const uint64_t a = threadIdx.x * per, b = a + per < m ? a + per : m;
+  uint64_t s = 0;
+  for (uint64_t i = a; i < b; ++i) s += k[i] == ~0ull ? 0 : k[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {   // inclusive Hillis-Steele scan
+    const uint64_t y = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint64_t acc = part[threadIdx.x] - s;
+  for (uint64_t i = a; i < b; ++i) {
+    off[i] = acc;
+    acc += k[i] == ~0ull ? 0 : k[i];
+  }
+  if (threadIdx.x == 1023) off[m] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_csr_pairs(const uint64_t* __restrict__ k, const uint64_t* __restrict__ cap_off,
+                                                   const uint64_t* __restrict__ syms,
+                                                   const uint64_t* __restrict__ counts,
+                                                   const uint64_t* __restrict__ off, uint64_t* __restrict__ pairs) {
+  const uint64_t row = blockIdx.x;
+  const uint64_t kk = k[row] == ~0ull ? 0 : k[row];
+  const uint64_t src = cap_off[row], dst = 2 * off[row];
+  for (uint64_t j = threadIdx.x; j < kk; j += 256) {
+    pairs[dst + 2 * j] = syms[src + j];
+    pairs[dst + 2 * j + 1] = counts[src + j];
+  }
+}
+
 uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* s = std::getenv(name);
   if (!s || !*s) return dflt;
@@ -335,6 +375,15 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
   fr.pre[1] = fr.pre[0] + T;
   k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr,
                                          min_count ? min_count : 1, child_lo);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64_t* syms, const uint64_t* counts,
+                        uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s) {
+  if (m == 0) return 0;
+  k_csr_offsets<<<1, 1024, 0, s>>>(k, m, off);
+  k_csr_pairs<<<(unsigned)m, 256, 0, s>>>(k, cap_off, syms, counts, off, pairs);
   FM_HIP(hipGetLastError());
   return 0;
 }

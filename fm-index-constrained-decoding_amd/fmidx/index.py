@@ -8,12 +8,17 @@ sets are identical to the reference's.  Differences are performance-only:
 ``get_range`` runs the whole pattern in one GPU launch (the reference makes
 one SWIG call per token, ``index.py:109-112``) and
 ``get_distinct_count_multi`` is one launch for all rows (``fm_index.cpp:146``
-spawns a thread per row).  ``.oth`` metadata is written as JSON, not pickle.
+spawns a thread per row).  ``.oth`` metadata is the reference's pickle of
+``(beginnings, occurring, labels)`` (index.py:189-207), read back with an
+unpickler that resolves no globals (plain lists / sets / ints / strings / None
+only), so a reference-saved ``.oth`` loads and nothing in it can run code.
 """
 from __future__ import annotations
 
 import bisect
+import io
 import json
+import pickle
 from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -139,22 +144,50 @@ class FMIndex(_FMIndex):
 
     # -- persistence ---------------------------------------------------------
     def save(self, path: str) -> None:  # type: ignore[override]
-        with open(path + ".oth", "w") as f:
-            json.dump({"beginnings": self.beginnings, "occurring": sorted(int(x) for x in self.occurring),
-                       "labels": self.labels}, f)
+        """index.py:189-195: ``.oth`` = pickle of (beginnings, occurring, labels)."""
+        with open(path + ".oth", "wb") as f:
+            pickle.dump((list(self.beginnings), list(self.occurring), self.labels), f)
         return super().save(path + ".fmi")
 
     @classmethod
     def load(cls, path: str, device: Optional[int] = None) -> "FMIndex":
+        """index.py:197-207."""
         index = load_FMIndex(path + ".fmi", device)
         index.__class__ = cls
-        with open(path + ".oth") as f:
-            meta = json.load(f)
-        index.beginnings = [int(x) for x in meta["beginnings"]]
-        index.occurring = [int(x) for x in meta["occurring"]]
-        index.labels = meta.get("labels")
+        index.beginnings, index.occurring, index.labels = read_oth(path + ".oth")
         index.occurring_distinct, index.occurring_counts = index.get_distinct_count(0, len(index))
         return index
 
 
-__all__ = ["FMIndex", "SHIFT", "encode_corpus"]
+class _DataOnlyUnpickler(pickle.Unpickler):
+    """Unpickles builtin containers and scalars only: every global lookup
+    (the only way a pickle can name code to run) is refused, except the set
+    constructors that pickle protocols < 4 spell as a global."""
+
+    _SAFE = {("builtins", "set"): set, ("builtins", "frozenset"): frozenset,
+             ("__builtin__", "set"): set, ("__builtin__", "frozenset"): frozenset}
+
+    def find_class(self, module, name):
+        if (module, name) in self._SAFE:
+            return self._SAFE[(module, name)]
+        raise pickle.UnpicklingError(f".oth metadata may not reference {module}.{name}")
+
+
+def read_oth(path: str):
+    """(beginnings, occurring, labels) of a ``.oth`` file: the reference's
+    pickle (index.py:194), or the JSON this engine wrote before it used pickle."""
+    with open(path, "rb") as f:
+        raw = f.read()
+    if raw[:1] == b"{":
+        meta = json.loads(raw.decode())
+        return ([int(x) for x in meta["beginnings"]], [int(x) for x in meta["occurring"]], meta.get("labels"))
+    obj = _DataOnlyUnpickler(io.BytesIO(raw)).load()
+    if not (isinstance(obj, tuple) and len(obj) == 3):
+        raise ValueError(f"{path}: expected a (beginnings, occurring, labels) tuple")
+    beginnings, occurring, labels = obj
+    if not all(isinstance(x, int) for x in beginnings):
+        raise ValueError(f"{path}: beginnings must be ints")
+    return list(beginnings), occurring, labels
+
+
+__all__ = ["FMIndex", "SHIFT", "encode_corpus", "read_oth"]

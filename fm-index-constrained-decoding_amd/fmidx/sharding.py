@@ -63,6 +63,34 @@ def shard_corpus(docs: Sequence[Sequence[int]], world: int, rank: int, halo: int
     return ([h] if h else []) + [list(d) for d in docs[a:b]], (a, b)
 
 
+def shard_text_device(text, beginnings, world: int, rank: int, halo: int):
+    """Shard ``rank``'s indexed text built on the device from the whole T'.
+
+    ``text`` is T' (int32, sentinel last, index.py:47-53 encoding) and
+    ``beginnings`` the doc offsets (index.py:50).  The encoding of
+    ``[halo] + docs[a:b]`` (shard_corpus) is ONE slice of T': T' holds
+    rev(d_0) rev(d_1) ..., and the halo -- the first H tokens of
+    d_{a-1} d_{a-2} ... -- reversed is exactly the H tokens of T' before
+    beginnings[a].  So T'_r = T'[max(0, beg[a] - H) : beg[b]] + sentinel, with
+    no host copy of the corpus.  Returns (T'_r int32 on text.device, (a, b))."""
+    import torch
+
+    beg = np.asarray(beginnings.cpu() if hasattr(beginnings, "cpu") else beginnings, dtype=np.int64)
+    a, b = shard_docs(np.diff(beg), world)[rank]
+    lo = max(0, int(beg[a]) - int(halo))
+    hi = int(beg[b])
+    out = torch.empty(hi - lo + 1, dtype=torch.int32, device=text.device)
+    out[:-1].copy_(text[lo:hi])
+    out[-1] = 0
+    return out, (a, b)
+
+
+class HaloExceeded(ValueError):
+    """A row's pattern outgrew the shards' halo: OR over shards would no longer
+    equal the unsharded mask (occurrences crossing a shard boundary by more
+    than the halo are in no shard)."""
+
+
 class ShardedDecoder:
     """Incremental constrained decoding over a doc-range shard.
 
@@ -80,7 +108,8 @@ class ShardedDecoder:
     is valid until the next step.
     """
 
-    def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8"):
+    def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8",
+                 halo: Optional[int] = None):
         self.index = index
         self.vocab = vocab
         self.shift = shift
@@ -88,14 +117,34 @@ class ShardedDecoder:
         if reduce not in ("max_u8", "gather_bits"):
             raise ValueError(reduce)
         self.reduce = reduce
+        self.halo = halo
         self.fused = hasattr(index, "decode_step")
         self.lo = None
         self.hi = None
         self._buf = None
+        self._plen = None      # per-row pattern length (device)
+        self._bound = 0        # host upper bound of max(_plen)
+
+    def _check_halo(self):
+        """Exactness needs every pattern to be at most halo - 1 tokens.  The
+        host bound grows by one per step; only when it crosses the limit is
+        the exact per-row maximum read back (one sync) -- restarts may have
+        shortened the rows."""
+        if self.halo is None or self._bound <= self.halo - 1:
+            return
+        exact = int(self._plen.max().item()) if self._plen.numel() else 0
+        if exact > self.halo - 1:
+            raise HaloExceeded(f"pattern of {exact} tokens needs a halo of >= {exact + 1} (shards built with "
+                               f"{self.halo}); rebuild the shards with a larger halo or restart the row")
+        self._bound = exact
 
     def start(self, patterns: Sequence[Sequence[int]], device):
         import torch
 
+        lens = [len(p) for p in patterns]
+        self._plen = torch.tensor(lens, dtype=torch.int64, device=device)
+        self._bound = max(lens, default=0)
+        self._check_halo()
         lo, hi = self.index.get_range_batch(patterns, self.shift)
         self.lo = torch.tensor(lo.astype(np.int64), device=device)
         self.hi = torch.tensor(hi.astype(np.int64), device=device)
@@ -103,12 +152,23 @@ class ShardedDecoder:
         return self.mask()
 
     def step(self, tokens):
-        """Append one token per row (token < 0: restart with an empty pattern)."""
+        """Append one token per row (token < 0: restart with an empty pattern).
+        Raises HaloExceeded (before any work) when a row's pattern would be
+        longer than the shards' halo allows."""
+        import torch
+
+        if self._plen is not None:
+            plen = torch.where(tokens < 0, torch.zeros_like(self._plen), self._plen + 1)
+            prev = (self._plen, self._bound)
+            self._plen, self._bound = plen, self._bound + 1
+            try:
+                self._check_halo()
+            except HaloExceeded:
+                self._plen, self._bound = prev
+                raise
         if not self.fused:
             self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
             return self.mask()
-        import torch
-
         packed = self.group is not None and self.reduce == "gather_bits"
         if self._buf is None:
             B = self.lo.numel()
@@ -178,4 +238,5 @@ def unpack_bits(packed, vocab: int):
     return bits[:, :vocab].contiguous()
 
 
-__all__ = ["shard_docs", "halo_tokens", "shard_corpus", "ShardedDecoder", "pack_bits", "unpack_bits"]
+__all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
+           "pack_bits", "unpack_bits"]

@@ -179,3 +179,50 @@ def test_shard_docs_balanced():
     docs = [[1, 2], [3, 4, 5], [6]]
     assert halo_tokens(docs, 2, 4) == [3, 4, 5, 1]   # F continues with d1 then d0
     assert halo_tokens(docs, 0, 4) == []
+
+
+def test_shard_text_device_is_shard_corpus_encoding():
+    """shard_text_device slices T' on the device; the slice must be exactly
+    index.py's encoding of shard_corpus's [halo] + docs[a:b] (+ sentinel)."""
+    from fmidx.index import encode_corpus
+    from fmidx.sharding import shard_corpus, shard_text_device
+
+    docs, _, _ = make_case(11)
+    data, beginnings, _ = encode_corpus(docs)
+    text = torch.tensor(np.concatenate([data.astype(np.int64), [0]]), dtype=torch.int32)
+    for world in (1, 2, 3, 5):
+        for rank in range(world):
+            for halo in (0, 1, 7, 40, 10 ** 6):
+                sd, ab = shard_corpus(docs, world, rank, halo)
+                want, _, _ = encode_corpus(sd)
+                got, ab2 = shard_text_device(text, beginnings, world, rank, halo)
+                assert ab == ab2
+                assert got.tolist() == want.tolist() + [0], (world, rank, halo)
+
+
+def test_halo_guard():
+    """A row whose pattern outgrows halo - 1 tokens raises HaloExceeded before
+    the step runs; restarts (token < 0) shorten rows and keep them legal."""
+    from fmidx.sharding import HaloExceeded, ShardedDecoder
+
+    docs, patterns, _ = make_case()
+    shard = OracleShard(docs)
+    pats = [p[:3] for p in patterns]
+    dec = ShardedDecoder(shard, V, SHIFT, halo=6)
+    dec.start(pats, "cpu")
+    B = len(pats)
+    tok = torch.full((B,), 5, dtype=torch.int64)
+    dec.step(tok)                                   # 4 tokens
+    dec.step(tok)                                   # 5 = halo - 1: still exact
+    with pytest.raises(HaloExceeded):
+        dec.step(tok)                               # 6 > halo - 1
+    lo_before = dec.lo.clone()
+    # the refused step left the state untouched; restarting every row makes it legal again
+    assert torch.equal(dec.lo, lo_before)
+    dec.step(torch.full((B,), -1, dtype=torch.int64))
+    for _ in range(5):
+        dec.step(tok)
+    with pytest.raises(HaloExceeded):
+        dec.step(tok)
+    with pytest.raises(HaloExceeded):
+        ShardedDecoder(shard, V, SHIFT, halo=3).start(pats + [[1, 2, 3]], "cpu")
