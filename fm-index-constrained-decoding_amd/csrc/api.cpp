@@ -925,6 +925,12 @@ int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
   return fmidx::launch_cache_probe(h->idx.view, d_lo, d_hi, m, d_out, reinterpret_cast<hipStream_t>(stream));
 }
 
+int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
+                    uint64_t* d_sink, void* stream) {
+  return fmidx::launch_probe_gather(d_buf, bytes, chase, loads, threads, d_sink,
+                                    reinterpret_cast<hipStream_t>(stream));
+}
+
 int fm_device_bwt(const fm_index* h, const uint32_t** out) {
   FM_CHECK_BUILT(h);
   *out = h->idx.bwt;

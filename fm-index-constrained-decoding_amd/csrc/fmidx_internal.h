@@ -590,6 +590,10 @@ size_t distinct_ws_bytes(uint64_t total_cap);
 int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64_t* syms, const uint64_t* counts,
                         uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s);
 
+// probe.hip (bench roofline): random 64-B gathers / dependent chase
+int launch_probe_gather(const void* buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads_or_chains,
+                        uint64_t* sink, hipStream_t s);
+
 // epilogue.hip
 int gpu_suffix_sort(const uint32_t* text, uint64_t n, uint32_t* bwt_out, uint64_t* sa_out, hipStream_t s);
 int gpu_wt_int_levels(const uint32_t* bwt, uint64_t n, uint32_t L, uint64_t* words, hipStream_t s);

@@ -127,3 +127,77 @@ def bwt_from_sa(text: torch.Tensor, sa: torch.Tensor) -> torch.Tensor:
     prev = sa - 1
     prev[prev < 0] = n - 1
     return text[prev]
+
+
+def decode_trace(fm, text: torch.Tensor, bwt: torch.Tensor, B: int, V: int, S: int, seed: int, device):
+    """The bench's decode trace, built on the device, untimed.
+
+    B rows start from true corpus patterns of U{1..32} tokens (n-grams of F =
+    reverse(T')); each step a live row appends a true continuation (the BWT
+    symbol of a uniformly chosen row of its range: a random occurrence's next
+    token) with p = 0.9, else a uniform random id; a row whose range went empty
+    restarts (token -1 = empty pattern = the full range).  Row 0 is an
+    empty-pattern row, row 1 an eos-terminated (empty-range) row fed an unknown
+    id.  Returns (tokens [S, B], (lo0, hi0), lo_hist [S, B], hi_hist [S, B],
+    patterns0): the ranges after every step come from fm.decode_step itself, and
+    ``patterns0`` (host lists) are the rows' initial patterns, from which
+    ``trace_patterns`` gives every row's whole pattern after any step (for the
+    reference-faithful full re-search)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 1)
+    n = bwt.numel()
+    lens = torch.randint(1, 33, (B,), generator=g, device=device)
+    q = torch.randint(0, n - 40, (B,), generator=g, device=device)
+    offs = torch.zeros(B + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, 0, out=offs[1:])
+    tot = int(offs[-1].item())
+    row_of = torch.repeat_interleave(torch.arange(B, device=device), lens)
+    k = torch.arange(tot, device=device) - offs[:-1][row_of]
+    toks = text[(n - 2) - (q[row_of] + k)].to(torch.int64) - SHIFT
+    lo = torch.zeros(B, dtype=torch.int64, device=device)
+    hi = torch.zeros(B, dtype=torch.int64, device=device)
+    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    lo[0], hi[0] = 0, n          # empty-pattern row
+    lo[1], hi[1] = 0, 0          # eos-terminated row
+    init = (lo.clone(), hi.clone())
+    tok_h = toks.cpu().tolist()
+    off_h = offs.cpu().tolist()
+    pats = [tok_h[off_h[b]:off_h[b + 1]] for b in range(B)]
+    pats[0] = []
+    tokens = torch.empty((S, B), dtype=torch.int64, device=device)
+    lo_hist = torch.empty((S, B), dtype=torch.int64, device=device)
+    hi_hist = torch.empty((S, B), dtype=torch.int64, device=device)
+    dummy = torch.empty((1, 1), dtype=torch.uint8, device=device)
+    for s in range(S):
+        live = lo < hi
+        width = (hi - lo).clamp(min=1)
+        u = torch.rand(B, generator=g, device=device, dtype=torch.float64)
+        j = (lo + (u * width.to(torch.float64)).to(torch.int64).clamp(max=n - 1)).clamp(max=n - 1)
+        true_tok = bwt[j].to(torch.int64) - SHIFT
+        rnd = torch.randint(0, V, (B,), generator=g, device=device)
+        coin = torch.rand(B, generator=g, device=device) < 0.9
+        tok = torch.where(coin & (true_tok >= 0), true_tok, rnd)
+        tok = torch.where(live, tok, torch.full_like(tok, -1))
+        tok[0] = -1
+        tok[1] = V + 1000             # unknown id: the eos row stays empty
+        tokens[s] = tok
+        fm.decode_step(tok, lo, hi, dummy, 0, SHIFT, reset_below=0)
+        lo_hist[s] = lo
+        hi_hist[s] = hi
+    torch.cuda.synchronize(device)
+    return tokens, init, lo_hist, hi_hist, pats
+
+
+def trace_patterns(patterns0, tokens, upto: int):
+    """Every row's whole pattern after step ``upto`` (inclusive) of a
+    decode_trace: the initial pattern plus the appended tokens, emptied by a
+    restart (token < 0)."""
+    pats = [list(p) for p in patterns0]
+    rows = tokens[: upto + 1].tolist() if hasattr(tokens, "tolist") else tokens[: upto + 1]
+    for row in rows:
+        for b, t in enumerate(row):
+            if t < 0:
+                pats[b] = []
+            else:
+                pats[b].append(int(t))
+    return pats

@@ -250,6 +250,15 @@ int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint
 int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
                           void* stream);
 
+/* HBM gather probe (bench roofline of the rank/LF path); no
+ * index needed, current device.  chase == 0: ``threads`` threads each load
+ * ``loads`` independent random 64-B lines of d_buf[0, bytes) (the random-line
+ * throughput ceiling); chase != 0: ``threads`` chains each follow ``loads``
+ * dependent hops (next line = the uint64 at the start of the current line
+ * mod the line count).  d_sink: >= 1024 uint64 (practically never written). */
+int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
+                    uint64_t* d_sink, void* stream);
+
 /* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces. */
 int fm_device_bwt(const fm_index* h, const uint32_t** out);
 

@@ -329,21 +329,39 @@ void cr_decode_step(void* p, const int64_t* tok, int64_t shift, int64_t reset_be
   });
 }
 
-// Reference-faithful step: get_range of the whole pattern from scratch
-// (index.py:103-114, one backward_search_step per token) + distinct_count.
+// index.py:103-114: get_range of tokens[a, b) from scratch, one
+// backward_search_step per token, early exit at (0, 0).
+inline void get_range(const CpuRef& h, const int64_t* tokens, int64_t a, int64_t b, int64_t shift, uint64_t& l,
+                      uint64_t& r) {
+  l = 0;
+  r = h.n;
+  for (int64_t j = a; j < b; ++j) {
+    const int64_t s = tokens[j] + shift;
+    uint64_t ol = 0, oh = 0;
+    if (s >= 0) h.backward_search_step((uint64_t)s, l, r - 1, ol, oh);
+    l = ol;
+    r = oh;
+    if (l == 0 && r == 0) break;
+  }
+}
+
+// Reference-faithful step: get_range of the whole pattern from scratch +
+// distinct_count.  faithful != 0 repeats the searches the Qwen processor makes
+// per row (document_constrained_generation_causal_qwen.py:97,135,138):
+// get_count([last]), get_range(sent), get_count(sent).
 void cr_full_step(void* p, const int64_t* tokens, const int64_t* offsets, int64_t shift, uint64_t m,
-                  uint64_t* lo, uint64_t* hi, uint8_t* mask, uint64_t vocab, int threads) {
+                  uint64_t* lo, uint64_t* hi, uint8_t* mask, uint64_t vocab, int threads, int faithful) {
   const CpuRef& h = *static_cast<CpuRef*>(p);
   parallel_rows(m, threads, [&](uint64_t i, std::vector<uint64_t>& buf) {
     uint64_t l = 0, r = h.n;
-    for (int64_t j = offsets[i]; j < offsets[i + 1]; ++j) {
-      const int64_t s = tokens[j] + shift;
-      uint64_t ol = 0, oh = 0;
-      if (s >= 0) h.backward_search_step((uint64_t)s, l, r - 1, ol, oh);
-      l = ol;
-      r = oh;
-      if (l == 0 && r == 0) break;
+    if (faithful && offsets[i + 1] > offsets[i]) {
+      uint64_t l1, r1;
+      get_range(h, tokens, offsets[i + 1] - 1, offsets[i + 1], shift, l1, r1);   // count([last])
+      get_range(h, tokens, offsets[i], offsets[i + 1], shift, l1, r1);           // get_count(sent)
+      buf.push_back(r1 - l1);   // keep the results live
+      buf.clear();
     }
+    get_range(h, tokens, offsets[i], offsets[i + 1], shift, l, r);
     lo[i] = l;
     hi[i] = r;
     const uint64_t k = h.distinct_count(l, r, buf);

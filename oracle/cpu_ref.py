@@ -30,7 +30,7 @@ def lib():
         d.cr_decode_step.argtypes = [c_void_p, POINTER(c_int64), c_int64, c_int64, u64p, u64p, c_uint64,
                                      POINTER(ctypes.c_uint8), c_uint64, c_int]
         d.cr_full_step.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), c_int64, c_uint64, u64p, u64p,
-                                   POINTER(ctypes.c_uint8), c_uint64, c_int]
+                                   POINTER(ctypes.c_uint8), c_uint64, c_int, c_int]
         _lib = d
     return _lib
 
@@ -76,6 +76,24 @@ class CpuRef:
         L = max(1, int(bwt.max()).bit_length())
         return cls(levels_numpy(bwt, L), bwt.size, L, c_array(bwt, L), int(np.unique(bwt).size))
 
+    @classmethod
+    def from_device_bwt(cls, bwt) -> "CpuRef":
+        """From a device BWT at any scale: the wt_int level vectors are built on
+        the GPU (fm_wt_int_levels_device, itself checked against
+        levels_numpy) and copied to the host; C / sigma by bincount."""
+        import torch
+
+        from fmidx.fm_index import wt_int_levels_device
+
+        n = bwt.numel()
+        L = max(1, int(bwt.max().item()).bit_length())
+        words = wt_int_levels_device(bwt, L).cpu().numpy().view(np.uint64)
+        cnt = torch.bincount(bwt.to(torch.int64), minlength=(1 << L) + 1)
+        C = torch.zeros((1 << L) + 1, dtype=torch.int64, device=bwt.device)
+        torch.cumsum(cnt[: 1 << L], 0, out=C[1:])
+        sigma = int((cnt > 0).sum().item())
+        return cls(words, n, L, C.cpu().numpy().view(np.uint64), sigma)
+
     def __del__(self):
         if getattr(self, "_h", None):
             lib().cr_free(self._h)
@@ -97,6 +115,9 @@ class CpuRef:
         lib().cr_decode_step(self._h, _p(tok, c_int64), shift, reset_below, _p(lo), _p(hi), lo.size,
                              _p(mask, ctypes.c_uint8), mask.shape[1], threads)
 
-    def full_step(self, tokens: np.ndarray, offsets: np.ndarray, shift: int, lo, hi, mask, threads: int):
+    def full_step(self, tokens: np.ndarray, offsets: np.ndarray, shift: int, lo, hi, mask, threads: int,
+                  faithful: bool = False):
+        """get_range of every row's whole pattern + distinct_count + mask row;
+        ``faithful`` also makes the Qwen processor's two extra searches per row."""
         lib().cr_full_step(self._h, _p(tokens, c_int64), _p(offsets, c_int64), shift, lo.size, _p(lo), _p(hi),
-                           _p(mask, ctypes.c_uint8), mask.shape[1], threads)
+                           _p(mask, ctypes.c_uint8), mask.shape[1], threads, 1 if faithful else 0)

@@ -535,52 +535,35 @@ def test_gpu_suffix_sort_at_scale_matches_doubling(dev):
     assert torch.equal(got, want)
 
 
-def test_index_beyond_2e32_rows(dev):
-    """n > 2^32 (enwiki scale): size-independent properties --
-    BWT histogram == text histogram, every true n-gram of F has a non-empty
-    range, and unigram / bigram counts equal brute-force counts of the text."""
+def test_distinct_workspace_across_streams(dev):
+    """fm_distinct_count_batch on a side stream and the host-API
+    distinct_count_multi (internal stream) share the k_distinct workspace;
+    interleaved, every result must still equal the oracle's."""
     import torch
 
-    from fmidx.fm_index import FMIndex, suffix_sort_device
-    from fmidx.synth import markov_corpus_gpu
-
-    if torch.cuda.get_device_properties(0).total_memory < (200 << 30):
-        pytest.skip("needs a 288 GB MI355X")
-    SHIFT = 10
-    text, _ = markov_corpus_gpu(4_400_000_000, 128256, 7, dev)
-    n = text.numel()
-    assert n > (1 << 32)
-    bwt, _ = suffix_sort_device(text)
-    assert torch.equal(torch.bincount(text, minlength=128300), torch.bincount(bwt, minlength=128300))
-    fm = FMIndex(device=0)
-    fm.initialize_from_bwt_device(bwt)
-    del bwt
-    g = torch.Generator(device=dev)
-    g.manual_seed(11)
-    B = 2048
-    lens = torch.randint(1, 9, (B,), generator=g, device=dev)
-    q = torch.randint(0, n - 20, (B,), generator=g, device=dev)
-    # half of the starts in the last 2^31 rows of F (T' positions < 2^31 are the
-    # other end), so both ends of the 64-bit position space are exercised
-    q[: B // 2] = q[: B // 2] % (1 << 31)
-    offs = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(lens, 0, out=offs[1:])
-    row_of = torch.repeat_interleave(torch.arange(B, device=dev), lens)
-    k = torch.arange(int(offs[-1]), device=dev) - offs[:-1][row_of]
-    toks = text[(n - 2) - (q[row_of] + k)].to(torch.int64) - SHIFT
-    lo = torch.zeros(B, dtype=torch.int64, device=dev)
-    hi = torch.zeros(B, dtype=torch.int64, device=dev)
-    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
-    assert bool((hi > lo).all()), int((hi <= lo).sum())
-    F = torch.flip(text[:-1], [0])
-    del text
-    for r in range(4):
-        a, b = int(toks[offs[r]]) + SHIFT, int(toks[offs[r] + 1]) + SHIFT
-        uni = int((F == a).sum())
-        bi = int(((F[:-1] == a) & (F[1:] == b)).sum())
-        for pat, want in (([a - SHIFT], uni), ([a - SHIFT, b - SHIFT], bi)):
-            l1 = torch.zeros(1, dtype=torch.int64, device=dev)
-            h1 = torch.zeros(1, dtype=torch.int64, device=dev)
-            fm.backward_search_batch(torch.tensor(pat, device=dev), torch.tensor([0, len(pat)], device=dev),
-                                     SHIFT, l1, h1)
-            assert int(h1 - l1) == want, (pat, int(h1 - l1), want)
+    docs = markov_docs(61, 300, 3000, 150)
+    ours = ours_index(docs)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    rng = np.random.default_rng(17)
+    side = torch.cuda.Stream(device=dev)
+    for it in range(6):
+        a = rng.integers(0, n, size=200)
+        b = np.minimum(a + rng.integers(1, 5000, size=200), n)
+        lo_t = torch.tensor(a, dtype=torch.int64, device=dev)
+        hi_t = torch.tensor(b, dtype=torch.int64, device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            res = ours.distinct_count_batch(lo_t, hi_t)
+        a2 = rng.integers(0, n, size=50).tolist()
+        b2 = [min(x + int(rng.integers(1, 20000)), n) for x in a2]
+        assert ours.distinct_count_multi(a2, b2) == ora.distinct_count_multi(a2, b2)
+        side.synchronize()
+        syms, counts, k, cap_off = [x.cpu().numpy() for x in res]
+        for i in range(0, 200, 7):
+            s0 = int(cap_off[i])
+            got = []
+            for j in range(int(k[i])):
+                got += [int(syms[s0 + j]), int(counts[s0 + j])]
+            assert tuple(got) == ora.distinct_count(int(a[i]), int(b[i])), (it, i)

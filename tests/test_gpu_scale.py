@@ -1,0 +1,236 @@
+"""Mask and range parity at BASELINE.json's full sizes, on the GPU.
+
+* C3 shape: n = 4.4e9 > 2^32 rows (64-bit positions), decode steps at B = 256
+  (1024-thread decode geometry) and at C5's B = 2048 (256-thread geometry).
+* C2 shape: n = 3e8, B = 32.
+
+Every step's ranges AND full [B, 128256] masks are compared with the
+sdsl-faithful CPU restatement (oracle/cpu_ref.cpp, an independent wt_int +
+rank_support_v implementation) fed the same tokens; 1- and 2-token patterns are
+also checked against a brute-force scan of the text ("the tokens that follow
+every occurrence").  Reference semantics: fm_index.cpp:67-97 (LF step),
+:119-144 (distinct symbols), index.py:103-114 (get_range), and the boolean
+core of document_constrained_generation_causal_qwen.py:189-204.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHIFT = 10
+V = 128256
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def _build(n_tokens, seed, dev):
+    import torch
+
+    from fmidx.fm_index import FMIndex, suffix_sort_device
+    from fmidx.synth import markov_corpus_gpu
+
+    text, _ = markov_corpus_gpu(n_tokens, V, seed, dev)
+    bwt, _ = suffix_sort_device(text)
+    fm = FMIndex(device=0)
+    fm.initialize_from_bwt_device(bwt)
+    torch.cuda.synchronize()
+    return fm, text, bwt
+
+
+@pytest.fixture(scope="module")
+def c3(dev):
+    import torch
+
+    if torch.cuda.get_device_properties(0).total_memory < (200 << 30):
+        pytest.skip("needs a 288 GB MI355X")
+    from oracle.cpu_ref import CpuRef
+
+    fm, text, bwt = _build(4_400_000_000, 7, dev)
+    assert bwt.numel() > (1 << 32)
+    ref = CpuRef.from_device_bwt(bwt)
+    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref}
+    del fm, text, bwt, ref
+    torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def c2(dev):
+    import torch
+
+    from oracle.cpu_ref import CpuRef
+
+    fm, text, bwt = _build(300_000_000, 5, dev)
+    ref = CpuRef.from_device_bwt(bwt)
+    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref}
+    del fm, text, bwt, ref
+    torch.cuda.empty_cache()
+
+
+def _decode_vs_cpu_ref(ix, B, S, seed, dev, threads=None, monkeypatch=None):
+    """S fused decode steps (LF + uint8 mask) for B rows of the bench's trace;
+    every step's ranges and masks against cpu_ref fed the same tokens."""
+    import torch
+
+    from fmidx.synth import decode_trace
+
+    fm, text, bwt, ref = ix["fm"], ix["text"], ix["bwt"], ix["ref"]
+    if threads is not None:
+        monkeypatch.setenv("FMIDX_DEC_THREADS", str(threads))
+    tokens, init, _, _, _ = decode_trace(fm, text, bwt, B, V, S, seed, dev)
+    lo, hi = init[0].clone(), init[1].clone()
+    clo = init[0].cpu().numpy().astype(np.uint64)
+    chi = init[1].cpu().numpy().astype(np.uint64)
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    cmask = np.zeros((B, V), dtype=np.uint8)
+    tok_np = tokens.cpu().numpy()
+    widths = []
+    for s in range(S):
+        fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
+        ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, clo, chi, cmask, 16)
+        glo = lo.cpu().numpy().astype(np.uint64)
+        ghi = hi.cpu().numpy().astype(np.uint64)
+        assert np.array_equal(glo, clo) and np.array_equal(ghi, chi), f"step {s}: ranges differ"
+        gm = mask.cpu().numpy()
+        bad = np.nonzero((gm != cmask).any(1))[0]
+        assert bad.size == 0, f"step {s}: masks differ on rows {bad[:8].tolist()}"
+        widths.append(ghi.astype(np.int64) - glo.astype(np.int64))
+    w = np.concatenate(widths)
+    return w
+
+
+@pytest.mark.timeout(900)
+def test_c3_decode_b256_vs_cpu_ref(dev, c3):
+    """C3 shape (n > 2^32, B = 256): the headline bench configuration."""
+    w = _decode_vs_cpu_ref(c3, 256, 6, 101, dev)
+    # the trace covers every row class: empty, narrow, wide, the full range
+    assert (w == 0).any() and ((w > 0) & (w <= 512)).any() and (w > 4096).any()
+
+
+@pytest.mark.timeout(900)
+def test_c3_decode_b2048_vs_cpu_ref(dev, c3):
+    """C5's row count (512 x beam 4 = 2048) on the > 2^32 index: the decode
+    kernel's 256-thread geometry (several rows per CU)."""
+    w = _decode_vs_cpu_ref(c3, 2048, 3, 202, dev)
+    assert ((w > 512) & (w <= 4096)).any()
+
+
+@pytest.mark.timeout(900)
+def test_c3_ngrams_vs_brute_force(dev, c3):
+    """1- and 2-token patterns: the allowed set == the tokens that follow
+    every occurrence in F, found by scanning the text (no index involved).
+    In T' coordinates (index.py:47-53) an occurrence of [a] at T'[j] (j >= 1)
+    is followed in F by T'[j - 1]; of [a, b] at T'[j] = b, T'[j + 1] = a."""
+    import torch
+
+    fm, text = c3["fm"], c3["text"]
+    n = text.numel()
+    body = text[:-1]
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    picks = body[torch.randint(1, n - 3, (6,), generator=g, device=dev)].tolist()
+    pats = []
+    for j, a in enumerate(picks):
+        pats.append([a - SHIFT])
+        if j < 4:   # a true bigram of F: a then the token after one of its occurrences
+            occ = torch.nonzero(body[1:] == a).squeeze(1) + 1
+            nxt = int(body[occ[len(occ) // 2] - 1])
+            pats.append([a - SHIFT, nxt - SHIFT])
+    pats.append([int(torch.argmax(torch.bincount(body[: 1 << 24], minlength=V + SHIFT))) - SHIFT])  # most frequent
+    m = len(pats)
+    offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), device=dev)
+    toks = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=dev)
+    lo = torch.zeros(m, dtype=torch.int64, device=dev)
+    hi = torch.zeros(m, dtype=torch.int64, device=dev)
+    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    got = fm.allowed_mask(lo, hi, V, SHIFT).cpu().numpy()
+    for i, p in enumerate(pats):
+        a = p[0] + SHIFT
+        if len(p) == 1:
+            hit = torch.nonzero(body[1:] == a).squeeze(1) + 1
+        else:
+            b = p[1] + SHIFT
+            hit = torch.nonzero((body[1:-1] == b) & (body[2:] == a)).squeeze(1) + 1
+        want = np.zeros(V, dtype=np.uint8)
+        want[(body[hit - 1].to(torch.int64) - SHIFT).unique().cpu().numpy()] = 1
+        # sentinel: an occurrence at T'[0] is followed by the sentinel (filtered)
+        assert int(hi[i] - lo[i]) == len(hit) + int(body[0] == a if len(p) == 1 else
+                                                    (body[0] == p[1] + SHIFT and body[1] == a)), p
+        assert np.array_equal(got[i], want), p
+    # the fused decode step from the full range gives the 1-gram masks too
+    one = [i for i, p in enumerate(pats) if len(p) == 1]
+    B = len(one)
+    lo1 = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi1 = torch.full((B,), n, dtype=torch.int64, device=dev)
+    mk = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    fm.decode_step(torch.tensor([pats[i][0] for i in one], device=dev), lo1, hi1, mk, V, SHIFT)
+    assert np.array_equal(mk.cpu().numpy(), got[one])
+
+
+@pytest.mark.timeout(900)
+def test_c3_index_properties(dev, c3):
+    """BWT histogram == text histogram, every true n-gram of F (B = 2048, both
+    ends of the 64-bit position space) has a non-empty range."""
+    import torch
+
+    fm, text, bwt = c3["fm"], c3["text"], c3["bwt"]
+    n = text.numel()
+    assert torch.equal(torch.bincount(text, minlength=V + 100), torch.bincount(bwt, minlength=V + 100))
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    B = 2048
+    lens = torch.randint(1, 9, (B,), generator=g, device=dev)
+    q = torch.randint(0, n - 20, (B,), generator=g, device=dev)
+    q[: B // 2] = q[: B // 2] % (1 << 31)
+    offs = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    row_of = torch.repeat_interleave(torch.arange(B, device=dev), lens)
+    k = torch.arange(int(offs[-1]), device=dev) - offs[:-1][row_of]
+    toks = text[(n - 2) - (q[row_of] + k)].to(torch.int64) - SHIFT
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.zeros(B, dtype=torch.int64, device=dev)
+    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    assert bool((hi > lo).all()), int((hi <= lo).sum())
+
+
+@pytest.mark.timeout(600)
+def test_c2_decode_b32_vs_cpu_ref(dev, c2):
+    """C2 shape (simplewiki scale n = 3e8, B = 32), 12 steps."""
+    w = _decode_vs_cpu_ref(c2, 32, 12, 303, dev)
+    assert (w > 0).any()
+
+
+@pytest.mark.timeout(600)
+def test_c2_full_research_equals_incremental(dev, c2):
+    """The reference re-searches the whole pattern every step (A3 x3,
+    index.py:103-114); the engine carries (lo, hi).  After 20 steps the ranges
+    of a full device re-search of every row's whole pattern, and cpu_ref's
+    full re-search, equal the incremental state."""
+    import torch
+
+    from fmidx.synth import decode_trace, trace_patterns
+
+    fm, text, bwt, ref = c2["fm"], c2["text"], c2["bwt"], c2["ref"]
+    B, S = 32, 20
+    tokens, _, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S, 404, dev)
+    pats = trace_patterns(pats0, tokens.cpu().numpy(), S - 1)
+    lo, hi = fm.get_range_batch(pats, SHIFT)
+    assert np.array_equal(lo.astype(np.int64), lo_hist[-1].cpu().numpy())
+    assert np.array_equal(hi.astype(np.int64), hi_hist[-1].cpu().numpy())
+    toks = np.asarray([t for p in pats for t in p], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum([len(p) for p in pats])]).astype(np.int64)
+    clo = np.zeros(B, dtype=np.uint64)
+    chi = np.zeros(B, dtype=np.uint64)
+    cm = np.zeros((B, V), dtype=np.uint8)
+    ref.full_step(toks, offs, SHIFT, clo, chi, cm, 8, faithful=True)
+    # the reference's early exit maps an empty pattern range to (0, 0); the
+    # empty pattern itself is (0, n)
+    assert np.array_equal(clo, lo) and np.array_equal(chi, hi)
+    gm = fm.allowed_mask(lo_hist[-1], hi_hist[-1], V, SHIFT).cpu().numpy()
+    assert np.array_equal(gm, cm)
+    del torch

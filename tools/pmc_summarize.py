@@ -7,12 +7,12 @@ import os
 import sys
 
 
-def per_dispatch(path, counter):
+def per_dispatch(path, counter, kernel="k_decode<false, true,"):
     vals = {}
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name", "")
-            if "k_decode<false, true>" not in name or r.get("Counter_Name") != counter:
+            if kernel not in name or r.get("Counter_Name") != counter:
                 continue
             d = int(r["Dispatch_Id"])
             vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
@@ -28,6 +28,10 @@ def main():
     write = per_dispatch(os.path.join(out, "counters_WRITE_SIZE.csv"), "WRITE_SIZE")[-steps:]
     fb = 2 * 1024 * sum(fetch) / len(fetch)
     wb = 1024 * sum(write) / len(write)
+    # the standalone LF kernel: the last K k_lf dispatches (eager replay)
+    lf_fetch = per_dispatch(os.path.join(out, "counters_FETCH_SIZE.csv"), "FETCH_SIZE", "k_lf")[-steps:]
+    lf_write = per_dispatch(os.path.join(out, "counters_WRITE_SIZE.csv"), "WRITE_SIZE", "k_lf")[-steps:]
+    lfb = (2 * 1024 * sum(lf_fetch) / len(lf_fetch) + 1024 * sum(lf_write) / len(lf_write)) if lf_fetch else None
     res = {
         "kernel": "k_decode<false, true> (fused LF step + uint8 mask)",
         "corpus_tokens": bench["config"]["corpus_tokens"],
@@ -37,6 +41,8 @@ def main():
         "write_bytes_per_launch": wb,
         "k_decode_bytes_per_launch": fb + wb,
         "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+        "k_lf_bytes_per_launch": lfb,
+        "k_lf_alg_bytes_per_launch": bench["standalone_kernels"]["k_lf"]["alg_bytes_per_launch"],
         "correction": "bytes = 2*1024*FETCH_SIZE + 1024*WRITE_SIZE (MI355X_MICROARCH.md HBM: gfx950 FETCH_SIZE "
                       "counts half of wide coalesced reads; counters in KB)",
     }
