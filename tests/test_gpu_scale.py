@@ -35,6 +35,7 @@ def _build(n_tokens, seed, dev):
     from fmidx.fm_index import FMIndex, suffix_sort_device
     from fmidx.synth import markov_corpus_gpu
 
+    torch.cuda.empty_cache()   # blocks torch cached for earlier tests: the index is hipMalloc'd beside them
     text, _ = markov_corpus_gpu(n_tokens, V, seed, dev)
     bwt, _ = suffix_sort_device(text)
     fm = FMIndex(device=0)
