@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -57,6 +58,11 @@ void Index::release() {
   cache_tab = nullptr;
   cache_nodes = cache_bytes = 0;
   if (D2) (void)hipFree(D2);
+  for (void* p : {(void*)mark, (void*)mark_cnt, (void*)sa_samp, (void*)isa_samp})
+    if (p) (void)hipFree(p);
+  mark = mark_cnt = isa_samp = nullptr;
+  sa_samp = nullptr;
+  samp_bytes = 0;
   w2_Z = nullptr;
   D2 = nullptr;
   w2_bytes = 0;
@@ -238,38 +244,63 @@ int ws_release(fm_index* h, hipStream_t s) {
   return 0;
 }
 
-// Build from a host text T' (+ sentinel already appended) on the host, then
-// the device structures.
+// Above this many rows the reference's construction entry points
+// (initialize / initialize_from_file, fm_index.cpp:33-48) sort on the GPU.
+uint64_t gpu_sort_min() {
+  const char* e = std::getenv("FMIDX_GPU_SORT_MIN");
+  return (e && *e) ? std::strtoull(e, nullptr, 10) : (1ull << 20);
+}
+
+// Build from a host text T' (+ sentinel already appended): suffix array by
+// GPU prefix doubling (n >= gpu_sort_min(), n < 2^34) or host SA-IS, then
+// the device structures; the suffix array is reduced to its samples (locate /
+// extract by LF walks) and freed.
 int build_from_text(fm_index* h, std::vector<uint32_t>& text) {
   auto& x = h->idx;
   const uint64_t n = text.size();
-  uint32_t maxs = 0;
-  for (uint32_t v : text) maxs = std::max(maxs, v);
-  std::vector<uint64_t> sa64(n);
-  try {
-    if (n < (1ull << 31)) {
-      std::vector<int32_t> sa;
-      fmidx::suffix_array<int32_t>(text.data(), (int64_t)n, maxs + 1, sa);
-      for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
-    } else {
-      std::vector<int64_t> sa;
-      fmidx::suffix_array<int64_t>(text.data(), (int64_t)n, maxs + 1, sa);
-      for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
-    }
-  } catch (const std::exception& e) {
-    set_error("suffix sorting failed: %s", e.what());
-    return -1;
-  }
-  std::vector<uint32_t> bwt(n);
-  for (uint64_t i = 0; i < n; ++i) bwt[i] = text[sa64[i] == 0 ? n - 1 : sa64[i] - 1];
   x.release();
   FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
-  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
-  FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
-  FM_HIP(hipMemcpyAsync(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(x.sa, sa64.data(), n * 8, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipMemcpyAsync(x.text, text.data(), n * 4, hipMemcpyHostToDevice, x.stream));
-  FM_HIP(hipStreamSynchronize(x.stream));
+  uint64_t* d_sa = nullptr;
+  FM_HIP(hipMalloc(reinterpret_cast<void**>(&d_sa), n * 8));
+  if (n >= gpu_sort_min() && n < (1ull << 34)) {
+    uint32_t* d_text = nullptr;
+    FM_HIP(hipMalloc(reinterpret_cast<void**>(&d_text), n * 4));
+    FM_HIP(hipMemcpyAsync(d_text, text.data(), n * 4, hipMemcpyHostToDevice, x.stream));
+    const int rc = fmidx::gpu_suffix_sort(d_text, n, x.bwt, d_sa, x.stream);
+    (void)hipStreamSynchronize(x.stream);
+    (void)hipFree(d_text);
+    if (rc) {
+      (void)hipFree(d_sa);
+      return -1;
+    }
+  } else {
+    uint32_t maxs = 0;
+    for (uint32_t v : text) maxs = std::max(maxs, v);
+    std::vector<uint64_t> sa64(n);
+    try {
+      if (n < (1ull << 31)) {
+        std::vector<int32_t> sa;
+        fmidx::suffix_array<int32_t>(text.data(), (int64_t)n, maxs + 1, sa);
+        for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
+      } else {
+        std::vector<int64_t> sa;
+        fmidx::suffix_array<int64_t>(text.data(), (int64_t)n, maxs + 1, sa);
+        for (uint64_t i = 0; i < n; ++i) sa64[i] = (uint64_t)sa[i];
+      }
+    } catch (const std::exception& e) {
+      (void)hipFree(d_sa);
+      set_error("suffix sorting failed: %s", e.what());
+      return -1;
+    }
+    std::vector<uint32_t> bwt(n);
+    for (uint64_t i = 0; i < n; ++i) bwt[i] = text[sa64[i] == 0 ? n - 1 : sa64[i] - 1];
+    FM_HIP(hipMemcpyAsync(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice, x.stream));
+    FM_HIP(hipMemcpyAsync(d_sa, sa64.data(), n * 8, hipMemcpyHostToDevice, x.stream));
+    FM_HIP(hipStreamSynchronize(x.stream));
+  }
+  const int rc = fmidx::device_build_samples(&x, d_sa, n, x.stream);
+  (void)hipFree(d_sa);
+  if (rc) return -1;
   return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
 }
 
@@ -476,10 +507,10 @@ int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n
   FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
   FM_HIP(hipMemcpyAsync(x.bwt, d_bwt, n * 4, hipMemcpyDeviceToDevice, x.stream));
   if (d_sa) {
-    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
-    FM_HIP(hipMemcpyAsync(x.sa, d_sa, n * 8, hipMemcpyDeviceToDevice, x.stream));
-  }
-  if (d_text) {
+    // locate / extract from SA and ISA samples taken from the caller's SA
+    if (fmidx::device_build_samples(&x, d_sa, n, x.stream)) return -1;
+  } else if (d_text) {
+    // no suffix array: extract_text reads T' directly (locate unavailable)
     FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
     FM_HIP(hipMemcpyAsync(x.text, d_text, n * 4, hipMemcpyDeviceToDevice, x.stream));
   }
@@ -500,14 +531,17 @@ int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t
   FM_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
   x.release();
   FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
-  if (keep_sa_text) {
-    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8));
-    FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.text), n * 4));
-    FM_HIP(hipMemcpyAsync(x.text, d_text, n * 4, hipMemcpyDeviceToDevice, x.stream));
-  }
-  if (fmidx::gpu_suffix_sort(d_text, n, x.bwt, keep_sa_text ? x.sa : nullptr, x.stream)) {
+  uint64_t* d_sa = nullptr;
+  if (keep_sa_text) FM_HIP(hipMalloc(reinterpret_cast<void**>(&d_sa), n * 8));
+  if (fmidx::gpu_suffix_sort(d_text, n, x.bwt, d_sa, x.stream)) {
+    if (d_sa) (void)hipFree(d_sa);
     x.release();
     return -1;
+  }
+  if (d_sa) {
+    const int rc = fmidx::device_build_samples(&x, d_sa, n, x.stream);
+    (void)hipFree(d_sa);
+    if (rc) return -1;
   }
   return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
 }
@@ -673,12 +707,26 @@ int fm_locate(fm_index* h, uint64_t row, uint64_t* out) {
     *out = ~0ull;
     return 0;
   }
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (x.mark) {      // LF walk to the next SA sample (locate.hip)
+    Stage st;
+    const size_t o_row = st.add<uint64_t>(1), o_out = st.add<uint64_t>(1);
+    if (stage_reserve(h, st)) return -1;
+    *hstage_at<uint64_t>(h, o_row) = row;
+    if (stage_up(h, o_row, o_out)) return -1;
+    if (fmidx::launch_locate(x.view, x.samples(), stage_at<uint64_t>(h, o_row), 1, stage_at<uint64_t>(h, o_out),
+                             x.stream))
+      return -1;
+    if (stage_down(h, o_out, o_out + 8)) return -1;
+    FM_HIP(hipStreamSynchronize(x.stream));
+    *out = *hstage_at<uint64_t>(h, o_out);
+    return 0;
+  }
   if (!x.sa) {
     set_error("index built without a suffix array: locate unavailable");
     return -1;
   }
-  FM_GUARD(h);
-  std::lock_guard<std::mutex> lk(h->mu);
   FM_HIP(hipMemcpyAsync(out, x.sa + row, 8, hipMemcpyDeviceToHost, x.stream));
   FM_HIP(hipStreamSynchronize(x.stream));
   return 0;
@@ -697,19 +745,37 @@ int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, ui
               (unsigned long long)begin, (unsigned long long)end);
     return -3;
   }
-  if (!x.text) {
-    set_error("index built without text: extract_text unavailable");
+  if (!x.isa_samp && !x.text) {
+    set_error("index built without a suffix array or text: extract_text unavailable");
     return -1;
   }
   const uint64_t L = end - begin;
   *len = L;
   const uint64_t w = std::min(L, cap);
   if (w == 0) return 0;
-  // The LF walk from isa[end-1] emits T'[end-2], T'[end-3], ... cyclically:
-  // out[j] = T'[(end - 2 - j) mod n].  Read those rows of T' from HBM.
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   const uint64_t n = x.n;
+  if (x.isa_samp) {  // LF walk from isa[end - 1] (locate.hip), out[j] = T'[(end - 2 - j) mod n]
+    Stage st;
+    const size_t o_b = st.add<uint64_t>(1), o_e = st.add<uint64_t>(1), o_off = st.add<uint64_t>(2),
+                 o_out = st.add<uint64_t>(w);
+    if (stage_reserve(h, st)) return -1;
+    *hstage_at<uint64_t>(h, o_b) = begin;
+    *hstage_at<uint64_t>(h, o_e) = end;
+    hstage_at<uint64_t>(h, o_off)[0] = 0;
+    hstage_at<uint64_t>(h, o_off)[1] = w;
+    if (stage_up(h, 0, o_out)) return -1;
+    if (fmidx::launch_extract(x.view, x.samples(), stage_at<uint64_t>(h, o_b), stage_at<uint64_t>(h, o_e),
+                              stage_at<uint64_t>(h, o_off), 1, stage_at<uint64_t>(h, o_out), x.stream))
+      return -1;
+    if (stage_down(h, o_out, o_out + w * 8)) return -1;
+    FM_HIP(hipStreamSynchronize(x.stream));
+    std::memcpy(out, hstage_at<uint64_t>(h, o_out), w * 8);
+    stage_trim(h);
+    return 0;
+  }
+  // legacy: read T' (kept when the index was built without a suffix array)
   std::vector<uint32_t> seg;
   uint64_t j = 0;
   uint64_t pos = (end + n - 2) % n;          // position of out[0]
@@ -726,22 +792,32 @@ int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, ui
   return 0;
 }
 
+// File layout (little endian): magic "FMIDXAMD", u32 version (2), u32 flags,
+// u64 n, BWT (n x u32); flags & 4: SA samples = mark bits (ceil(n/64) x u64),
+// sa_samp (ceil(n/32) x u32), isa_samp ((n-1)/64 + 1 x u64); flags & 2: T'
+// (n x u32, indexes built without a suffix array).  Version 1 files (flags & 1:
+// the full SA) are read too; their SA is reduced to samples on load.
 int fm_save(fm_index* h, const char* path) {
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   auto& x = h->idx;
   const uint64_t n = x.n;
-  std::vector<uint32_t> bwt(n), text;
-  std::vector<uint64_t> sa;
+  const uint64_t nwords = (n + 63) / 64, nsamp = (n + fmidx::kSaRate - 1) / fmidx::kSaRate,
+                 nisa = (n - 1) / fmidx::kIsaRate + 1;
+  std::vector<uint32_t> bwt(n), text, samp;
+  std::vector<uint64_t> mark, isa;
   FM_HIP(hipMemcpy(bwt.data(), x.bwt, n * 4, hipMemcpyDeviceToHost));
   uint32_t flags = 0;
-  if (x.sa) {
-    sa.resize(n);
-    FM_HIP(hipMemcpy(sa.data(), x.sa, n * 8, hipMemcpyDeviceToHost));
-    flags |= 1;
-  }
-  if (x.text) {
+  if (x.mark) {
+    mark.resize(nwords);
+    samp.resize(nsamp);
+    isa.resize(nisa);
+    FM_HIP(hipMemcpy(mark.data(), x.mark, nwords * 8, hipMemcpyDeviceToHost));
+    FM_HIP(hipMemcpy(samp.data(), x.sa_samp, nsamp * 4, hipMemcpyDeviceToHost));
+    FM_HIP(hipMemcpy(isa.data(), x.isa_samp, nisa * 8, hipMemcpyDeviceToHost));
+    flags |= 4;
+  } else if (x.text) {
     text.resize(n);
     FM_HIP(hipMemcpy(text.data(), x.text, n * 4, hipMemcpyDeviceToHost));
     flags |= 2;
@@ -751,13 +827,17 @@ int fm_save(fm_index* h, const char* path) {
     set_error("cannot write %s", path);
     return -1;
   }
-  const uint32_t version = 1;
+  const uint32_t version = 2;
   f.write(kMagic, 8);
   f.write(reinterpret_cast<const char*>(&version), 4);
   f.write(reinterpret_cast<const char*>(&flags), 4);
   f.write(reinterpret_cast<const char*>(&n), 8);
   f.write(reinterpret_cast<const char*>(bwt.data()), n * 4);
-  if (flags & 1) f.write(reinterpret_cast<const char*>(sa.data()), n * 8);
+  if (flags & 4) {
+    f.write(reinterpret_cast<const char*>(mark.data()), nwords * 8);
+    f.write(reinterpret_cast<const char*>(samp.data()), nsamp * 4);
+    f.write(reinterpret_cast<const char*>(isa.data()), nisa * 8);
+  }
   if (flags & 2) f.write(reinterpret_cast<const char*>(text.data()), n * 4);
   if (!f) {
     set_error("write failed: %s", path);
@@ -779,16 +859,26 @@ int fm_load(fm_index** out, const char* path, int device) {
   f.read(reinterpret_cast<char*>(&version), 4);
   f.read(reinterpret_cast<char*>(&flags), 4);
   f.read(reinterpret_cast<char*>(&n), 8);
-  if (!f || std::memcmp(magic, kMagic, 8) != 0 || version != 1 || n == 0) {
+  if (!f || std::memcmp(magic, kMagic, 8) != 0 || (version != 1 && version != 2) || n == 0) {
     set_error("%s is not an fmidx index file", path);
     return -1;
   }
-  std::vector<uint32_t> bwt(n), text;
-  std::vector<uint64_t> sa;
+  const uint64_t nwords = (n + 63) / 64, nsamp = (n + fmidx::kSaRate - 1) / fmidx::kSaRate,
+                 nisa = (n - 1) / fmidx::kIsaRate + 1;
+  std::vector<uint32_t> bwt(n), text, samp;
+  std::vector<uint64_t> sa, mark, isa;
   f.read(reinterpret_cast<char*>(bwt.data()), n * 4);
-  if (flags & 1) {
+  if (version == 1 && (flags & 1)) {
     sa.resize(n);
     f.read(reinterpret_cast<char*>(sa.data()), n * 8);
+  }
+  if (version == 2 && (flags & 4)) {
+    mark.resize(nwords);
+    samp.resize(nsamp);
+    isa.resize(nisa);
+    f.read(reinterpret_cast<char*>(mark.data()), nwords * 8);
+    f.read(reinterpret_cast<char*>(samp.data()), nsamp * 4);
+    f.read(reinterpret_cast<char*>(isa.data()), nisa * 8);
   }
   if (flags & 2) {
     text.resize(n);
@@ -809,11 +899,25 @@ int fm_load(fm_index** out, const char* path, int device) {
     };
     if (hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4) != hipSuccess) return fail();
     if (hipMemcpy(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
-    if (flags & 1) {
-      if (hipMalloc(reinterpret_cast<void**>(&x.sa), n * 8) != hipSuccess) return fail();
-      if (hipMemcpy(x.sa, sa.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess) return fail();
+    if (!sa.empty()) {
+      uint64_t* d_sa = nullptr;
+      if (hipMalloc(reinterpret_cast<void**>(&d_sa), n * 8) != hipSuccess) return fail();
+      const bool ok = hipMemcpy(d_sa, sa.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+                      fmidx::device_build_samples(&x, d_sa, n, x.stream) == 0;
+      (void)hipFree(d_sa);
+      if (!ok) return fail();
+    } else if (!mark.empty()) {
+      if (hipMalloc(reinterpret_cast<void**>(&x.mark), nwords * 8) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&x.sa_samp), nsamp * 4) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&x.isa_samp), nisa * 8) != hipSuccess)
+        return fail();
+      if (hipMemcpy(x.mark, mark.data(), nwords * 8, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(x.sa_samp, samp.data(), nsamp * 4, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(x.isa_samp, isa.data(), nisa * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return fail();
+      if (fmidx::device_finish_samples(&x, n, x.stream)) return fail();
     }
-    if (flags & 2) {
+    if (!text.empty() && !x.isa_samp) {
       if (hipMalloc(reinterpret_cast<void**>(&x.text), n * 4) != hipSuccess) return fail();
       if (hipMemcpy(x.text, text.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
     }
@@ -883,6 +987,34 @@ int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, ui
   static_assert(sizeof(fm_row_params) == 32, "fm_row_params layout");
   return fmidx::launch_epilogue(dtype, d_scores, d_out, B, V, ld_scores, ld_out, d_bits, ld_bits,
                                 d_unigram_bits, d_rows, eos, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_locate_batch(fm_index* h, const uint64_t* d_rows, uint64_t m, uint64_t* d_out, void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_locate(h->idx.view, h->idx.samples(), d_rows, m, d_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_extract_batch(fm_index* h, const uint64_t* d_begin, const uint64_t* d_end, const uint64_t* d_off, uint64_t m,
+                     uint64_t* d_out, void* stream) {
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_extract(h->idx.view, h->idx.samples(), d_begin, d_end, d_off, m, d_out,
+                               reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, uint64_t* total_bytes) {
+  FM_CHECK_BUILT(h);
+  const auto& x = h->idx;
+  const uint64_t e = x.E ? x.n * 8 : 0;
+  const uint64_t K = (1ull << x.L) + 1;
+  if (e_bytes) *e_bytes = e;
+  if (sample_bytes) *sample_bytes = x.samp_bytes;
+  if (total_bytes)
+    *total_bytes = x.wm_bytes + x.n * 4 + x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0) +
+                   x.w2_bytes + e + x.cache_bytes + x.trans_bytes + x.samp_bytes + (x.sa ? x.n * 8 : 0) +
+                   (x.text ? x.n * 4 : 0) + 3 * K * 8;
+  return 0;
 }
 
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,

@@ -512,6 +512,18 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
 }
 
 // ---------------------------------------------------------------------------
+// suffix-array / inverse-suffix-array samples (locate.hip): text-order
+// sampling at sdsl csa_wt's default rates
+constexpr uint64_t kSaRate = 32;
+constexpr uint64_t kIsaRate = 64;
+struct SampleView {
+  const uint64_t* mark;       // n bits: SA[i] % kSaRate == 0
+  const uint64_t* mark_cnt;   // marked rows before each 512-row block
+  const uint32_t* sa_samp;    // SA[i] / kSaRate of the marked rows, row order
+  const uint64_t* isa_samp;   // row of text position kIsaRate * k
+};
+
+// ---------------------------------------------------------------------------
 // host-side owner of the device structures
 struct Index {
   int device = 0;
@@ -542,9 +554,15 @@ struct Index {
   uint32_t* cblock = nullptr;
   uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0, trans_dropped = 0, trans_bytes = 0;
   int64_t* D2 = nullptr;
-  uint64_t* sa = nullptr;
-  uint32_t* text = nullptr;
+  uint64_t* sa = nullptr;         // legacy (v1 files / no samples): full suffix array
+  uint32_t* text = nullptr;       // legacy: T' (extract without ISA samples)
+  uint64_t* mark = nullptr;       // SA / ISA samples (locate.hip)
+  uint64_t* mark_cnt = nullptr;
+  uint32_t* sa_samp = nullptr;
+  uint64_t* isa_samp = nullptr;
+  uint64_t samp_bytes = 0;
   uint64_t wm_bytes = 0, bm_bytes = 0, follow_bytes = 0, w2_bytes = 0;
+  SampleView samples() const { return SampleView{mark, mark_cnt, sa_samp, isa_samp}; }
   // grow-only workspace for batched traversals
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -559,6 +577,14 @@ int device_build_cache(Index* h, hipStream_t s);   // cache.hip
 int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
 int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s,
                        uint64_t* d_total);
+
+// locate.hip: samples from a device suffix array (uint64[n]); from loaded samples
+int device_build_samples(Index* h, const uint64_t* d_sa, uint64_t n, hipStream_t s);
+int device_finish_samples(Index* h, uint64_t n, hipStream_t s);
+int launch_locate(const DevView& v, const SampleView& sv, const uint64_t* rows, uint64_t m, uint64_t* out,
+                  hipStream_t s);
+int launch_extract(const DevView& v, const SampleView& sv, const uint64_t* begin, const uint64_t* end,
+                   const uint64_t* off, uint64_t m, uint64_t* out, hipStream_t s);
 
 // query.hip launchers
 int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,

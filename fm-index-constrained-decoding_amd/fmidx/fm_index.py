@@ -246,6 +246,10 @@ class FMIndex:
         check(lib().fm_stats_trans(self._h, *[byref(v) for v in tr]), "stats_trans")
         for k, v in zip(["trans_entries", "trans_dropped", "trans_bytes"], tr):
             out[k] = int(v.value)
+        mem = [c_uint64() for _ in range(3)]
+        check(lib().fm_stats_mem(self._h, *[byref(v) for v in mem]), "stats_mem")
+        for k, v in zip(["lf_e_bytes", "sample_bytes", "device_bytes"], mem):
+            out[k] = int(v.value)
         return out
 
     def cache_contains(self, lo, hi):
@@ -363,6 +367,49 @@ class FMIndex:
                                             c_void_p(k.data_ptr()), c_void_p(_stream_of(lo))),
               "distinct_count_batch")
         return syms, counts, k, cap_off
+
+    def locate_batch(self, rows):
+        """SA[row] for an int64 device tensor of rows (fm_index.cpp:168-172 for
+        all rows at once; UINT64_MAX -- as int64, -1 -- for rows >= size())."""
+        import torch
+
+        out = torch.empty(rows.numel(), dtype=torch.int64, device=rows.device)
+        check(lib().fm_locate_batch(self._h, c_void_p(rows.data_ptr()), rows.numel(), c_void_p(out.data_ptr()),
+                                    c_void_p(_stream_of(rows))), "locate_batch")
+        return out
+
+    def extract_batch(self, begins: Sequence[int], ends: Sequence[int]) -> List[Tuple[int, ...]]:
+        """extract_text (fm_index.cpp:174-194) of many (begin, end) pairs in one
+        launch; same results and clamping as ``extract_text`` (an empty tuple
+        when end <= begin)."""
+        import torch
+
+        n = self.size()
+        m = len(begins)
+        if m != len(ends):
+            raise ValueError("begins and ends differ in length")
+        b = [_u64(x, "extract_text", 2) for x in begins]
+        e = [_u64(x, "extract_text", 3) for x in ends]
+        lens = []
+        for x, y in zip(b, e):
+            if y <= x:
+                lens.append(0)
+                continue
+            if min(y, n) <= x:
+                raise FMIndexError(f"extract_text: begin {x} >= clamped end {min(y, n)} (unbounded in the reference)")
+            lens.append(min(y, n) - x)
+        if m == 0:
+            return []
+        dev = torch.device("cuda", self._device)
+        off = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
+        bt = torch.tensor(np.asarray(b, dtype=np.uint64).view(np.int64), device=dev)
+        et = torch.tensor(np.asarray(e, dtype=np.uint64).view(np.int64), device=dev)
+        out = torch.empty(max(1, int(off[-1])), dtype=torch.int64, device=dev)
+        check(lib().fm_extract_batch(self._h, c_void_p(bt.data_ptr()), c_void_p(et.data_ptr()), c_void_p(off.data_ptr()),
+                                     m, c_void_p(out.data_ptr()), c_void_p(_stream_of(bt))), "extract_batch")
+        flat = out.cpu().tolist()
+        o = off.cpu().tolist()
+        return [tuple(flat[o[i]:o[i + 1]]) for i in range(m)]
 
     def device_bwt_ptr(self) -> int:
         p = c_void_p()

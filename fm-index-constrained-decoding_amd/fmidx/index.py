@@ -32,16 +32,15 @@ SHIFT = 10                      # index.py:16
 def encode_corpus(sequences: Iterable[Sequence[int]]):
     """index.py:47-56 -> (T' as uint64 array, beginnings, occurring set)."""
     beginnings = [0]
-    occurring = set()
     parts = []
     for seq in sequences:
         a = np.asarray(list(seq) if not isinstance(seq, np.ndarray) else seq, dtype=np.int64)
         beginnings.append(beginnings[-1] + int(a.size))
-        occurring |= set(a.tolist())
         parts.append(a[::-1] + SHIFT)
     data = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
     if data.size and int(data.min()) < 0:
         raise OverflowError("token id below -SHIFT cannot be encoded")
+    occurring = set((np.unique(data) - SHIFT).tolist())    # the union of set(seq) (index.py:51)
     return data.astype(np.uint64), beginnings, occurring
 
 
@@ -108,9 +107,28 @@ class FMIndex(_FMIndex):
         return end - start
 
     def get_doc_indices(self, sequence: List[int]) -> Iterator[int]:
+        """index.py:123-129: the doc of every occurrence, in row order.  All rows
+        are located in one launch (fm_locate_batch) and mapped to docs by a
+        binary search of ``beginnings`` on the device."""
         start, end = self.get_range(sequence)
-        for row in range(start, end):
-            yield self.get_doc_index_from_row(row)
+        if end <= start:
+            return
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        beg = torch.tensor(self.beginnings, dtype=torch.int64, device=dev)
+        chunk = 1 << 20          # rows per launch: the generator stays lazy over huge ranges
+        for a in range(start, end, chunk):
+            rows = torch.arange(a, min(end, a + chunk), dtype=torch.int64, device=dev)
+            pos = self.locate_batch(rows)
+            docs = torch.searchsorted(beg, pos, right=True) - 1      # bisect_right - 1 (get_doc_index)
+            yield from docs.cpu().tolist()
+
+    def get_docs(self, doc_indices: Sequence[int]) -> List[List[int]]:
+        """get_doc (index.py:69-80) of many docs in one launch."""
+        b = [self.beginnings[d] for d in doc_indices]
+        e = [self.beginnings[d + 1] for d in doc_indices]
+        return [[x - SHIFT for x in doc] for doc in self.extract_batch(b, e)]
 
     def get_continuations(self, sequence: List[int]) -> List[int]:
         start, end = self.get_range(sequence)

@@ -138,16 +138,20 @@ int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offset
                        int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in,
                        uint64_t* lo_out, uint64_t* hi_out);
 
-/* FMIndex::locate(row) -- fm_index.cpp:168-172: SA[row]; UINT64_MAX if row >= n. */
+/* FMIndex::locate(row) -- fm_index.cpp:168-172: SA[row]; UINT64_MAX if row >= n.
+ * From suffix-array samples (every 32nd text position, as sdsl csa_wt's
+ * default): an LF walk of <= 31 steps on the GPU. */
 int fm_locate(fm_index* h, uint64_t row, uint64_t* out);
 
 /* FMIndex::extract_text(begin, end) -- fm_index.cpp:174-194 (LF walk from
- * isa[end-1], cyclic).  Writes min(len, cap) symbols; *len = true length. */
+ * isa[end-1], cyclic; isa from samples every 64 positions).  Writes
+ * min(len, cap) symbols; *len = true length. */
 int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, uint64_t cap,
                     uint64_t* len);
 
 /* FMIndex::save(path) / load_FMIndex(path) -- fm_index.cpp:196-209.  Own
- * little-endian binary format (sdsl's serialization is not reproduced). */
+ * little-endian binary format (sdsl's serialization is not reproduced):
+ * BWT + SA/ISA samples; everything else is rebuilt on load. */
 int fm_save(fm_index* h, const char* path);
 int fm_load(fm_index** out, const char* path, int device);
 
@@ -198,6 +202,18 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
                             const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
                             uint64_t* d_counts, uint64_t* d_k, void* stream);
 
+/* Batched locate (fm_index.cpp:168-172) for m device rows: d_out[i] =
+ * SA[d_rows[i]] (UINT64_MAX for rows >= n), one LF walk per row, all rows in
+ * parallel.  For get_doc_indices (index.py:123-129) over a whole range. */
+int fm_locate_batch(fm_index* h, const uint64_t* d_rows, uint64_t m, uint64_t* d_out, void* stream);
+
+/* Batched extract_text (fm_index.cpp:174-194): request i writes
+ * d_out[d_off[i] .. d_off[i+1]) = the first d_off[i+1] - d_off[i] symbols of
+ * extract_text(d_begin[i], d_end[i]) (the caller sizes d_off from the clamped
+ * lengths min(end, n) - begin).  For get_doc (index.py:69-80) of many docs. */
+int fm_extract_batch(fm_index* h, const uint64_t* d_begin, const uint64_t* d_end, const uint64_t* d_off,
+                     uint64_t m, uint64_t* d_out, void* stream);
+
 /* ---- fused logits-processor epilogue (no index needed) ------------------ */
 
 /* Per-row parameters of fm_apply_boosts (32 bytes, packed as declared). */
@@ -244,6 +260,10 @@ int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint
  * entries inserted, entries left out (probe window full; those steps take the
  * wavelet-matrix descent) and bytes in HBM. */
 int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes);
+
+/* Device memory of the index: the E array, the SA/ISA samples and the total
+ * of every device structure (bytes). */
+int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, uint64_t* total_bytes);
 
 /* For m device ranges, out[i] = 1 if [lo[i], hi[i]) has a cached bitmap
  * (accounting / tests; stream-ordered). */

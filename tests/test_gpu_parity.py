@@ -54,8 +54,15 @@ def markov_docs(seed, n_docs, vocab, max_len, sticky=0.7):
 
 
 # ---------------------------------------------------------------- golden
-def test_golden_index_cases(dev, golden_index_cases):
+@pytest.mark.parametrize("gpu_sort_min", [None, "1"])
+def test_golden_index_cases(dev, golden_index_cases, gpu_sort_min, monkeypatch):
+    """gpu_sort_min=1: FMIndex.initialize sorts every corpus on the GPU (the
+    path of corpora >= 2^20 tokens); locate / extract / get_doc go through the
+    SA / ISA samples and LF walks either way."""
     from fmidx.index import FMIndex
+
+    if gpu_sort_min is not None:
+        monkeypatch.setenv("FMIDX_GPU_SORT_MIN", gpu_sort_min)
 
     checked = 0
     for case in golden_index_cases:
@@ -339,6 +346,56 @@ def test_save_load_roundtrip(dev, tmp_path):
     assert b.occurring_distinct == a.occurring_distinct
     for d in range(len(docs)):
         assert b.get_doc(d) == a.get_doc(d)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    for r in range(b.size() + 1):             # every row from the saved SA samples, and one past the end
+        assert b.locate(r) == ora.locate(r)
+    assert b.get_docs(list(range(len(docs)))) == [ora.get_doc(d) for d in range(len(docs))]
+
+
+def test_initialize_docs_device_path_at_scale(dev):
+    """FMIndex.initialize (index.py:39-67 -> fm_initialize) of a 5e7-token
+    corpus: suffix sorting on the GPU, SA / ISA samples instead of a resident
+    suffix array.  locate (single and batched), get_docs and get_doc_indices
+    against the full suffix array and the text."""
+    import torch
+
+    from fmidx.fm_index import suffix_sort_device
+    from fmidx.index import FMIndex
+    from fmidx.synth import markov_corpus_gpu
+
+    text, beg = markov_corpus_gpu(50_000_000, 128256, 3, dev)
+    T = text.cpu().numpy().astype(np.int64)
+    Bg = beg.cpu().numpy()
+    docs = [T[Bg[d]:Bg[d + 1]][::-1] - 10 for d in range(Bg.size - 1)]     # the forward docs
+    idx = FMIndex(device=0)
+    idx.initialize(docs)
+    n = text.numel()
+    assert idx.size() == n and idx.beginnings == Bg.tolist()
+    st = idx.stats()
+    assert 0 < st["sample_bytes"] < n * 2          # samples, not an 8n-byte suffix array
+    _, sa = suffix_sort_device(text, want_sa=True)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    rows = torch.cat([torch.randint(0, n, (200000,), generator=g, device=dev),
+                      torch.tensor([0, 1, n - 2, n - 1], device=dev)])
+    assert torch.equal(idx.locate_batch(rows), sa[rows])
+    assert int(idx.locate_batch(torch.tensor([n, n + 5], device=dev))[0]) == -1   # UINT64_MAX
+    for r in rows[:20].tolist():
+        assert idx.locate(r) == int(sa[r])
+    pick = np.random.default_rng(2).choice(Bg.size - 1, size=300, replace=False).tolist() + [0, Bg.size - 2]
+    for d, got in zip(pick, idx.get_docs(pick)):
+        e = int(Bg[d + 1])                     # get_doc(d): T'[(end - 2 - j) mod n] - SHIFT, j < len(d)
+        want = [int(T[(e - 2 - j) % n]) - 10 for j in range(len(docs[d]))]
+        assert got == want, d
+    assert idx.get_doc(pick[0]) == idx.get_docs(pick[:1])[0]
+    F = T[:-1][::-1]
+    pat = F[123456:123459].tolist()
+    pat = [t - 10 for t in pat]
+    lo, hi = idx.get_range(pat)
+    assert hi > lo
+    want = (np.searchsorted(Bg, sa[lo:hi].cpu().numpy(), side="right") - 1).tolist()
+    assert list(idx.get_doc_indices(pat)) == want
 
 
 def test_properties_at_scale(dev):

@@ -121,12 +121,42 @@ def test_c3_decode_b2048_vs_cpu_ref(dev, c3):
     assert ((w > 512) & (w <= 4096)).any()
 
 
+def _follow_scan(body, a, b=None, chunk=1 << 28):
+    """Brute force over the text, in chunks (no index): the occurrences of
+    [a] -- or of [a, b] -- in F and the set of tokens that follow them.  In T'
+    coordinates (index.py:47-53) an occurrence of [a] at T'[j] (j >= 1) is
+    followed in F by T'[j - 1]; of [a, b] at T'[j] = b, T'[j + 1] = a; an
+    occurrence at j = 0 is followed by the sentinel (filtered)."""
+    import torch
+
+    n1 = body.numel()
+    seen = torch.zeros(V + SHIFT, dtype=torch.bool, device=body.device)
+    count = 0
+    for j0 in range(0, n1, chunk):
+        j1 = min(n1, j0 + chunk)
+        x = body[j0:j1]
+        hit = x == (a if b is None else b)
+        if b is not None:
+            nxt = body[j0 + 1:j1 + 1]
+            hit[: nxt.numel()] &= nxt == a
+            if nxt.numel() < hit.numel():
+                hit[nxt.numel():] = False
+        count += int(hit.sum())
+        if j0 == 0:
+            hit[0] = False          # followed by the sentinel
+        if j0 > 0:
+            prev = body[j0 - 1:j1 - 1]
+        else:
+            prev = torch.cat([body[:1], body[: j1 - 1]])
+        seen[prev[hit].to(torch.int64)] = True
+    want = seen[SHIFT:].cpu().numpy().astype(np.uint8)
+    return count, want
+
+
 @pytest.mark.timeout(900)
 def test_c3_ngrams_vs_brute_force(dev, c3):
     """1- and 2-token patterns: the allowed set == the tokens that follow
-    every occurrence in F, found by scanning the text (no index involved).
-    In T' coordinates (index.py:47-53) an occurrence of [a] at T'[j] (j >= 1)
-    is followed in F by T'[j - 1]; of [a, b] at T'[j] = b, T'[j + 1] = a."""
+    every occurrence in F, found by scanning the text (no index involved)."""
     import torch
 
     fm, text = c3["fm"], c3["text"]
@@ -134,14 +164,13 @@ def test_c3_ngrams_vs_brute_force(dev, c3):
     body = text[:-1]
     g = torch.Generator(device=dev)
     g.manual_seed(5)
-    picks = body[torch.randint(1, n - 3, (6,), generator=g, device=dev)].tolist()
+    pos = torch.randint(1, n - 3, (6,), generator=g, device=dev)
+    picks = body[pos].tolist()
     pats = []
     for j, a in enumerate(picks):
         pats.append([a - SHIFT])
-        if j < 4:   # a true bigram of F: a then the token after one of its occurrences
-            occ = torch.nonzero(body[1:] == a).squeeze(1) + 1
-            nxt = int(body[occ[len(occ) // 2] - 1])
-            pats.append([a - SHIFT, nxt - SHIFT])
+        if j < 4:   # a true bigram of F: a, then the token after that occurrence (T'[pos - 1])
+            pats.append([a - SHIFT, int(body[pos[j] - 1]) - SHIFT])
     pats.append([int(torch.argmax(torch.bincount(body[: 1 << 24], minlength=V + SHIFT))) - SHIFT])  # most frequent
     m = len(pats)
     offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), device=dev)
@@ -151,17 +180,8 @@ def test_c3_ngrams_vs_brute_force(dev, c3):
     fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
     got = fm.allowed_mask(lo, hi, V, SHIFT).cpu().numpy()
     for i, p in enumerate(pats):
-        a = p[0] + SHIFT
-        if len(p) == 1:
-            hit = torch.nonzero(body[1:] == a).squeeze(1) + 1
-        else:
-            b = p[1] + SHIFT
-            hit = torch.nonzero((body[1:-1] == b) & (body[2:] == a)).squeeze(1) + 1
-        want = np.zeros(V, dtype=np.uint8)
-        want[(body[hit - 1].to(torch.int64) - SHIFT).unique().cpu().numpy()] = 1
-        # sentinel: an occurrence at T'[0] is followed by the sentinel (filtered)
-        assert int(hi[i] - lo[i]) == len(hit) + int(body[0] == a if len(p) == 1 else
-                                                    (body[0] == p[1] + SHIFT and body[1] == a)), p
+        cnt, want = _follow_scan(body, p[0] + SHIFT, None if len(p) == 1 else p[1] + SHIFT)
+        assert int(hi[i] - lo[i]) == cnt, (p, int(hi[i] - lo[i]), cnt)
         assert np.array_equal(got[i], want), p
     # the fused decode step from the full range gives the 1-gram masks too
     one = [i for i, p in enumerate(pats) if len(p) == 1]
