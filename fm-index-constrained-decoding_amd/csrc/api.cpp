@@ -1057,6 +1057,12 @@ int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
   return fmidx::launch_cache_probe(h->idx.view, d_lo, d_hi, m, d_out, reinterpret_cast<hipStream_t>(stream));
 }
 
+int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
+               uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream) {
+  return fmidx::launch_or_bits(d_parts, nparts, part_stride, B, words_per_row, vocab, d_out, ld_out, unpack,
+                               reinterpret_cast<hipStream_t>(stream));
+}
+
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream) {
   return fmidx::launch_probe_gather(d_buf, bytes, chase, loads, threads, d_sink,

@@ -616,6 +616,10 @@ size_t distinct_ws_bytes(uint64_t total_cap);
 int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64_t* syms, const uint64_t* counts,
                         uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s);
 
+// shard.hip: OR of the shards' packed allowed rows (+ expansion to uint8)
+int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t wpr,
+                   uint64_t vocab, void* out, uint64_t ld_out, int unpack, hipStream_t s);
+
 // probe.hip (bench roofline): random 64-B gathers / dependent chase
 int launch_probe_gather(const void* buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads_or_chains,
                         uint64_t* sink, hipStream_t s);

@@ -124,6 +124,8 @@ class ShardedDecoder:
         self._buf = None
         self._plen = None      # per-row pattern length (device)
         self._bound = 0        # host upper bound of max(_plen)
+        self._parts = None     # gathered packed rows of every rank (device path)
+        self._out = None
 
     def _check_halo(self):
         """Exactness needs every pattern to be at most halo - 1 tokens.  The
@@ -201,10 +203,20 @@ class ShardedDecoder:
         if self.reduce == "max_u8":
             dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
             return m
-        # bit-pack (8 tokens per byte) unless the kernel already did, all-gather, OR locally, unpack.
+        world = dist.get_world_size(self.group)
+        if m.is_cuda and packed:
+            # device path: one all_gather of the kernel's own int32 rows into a
+            # [world, B, W] buffer, then ONE fused OR + unpack pass (fm_or_bits)
+            B, W = m.shape
+            if self._parts is None or self._parts.shape != (world, B, W):
+                self._parts = torch.empty((world, B, W), dtype=torch.int32, device=m.device)
+                self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=m.device)
+            dist.all_gather_into_tensor(self._parts, m, group=self.group)
+            or_bits(self._parts, self.vocab, out=self._out)
+            return self._out
+        # host tensors (gloo, CPU tests): the same exchange with torch ops.
         # int32 words in little-endian bit order are, byte for byte, pack_bits' layout.
         pk = m if packed else pack_bits(m)
-        world = dist.get_world_size(self.group)
         parts = [torch.empty_like(pk) for _ in range(world)]
         dist.all_gather(parts, pk, group=self.group)
         acc = parts[0].clone()
@@ -213,6 +225,27 @@ class ShardedDecoder:
         if packed:
             acc = acc.view(torch.uint8)
         return unpack_bits(acc, self.vocab)
+
+
+def or_bits(parts, vocab: int, out=None, unpack: bool = True):
+    """OR of the shards' bit-packed allowed rows (fm_or_bits, csrc/shard.hip):
+    ``parts`` int32 [P, B, W] on the GPU -> uint8 [B, vocab] (unpack) or the
+    ORed int32 [B, W] words."""
+    import torch
+    from ctypes import c_void_p
+
+    from ._lib import check, lib
+
+    P, B, W = parts.shape
+    assert parts.is_cuda and parts.dtype == torch.int32 and parts.is_contiguous()
+    if out is None:
+        out = (torch.empty((B, vocab), dtype=torch.uint8, device=parts.device) if unpack
+               else torch.empty((B, W), dtype=torch.int32, device=parts.device))
+    ld = out.stride(0) * out.element_size()
+    stream = torch.cuda.current_stream(parts.device).cuda_stream
+    check(lib().fm_or_bits(c_void_p(parts.data_ptr()), P, B * W, B, W, vocab, c_void_p(out.data_ptr()), ld,
+                           1 if unpack else 0, c_void_p(stream)), "or_bits")
+    return out
 
 
 def pack_bits(mask_u8):
@@ -239,4 +272,4 @@ def unpack_bits(packed, vocab: int):
 
 
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
-           "pack_bits", "unpack_bits"]
+           "or_bits", "pack_bits", "unpack_bits"]

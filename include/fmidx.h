@@ -243,6 +243,17 @@ int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, ui
                     const uint32_t* d_unigram_bits, const fm_row_params* d_rows, int64_t eos,
                     void* stream);
 
+/* ---- doc-range sharding (no index needed) ------------------- */
+
+/* The exchange step of a sharded decode: OR of the bit-packed allowed rows of
+ * ``nparts`` shards (block p = d_parts + p * part_stride words, B rows of
+ * words_per_row uint32, fm_allowed_mask_batch(packed=1)'s bit order -- what an
+ * RCCL all_gather of every rank's decode-step output holds).  unpack != 0
+ * writes the uint8 [B, vocab] 0/1 mask (ld_out bytes per row); 0 the ORed
+ * words (ld_out bytes per row, a multiple of 4).  Stream-ordered. */
+int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
+               uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream);
+
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
 /* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip

@@ -1,6 +1,8 @@
 """Where does a decode step's time go?  Loads the diagnostic library
 (libfmidx_stamps.so), replays trace steps one launch at a time and prints
-per-workgroup phase durations (s_memrealtime, 10 ns ticks)."""
+per-workgroup phase durations (s_memrealtime, 10 ns ticks).  COLD=1 evicts
+the caches (1 GiB read-modify-write) before every stamped launch instead of
+running the step once unstamped first (warm)."""
 import ctypes
 import os
 import sys
@@ -12,15 +14,19 @@ sys.path[:0] = [REPO, PKG]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from bench import SHIFT, build_index, make_trace  # noqa: E402
+from bench import SHIFT, build_index  # noqa: E402
 from fmidx._lib import lib  # noqa: E402
+from fmidx.synth import decode_trace  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
 V, B, W = 128256, 256, 5
 fm, text, bwt, _ = build_index(int(float(os.environ.get("TOKENS", "4.5e9"))), V, 20250905, dev)
 n = bwt.numel()
-tokens, init, lo_hist, hi_hist = make_trace(fm, text, bwt, B, V, W + 12, 20250905, dev)
+tokens, init, lo_hist, hi_hist, _ = decode_trace(fm, text, bwt, B, V, W + 12, 20250905, dev)
+del text
+COLD = os.environ.get("COLD", "0") != "0"
+flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
 dl = lib()
 dl.fm_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
@@ -39,7 +45,10 @@ names = ["lohi", "lf", "plan+bar", "stream", "(w15arr-s4)", "bar2", "emit"]
 summary = []
 for s in range(W, W + 12):
     lo_i, hi_i = lo_hist[s - 1].clone(), hi_hist[s - 1].clone()
-    fm.decode_step(tokens[s], lo_i, hi_i, mask, V, SHIFT, reset_below=0, lo_out=lo_o, hi_out=hi_o)  # warm
+    if COLD:
+        flush.add_(1)
+    else:
+        fm.decode_step(tokens[s], lo_i, hi_i, mask, V, SHIFT, reset_below=0, lo_out=lo_o, hi_out=hi_o)  # warm
     torch.cuda.synchronize()
     stamps.zero_()
     dl.fm_debug_set_stamps(fm._h, ctypes.c_void_p(stamps.data_ptr()))
