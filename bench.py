@@ -269,6 +269,97 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, seconds, d
 
 
 # ---------------------------------------------------------------------------
+def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, halo=128):
+    """Doc-range sharded decode, measured after the
+    replica run at N > 1.  The trace (tokens + initial patterns) and the
+    reference masks of its last step come from the replica (unsharded) index;
+    then every rank indexes its doc range + halo (one slice of T', built on the
+    device), decodes all B rows against it into bit-packed rows, and a step is:
+    fused LF + packed mask (fm_decode_step_batch) + RCCL all_gather of the
+    packed rows + one fused OR/unpack pass (fm_or_bits) to the uint8 [B, V]
+    mask of the whole corpus.  The last step's mask must equal the replica's."""
+    import torch.distributed as dist
+
+    from fmidx.sharding import or_bits, shard_text_device
+
+    fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
+    text, beg = markov_corpus_gpu(n_tokens, V, text_seed, dev)
+    S = W + K
+    tokens, _, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S, 777, dev)
+    del bwt
+    ref = fm.allowed_mask(lo_hist[S - 1], hi_hist[S - 1], V, SHIFT)   # unsharded masks of the last step
+    del fm
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    t0 = time.time()
+    ix, err = None, ""
+    try:
+        shard, (a, b) = shard_text_device(text, beg, world, rank, halo)
+        del text
+        torch.cuda.empty_cache()
+        ix = FMIndex(device=dev.index)
+        ix.initialize_from_text_device(shard)
+        del shard
+        torch.cuda.synchronize()
+    except Exception as e:   # every rank learns of it below: no rank is left waiting in a collective
+        err = repr(e)
+    build_s = time.time() - t0
+    ok_all = torch.tensor([0 if err else 1], device=dev)
+    dist.all_reduce(ok_all, op=dist.ReduceOp.MIN)
+    if not int(ok_all.item()):
+        raise RuntimeError(f"shard build failed on some rank ({err or 'another rank'})")
+    lens = [len(p) for p in pats0]
+    assert max(lens) + S <= halo - 1, "trace patterns would outgrow the halo"
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
+    toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
+    lo = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi = torch.zeros(B, dtype=torch.int64, device=dev)
+    ix.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    Wd = (V + 31) // 32
+    mine = torch.empty((B, Wd), dtype=torch.int32, device=dev)
+    parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
+    out = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+
+    def step(i, k):
+        src, dst = bufs[k % 2], bufs[(k + 1) % 2]
+        ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1],
+                       packed=True)
+        dist.all_gather_into_tensor(parts, mine)
+        or_bits(parts, V, out=out)
+
+    for i in range(W):
+        step(i, i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    a_ev = torch.cuda.Event(enable_timing=True)
+    b_ev = torch.cuda.Event(enable_timing=True)
+    a_ev.record()
+    for i in range(W, S):
+        step(i, i)
+    b_ev.record()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    ms = a_ev.elapsed_time(b_ev) / K
+    t = torch.tensor([ms], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item())
+    exact = bool(torch.equal(out, ref))
+    ok = torch.tensor([1 if exact else 0], device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    st = ix.stats()
+    return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": B * K / (ms / 1e3),
+            "unit": "masks/s", "ms_per_step": ms, "scaling": "strong", "shards": world, "halo": halo,
+            "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": st["bwt_bytes"] // 4,
+            "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
+            "masks_equal_unsharded": bool(ok.item()),
+            "step": "fused LF + packed mask, RCCL all_gather of packed rows (4 B x ceil(V/32) per row), "
+                    "fused OR + unpack (fm_or_bits) to uint8 [B, V]; eager launches"}
+
+
+# ---------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,6 +373,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=400)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the gather-ceiling probe")
+    ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the doc-range sharded leg")
+    ap.add_argument("--sharded-at-1", action="store_true",
+                    help="run the sharded leg at N = 1 too (one shard; exercises the path on a one-GPU box)")
     ap.add_argument("--packed", action="store_true",
                     help="bit-packed masks (uint32[B, ceil(V/32)]) instead of uint8[B, V] (not the headline)")
     ap.add_argument("--dump-trace", default="", help="write the timed trace states to this .npz")
@@ -556,6 +650,22 @@ def main():
                                                   args.cpu_seconds, dev)
         except Exception as e:  # the GPU line must still print
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if (world > 1 and not args.no_sharded) or args.sharded_at_1:
+        if world == 1:
+            import torch.distributed as dist
+
+            if not dist.is_initialized():
+                dist.init_process_group("nccl", device_id=dev, init_method="tcp://127.0.0.1:29533",
+                                        world_size=1, rank=0)
+        holder = [bwt, fm]
+        del bwt, fm
+        torch.cuda.empty_cache()
+        try:
+            result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, B, K, W, world, rank, dev)
+            log(f"sharded: {result['sharded']['value'] / 1e6:.2f} M masks/s, "
+                f"{result['sharded']['ms_per_step'] * 1e3:.1f} us/step, exact {result['sharded']['masks_equal_unsharded']}")
+        except Exception as e:  # the replica line must still print
+            result["sharded"] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

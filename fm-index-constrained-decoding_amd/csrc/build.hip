@@ -593,6 +593,7 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   v.bm_words = words;
   v.bm_levels = bm_levels;
   v.bm_log2 = log2b0;
+  v.probe_first = env_u32("FMIDX_PROBE_FIRST", 0) != 0;
   // -- follow-set bitmaps (one per symbol's C-block), built with the mask
   //    kernel itself once the view above is complete
   // (off by default: the range-bitmap cache below holds every C-block of

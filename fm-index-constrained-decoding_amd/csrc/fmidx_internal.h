@@ -104,6 +104,8 @@ struct DevView {
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
+  uint32_t probe_first;       // 1: a cached range's LF step waits for its transition probe before
+                              //    issuing the descent (a hit needs no rank loads); 0: issued together
 #ifdef FMIDX_STAMPS
   uint64_t* stamps;           // diagnostic build only: per-workgroup phase timestamps
 #endif
@@ -161,7 +163,7 @@ struct DevView {
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
                  "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
-                 "s"((v).trans_cap), "s"((v).cblock));                                                                     \
+                 "s"((v).trans_cap), "s"((v).cblock), "s"((v).probe_first));                                               \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -470,6 +472,23 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     if (slot >= v.trans_cap) slot -= v.trans_cap;
     tw = v.trans_tab[3 * slot + lane % 3];
   }
+  if (probe && v.probe_first) {   // the probe alone: one round trip of 384 B for a hit
+    const uint64_t w1n = __shfl_down(tw, 1, 64);
+    const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
+    if (bh) {
+      const int src = __ffsll((long long)bh) - 1;
+      const uint64_t w1 = __shfl(tw, src + 1, 64), w2 = __shfl(tw, src + 2, 64);
+      const uint64_t clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
+      const uint64_t aux = w2 >> 38;
+      lo = clo;
+      hi = clo + ((w2 >> 4) & kMask34);
+      if (aux & kTransOne)
+        one = (int64_t)(aux & (kTransOne - 1));
+      else if (aux)
+        cbm = v.cache_bm + (aux - 1) * v.bm_words;
+      return;
+    }
+  }
   // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
   uint64_t z[kW2MaxLevels];
@@ -481,7 +500,7 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   for (int l = 0; l < (int)v.NL2; ++l) {
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
     const uint64_t r = rank_w2(v.w2[l], pos, d, q);
-    if (l == 0 && probe) {   // the probe's loads were issued before this level's
+    if (l == 0 && probe && !v.probe_first) {   // the probe's loads were issued before this level's
       const uint64_t w1n = __shfl_down(tw, 1, 64);
       const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
       if (bh) {

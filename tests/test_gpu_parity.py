@@ -624,3 +624,59 @@ def test_distinct_workspace_across_streams(dev):
             for j in range(int(k[i])):
                 got += [int(syms[s0 + j]), int(counts[s0 + j])]
             assert tuple(got) == ora.distinct_count(int(a[i]), int(b[i])), (it, i)
+
+
+def test_sharded_decode_at_scale_one_gpu(dev):
+    """Doc-range sharding at 1e8 tokens on one GPU, in process: three shards
+    built on the device (shard_text_device: one slice of T' each), every row
+    decoded against every shard into bit-packed rows, ORed by fm_or_bits --
+    equal, step by step, to the unsharded index's uint8 masks.  The same
+    shards through ShardedDecoder (uint8 rows, OR on the host side of the
+    test) agree too."""
+    import torch
+
+    from fmidx.fm_index import FMIndex, suffix_sort_device
+    from fmidx.sharding import ShardedDecoder, or_bits, shard_text_device
+    from fmidx.synth import decode_trace, markov_corpus_gpu
+
+    V, B, S, H = 128256, 64, 6, 64
+    text, beg = markov_corpus_gpu(100_000_000, V, 13, dev)
+    bwt, _ = suffix_sort_device(text)
+    full = FMIndex(device=0)
+    full.initialize_from_bwt_device(bwt)
+    tokens, init, lo_hist, hi_hist, pats0 = decode_trace(full, text, bwt, B, V, S, 99, dev)
+    del bwt
+    assert max(len(p) for p in pats0) + S <= H - 1
+    shards = []
+    for r in range(3):
+        t_r, _ = shard_text_device(text, beg, 3, r, H)
+        ix = FMIndex(device=0)
+        ix.initialize_from_text_device(t_r)
+        shards.append(ix)
+    decs = [ShardedDecoder(ix, V, 10, halo=H) for ix in shards]
+    starts = [d.start(pats0, dev) for d in decs]
+    want0 = full.allowed_mask(init[0], init[1], V, 10)
+    assert torch.equal(starts[0] | starts[1] | starts[2], want0)
+    Wd = (V + 31) // 32
+    st = []
+    for ix in shards:
+        lo = torch.zeros(B, dtype=torch.int64, device=dev)
+        hi = torch.zeros(B, dtype=torch.int64, device=dev)
+        offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats0])]), device=dev)
+        toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
+        ix.backward_search_batch(toks, offs, 10, lo, hi)
+        st.append((lo, hi))
+    parts = torch.empty((3, B, Wd), dtype=torch.int32, device=dev)
+    for s in range(S):
+        for r, ix in enumerate(shards):
+            lo2, hi2 = torch.empty_like(st[r][0]), torch.empty_like(st[r][1])
+            ix.decode_step(tokens[s], st[r][0], st[r][1], parts[r], V, 10, reset_below=0, lo_out=lo2, hi_out=hi2,
+                           packed=True)
+            st[r] = (lo2, hi2)
+        got = or_bits(parts, V)
+        want = full.allowed_mask(lo_hist[s], hi_hist[s], V, 10)
+        assert torch.equal(got, want), s
+        ms = [d.step(tokens[s]) for d in decs]
+        assert torch.equal(ms[0] | ms[1] | ms[2], want), s
+    packed_or = or_bits(parts, V, unpack=False)
+    assert torch.equal(packed_or, parts[0] | parts[1] | parts[2])
