@@ -164,6 +164,7 @@ def decode_trace(fm, text: torch.Tensor, bwt: torch.Tensor, B: int, V: int, S: i
     off_h = offs.cpu().tolist()
     pats = [tok_h[off_h[b]:off_h[b + 1]] for b in range(B)]
     pats[0] = []
+    pats[1].append(V + 1000)     # the eos row: an unknown id ends its pattern, as its (0, 0) state says
     tokens = torch.empty((S, B), dtype=torch.int64, device=device)
     lo_hist = torch.empty((S, B), dtype=torch.int64, device=device)
     hi_hist = torch.empty((S, B), dtype=torch.int64, device=device)
