@@ -86,6 +86,15 @@ void Index::release() {
 
 }  // namespace fmidx
 
+namespace fmidx {
+// process.hip
+int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int64_t* ids, uint64_t B, uint64_t L,
+                          uint64_t ld, const int64_t* fdf, uint64_t fdf_len, const float* pow_tab, uint64_t pow_len,
+                          const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
+                          fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
+                          hipStream_t s);
+}  // namespace fmidx
+
 using fmidx::set_error;
 
 struct fm_index {
@@ -1055,6 +1064,23 @@ int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_cache_probe(h->idx.view, d_lo, d_hi, m, d_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_ids, uint64_t B, uint64_t L,
+                      uint64_t ld_ids, const int64_t* d_fdf, uint64_t fdf_len, const float* d_pow, uint64_t pow_len,
+                      const int64_t* d_prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* d_prev_state,
+                      fm_row_params* d_rows, uint64_t* d_mask_lo, uint64_t* d_mask_hi, int64_t* d_state,
+                      uint32_t* d_status, void* stream) {
+  static_assert(sizeof(fm_prep_config) == 192, "fm_prep_config layout");
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  if (!cfg) {
+    set_error("null config");
+    return -1;
+  }
+  return fmidx::launch_processor_step(h->idx.view, *cfg, d_ids, B, L, ld_ids, d_fdf, fdf_len, d_pow, pow_len,
+                                      d_prev_ids, prev_ld, prev_B, d_prev_state, d_rows, d_mask_lo, d_mask_hi,
+                                      d_state, d_status, reinterpret_cast<hipStream_t>(stream));
 }
 
 int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,

@@ -25,7 +25,8 @@ from __future__ import annotations
 
 import ctypes
 import functools
-from ctypes import c_void_p
+import math
+from ctypes import c_float, c_int32, c_int64, c_uint32, c_void_p
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -48,6 +49,105 @@ def _round(x, dtype) -> float:
     t = torch.zeros(1, dtype=dtype)
     t[0] = x
     return float(t[0])
+
+
+class _PrepConfig(ctypes.Structure):
+    """fm_prep_config (include/fmidx.h)."""
+    _fields_ = [("marker", c_int64 * 8), ("think", c_int64 * 2), ("sys", c_int64 * 4), ("eos", c_int64),
+                ("pad", c_int64), ("stop_at_count", c_int64), ("min_new_tokens", c_int64), ("forced_bos", c_int64),
+                ("shift", c_int64), ("marker_len", c_int32), ("num_beams", c_int32), ("flags", c_uint32),
+                ("base", c_float), ("v_uni_full", c_float), ("v_uni_half", c_float), ("v_forced", c_float),
+                ("reserved", c_int32)]
+
+
+assert ctypes.sizeof(_PrepConfig) == 192
+PREP_THINK, PREP_SKIP_FIRST, PREP_EOS, PREP_EOS_ALL, PREP_UNI_HALF = 1, 2, 4, 8, 16
+
+
+def _boost_table(boost: float, lrf: float, dtype, n: int) -> List[float]:
+    """BOOST * lrf ** k (the reference's Python float arithmetic, k < n)
+    rounded like an index-put into ``dtype``; NaN where ``lrf ** k`` is not a
+    finite Python float (the reference raises OverflowError there: such rows
+    take the host path, which raises the same)."""
+    out = []
+    for k in range(n):
+        try:
+            out.append(_round(boost * (lrf ** k), dtype))
+        except OverflowError:
+            out.append(math.nan)
+    return out
+
+
+class _DeviceStep:
+    """One soft-processor call on the device: fm_processor_step (per-row
+    bookkeeping + pattern ranges, csrc/process.hip), the packed allowed bits of
+    the rows that need them, the fused epilogue.  Keeps the previous call's
+    input_ids and per-row (pattern, range) state on the device so a row whose
+    pattern grew by one token costs ONE LF step.  Returns None when a row does
+    not have exactly one end marker at a common position (or a boost overflows):
+    the caller then runs the host path, which reproduces the reference's
+    behaviour for such inputs."""
+
+    def __init__(self, core: "_BatchedCore", boost: float, lrf: float, fdf: Optional[List[int]]):
+        self.core = core
+        self.index = core.index
+        self.dev = torch.device("cuda", self.index.device)
+        self.boost = boost
+        self.lrf = lrf
+        self.fdf = torch.tensor(list(fdf or []) + [0], dtype=torch.int64, device=self.dev)
+        self.fdf_len = len(fdf or [])
+        self._pow = {}
+        self.prev_ids = None          # device [B, Lcap] of the last call
+        self.prev_state = None
+        self.prev_B = 0
+        self.status = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self.status_h = torch.zeros(4, dtype=torch.int32).pin_memory()
+
+    def _pow_table(self, dtype, need: int):
+        t = self._pow.get(dtype)
+        if t is None or t.numel() < need:
+            n = max(need, 2 * (t.numel() if t is not None else 256))
+            t = torch.tensor(_boost_table(self.boost, self.lrf, dtype, n), dtype=torch.float32, device=self.dev)
+            self._pow[dtype] = t
+        return t
+
+    def __call__(self, input_ids, scores, cfg: _PrepConfig):
+        dev = self.dev
+        ids = input_ids.to(dev, torch.int64).contiguous()
+        if ids.dim() != 2:
+            return None
+        B, Lt = ids.shape
+        if B != scores.shape[0] or B % max(1, cfg.num_beams):
+            return None
+        V = scores.shape[1]
+        pow_t = self._pow_table(scores.dtype, Lt + 1)
+        rows = torch.empty(B * ROW_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        mlo = torch.empty(B, dtype=torch.int64, device=dev)
+        mhi = torch.empty(B, dtype=torch.int64, device=dev)
+        state = torch.empty((4, B), dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        prev = self.prev_ids
+        with torch.cuda.device(dev):
+            check(lib().fm_processor_step(
+                self.index._h, ctypes.byref(cfg), c_void_p(ids.data_ptr()), B, Lt, Lt,
+                c_void_p(self.fdf.data_ptr()), self.fdf_len, c_void_p(pow_t.data_ptr()), pow_t.numel(),
+                c_void_p(prev.data_ptr()) if prev is not None else None, prev.stride(0) if prev is not None else 0,
+                self.prev_B if prev is not None else 0,
+                c_void_p(self.prev_state.data_ptr()) if prev is not None else None,
+                c_void_p(rows.data_ptr()), c_void_p(mlo.data_ptr()), c_void_p(mhi.data_ptr()),
+                c_void_p(state.data_ptr()), c_void_p(self.status.data_ptr()), c_void_p(stream)), "processor_step")
+            bits = self.index.allowed_mask(mlo, mhi, V, SHIFT, packed=True)
+            out = self.core.epilogue_device(scores, rows, bits, int(cfg.eos))
+            self.status_h.copy_(self.status, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+        st = self.status_h.tolist()
+        if st[0] != 0 or st[1] != st[2]:
+            self.prev_ids = None
+            return None
+        self.prev_ids = ids.clone()     # the caller may reuse its input_ids buffer
+        self.prev_state = state
+        self.prev_B = B
+        return out
 
 
 class _BatchedCore:
@@ -108,6 +208,25 @@ class _BatchedCore:
             self._uni_cache[key] = torch.from_numpy(packed.copy()).to(device)
         return self._uni_cache[key]
 
+    def epilogue_device(self, scores: torch.Tensor, rows_dev, bits, eos: int) -> torch.Tensor:
+        """As ``epilogue`` with the row parameters already on the device."""
+        dev_index = torch.device("cuda", self.index.device)
+        dtype = scores.dtype
+        if dtype not in _DTYPE_CODE:
+            raise TypeError(f"unsupported scores dtype {dtype}")
+        src = scores.to(dev_index).contiguous()
+        out = torch.empty_like(src)
+        B, V = src.shape
+        uni = self.unigram_bits(V, dev_index)
+        stream = torch.cuda.current_stream(dev_index).cuda_stream
+        ldb = bits.stride(0) if bits is not None else 0
+        check(lib().fm_apply_boosts(_DTYPE_CODE[dtype], c_void_p(src.data_ptr()), c_void_p(out.data_ptr()), B, V,
+                                    src.stride(0), out.stride(0),
+                                    c_void_p(bits.data_ptr()) if bits is not None else None, ldb,
+                                    c_void_p(uni.data_ptr()), c_void_p(rows_dev.data_ptr()), int(eos),
+                                    c_void_p(stream)), "apply_boosts")
+        return out.to(scores.device)
+
     def epilogue(self, scores: torch.Tensor, rows: np.ndarray, bits, eos: int) -> torch.Tensor:
         """scores [B, V] (any supported dtype/device) -> scores + mask."""
         dev_index = torch.device("cuda", self.index.device)
@@ -128,6 +247,16 @@ class _BatchedCore:
                                         c_void_p(uni.data_ptr()), c_void_p(rp.data_ptr()), int(eos),
                                         c_void_p(stream)), "apply_boosts")
         return out.to(scores.device)
+
+
+def _device_step(core, boost, lrf, fdf):
+    """The device path when the index is this engine's GPU index (its
+    handle), else None (e.g. an oracle index in the CPU tests)."""
+    from .fm_index import FMIndex as _Engine
+
+    if not isinstance(core.index, _Engine) or not torch.cuda.is_available():
+        return None
+    return _DeviceStep(core, boost, lrf, fdf)
 
 
 def _find_marker_rows(input_ids: torch.Tensor, marker: Sequence[int]) -> List[torch.Tensor]:
@@ -184,6 +313,7 @@ class QwenIndexBasedLogitsProcessor:
         self.BOOST = 10.0
         self.end_marker = [151645, 198, 151644, 77091, 198]
         self._core = _BatchedCore(index)
+        self._dev = _device_step(self._core, self.BOOST, length_reward_factor, force_decoding_from)
 
     @classmethod
     def remove_system_tokens(cls, sent: List[int]) -> List[int]:
@@ -200,7 +330,27 @@ class QwenIndexBasedLogitsProcessor:
     def __call__(self, input_ids, scores):
         return self._process(input_ids, scores)
 
+    def _prep_config(self, dtype) -> _PrepConfig:
+        c = _PrepConfig()
+        for i, t in enumerate(self.end_marker):
+            c.marker[i] = t
+        c.marker_len = len(self.end_marker)
+        c.think[0], c.think[1] = self.FINISHED_THINKING
+        for i, t in enumerate(self.SYSTEM_TOKENS):
+            c.sys[i] = t
+        c.eos, c.pad = self.eos_token_id, self.pad_token_id
+        c.stop_at_count, c.min_new_tokens, c.shift = self.stop_at_count, self.min_new_tokens, SHIFT
+        c.num_beams = self._num_beams
+        c.flags = PREP_THINK | (PREP_EOS if self.always_allow_eos else 0)
+        c.base = 0.0
+        c.v_uni_full, c.v_uni_half = _round(self.BOOST, dtype), _round(self.BOOST / 2, dtype)
+        return c
+
     def _process(self, input_ids: torch.LongTensor, scores: torch.FloatTensor) -> torch.Tensor:
+        if self._dev is not None:
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            if out is not None:
+                return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
         B, V = scores.shape
         rows = np.zeros(B, dtype=ROW_DTYPE)
@@ -300,11 +450,33 @@ class CausalIndexBasedLogitsProcessor:
         if model_name.lower().startswith("qwen"):
             self.end_marker = self.END_MARKERS["qwen"]
         self._core = _BatchedCore(index)
+        self._dev = _device_step(self._core, self.BOOST, length_reward_factor, force_decoding_from)
 
     def __call__(self, input_ids, scores):
         return self._process(input_ids, scores)
 
+    def _prep_config(self, dtype) -> _PrepConfig:
+        c = _PrepConfig()
+        for i, t in enumerate(self.end_marker):
+            c.marker[i] = t
+        c.marker_len = len(self.end_marker)
+        c.eos, c.pad = self.eos_token_id, self.pad_token_id
+        c.stop_at_count, c.shift = self.stop_at_count, SHIFT
+        c.num_beams = self._num_beams
+        c.flags = PREP_UNI_HALF | ((PREP_EOS | PREP_EOS_ALL) if self.always_allow_eos else 0)
+        if self.forced_bos_token_id is not None:
+            c.flags |= PREP_SKIP_FIRST
+            c.forced_bos = self.forced_bos_token_id
+        c.base = 0.0
+        c.v_uni_full, c.v_uni_half = _round(self.BOOST, dtype), _round(self.BOOST / 2, dtype)
+        c.v_forced = c.v_uni_full
+        return c
+
     def _process(self, input_ids, scores):
+        if self._dev is not None:
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            if out is not None:
+                return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
         B, V = scores.shape
         dt = scores.dtype

@@ -254,6 +254,55 @@ int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, ui
 int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
                uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream);
 
+/* ---- logits-processor step on the device --------------------------------- */
+
+/* The per-row bookkeeping of the soft processors' _process
+ * (document_constrained_generation_causal_qwen.py:101-214,
+ * document_constrained_generation_causal.py:74-180), one wave per row. */
+typedef struct fm_prep_config {
+  int64_t marker[8];       /* remove_end_marker's marker, marker_len tokens (causal_qwen.py:42,44-56) */
+  int64_t think[2];        /* finished_thinking's pair (causal_qwen.py:76) */
+  int64_t sys[4];          /* remove_system_tokens' prefix (causal_qwen.py:60) */
+  int64_t eos, pad, stop_at_count, min_new_tokens, forced_bos, shift;
+  int32_t marker_len;      /* 1..8 */
+  int32_t num_beams;       /* rows = batch x num_beams, beams of one batch item adjacent */
+  uint32_t flags;          /* FM_PREP_* */
+  float base;              /* mask value of untouched tokens (0.0 for the soft processors) */
+  float v_uni_full;        /* BOOST rounded to the scores dtype */
+  float v_uni_half;        /* BOOST / 2 rounded */
+  float v_forced;          /* BOOST rounded (forced bos) */
+  int32_t reserved;
+} fm_prep_config;
+
+#define FM_PREP_THINK 1u       /* think gating + system-token removal (Qwen) */
+#define FM_PREP_SKIP_FIRST 2u  /* forced_bos_token_id set: strip the first generated token (causal.py:80-85) */
+#define FM_PREP_EOS 4u         /* always_allow_eos */
+#define FM_PREP_EOS_ALL 8u     /* the eos boost on every row, no min_new_tokens gate (causal.py:173-178) */
+#define FM_PREP_UNI_HALF 16u   /* BOOST / 2 for the other unigrams even when distinct is empty (causal.py:171) */
+
+#define FM_PREP_BAD_MARKER 1u  /* status: a row without exactly one end marker */
+#define FM_PREP_BAD_POW 2u     /* status: a boost BOOST * lrf^k outside the table (Python float overflow) */
+
+/* One processor step on the device, for B rows of d_ids (int64 [B, L], ld_ids
+ * elements per row): end marker, think gating, system tokens, the trailing
+ * n-gram rule (count of the last token), the eos / pad / stop_at_count rules,
+ * and the pattern range -- ONE LF step from the previous call's range of the
+ * row whose pattern this one extends (d_prev_ids / d_prev_state, rows of the
+ * same beam group, compared token by token), else a full search of
+ * force_decoding_from + sent (index.py:103-114).  Writes the epilogue's row
+ * parameters (d_rows), the range of every row whose distinct set is the
+ * mask's (d_mask_lo / d_mask_hi, (0, 0) otherwise) and this call's state
+ * d_state = int64 [4][B] (pattern start in the row, length or -1, lo, hi).
+ * d_pow[k] = BOOST * lrf^k rounded to the scores dtype (NaN: not a finite
+ * Python float).  d_status (4 uint32, written by the call): [0] FM_PREP_BAD_*
+ * bits, [1] / [2] min / max marker end over the rows (they must agree, as
+ * the reference's torch.stack requires).  Stream-ordered; no allocation. */
+int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_ids, uint64_t B, uint64_t L,
+                      uint64_t ld_ids, const int64_t* d_fdf, uint64_t fdf_len, const float* d_pow, uint64_t pow_len,
+                      const int64_t* d_prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* d_prev_state,
+                      fm_row_params* d_rows, uint64_t* d_mask_lo, uint64_t* d_mask_hi, int64_t* d_state,
+                      uint32_t* d_status, void* stream);
+
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
 /* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip
