@@ -66,14 +66,15 @@ PREP_THINK, PREP_SKIP_FIRST, PREP_EOS, PREP_EOS_ALL, PREP_UNI_HALF = 1, 2, 4, 8,
 
 def _boost_table(boost: float, lrf: float, dtype, n: int) -> List[float]:
     """BOOST * lrf ** k (the reference's Python float arithmetic, k < n)
-    rounded like an index-put into ``dtype``; NaN where ``lrf ** k`` is not a
-    finite Python float (the reference raises OverflowError there: such rows
-    take the host path, which raises the same)."""
+    rounded like an index-put into ``dtype``; NaN where the reference's
+    assignment raises instead -- ``lrf ** k`` is not a finite Python float
+    (OverflowError) or the value does not fit ``dtype`` (torch's RuntimeError):
+    rows needing such an entry take the host path, which raises the same."""
     out = []
     for k in range(n):
         try:
             out.append(_round(boost * (lrf ** k), dtype))
-        except OverflowError:
+        except (OverflowError, RuntimeError):
             out.append(math.nan)
     return out
 
