@@ -38,7 +38,7 @@ for _p in (REPO, PKG):
         sys.path.insert(0, _p)
 
 from fmidx._lib import check, lib  # noqa: E402
-from fmidx.fm_index import FMIndex, suffix_sort_device  # noqa: E402
+from fmidx.fm_index import FMIndex  # noqa: E402
 from fmidx.synth import decode_trace, markov_corpus_gpu, trace_patterns  # noqa: E402
 
 SHIFT = 10
@@ -58,17 +58,16 @@ def build_index(n_tokens: int, vocab: int, seed: int, dev):
     text, beg = markov_corpus_gpu(n_tokens, vocab, seed, dev)
     torch.cuda.synchronize()
     t1 = time.time()
-    log(f"corpus n={text.numel()} docs={beg.numel() - 1} in {t1 - t0:.1f}s; GPU suffix sorting ...")
-    bwt, _ = suffix_sort_device(text)      # csrc/sa.hip: prefix doubling, 64-bit positions
+    log(f"corpus n={text.numel()} docs={beg.numel() - 1} in {t1 - t0:.1f}s; GPU construction ...")
+    # fm_initialize_from_text_device: suffix array by GPU prefix doubling (64-bit
+    # positions, csrc/sa.hip), SA / ISA samples for locate / extract, the index
+    fm = FMIndex(device=dev.index)
+    fm.initialize_from_text_device(text, keep_sa_text=True)
     torch.cuda.synchronize()
     t2 = time.time()
-    log(f"suffix sorting {t2 - t1:.1f}s; building the index ...")
-    fm = FMIndex(device=dev.index)
-    fm.initialize_from_bwt_device(bwt)
-    torch.cuda.synchronize()
-    t3 = time.time()
-    log(f"corpus {t1 - t0:.1f}s  suffix array {t2 - t1:.1f}s  index {t3 - t2:.1f}s  n={bwt.numel()}")
-    return fm, text, bwt, {"corpus_s": t1 - t0, "sa_s": t2 - t1, "index_s": t3 - t2}
+    bwt = fm.device_bwt()                  # zero-copy view of the index's BWT
+    log(f"corpus {t1 - t0:.1f}s  suffix array + index {t2 - t1:.1f}s  n={bwt.numel()}")
+    return fm, text, bwt, {"corpus_s": t1 - t0, "sa_and_index_s": t2 - t1}
 
 
 def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int,

@@ -411,6 +411,25 @@ class FMIndex:
         o = off.cpu().tolist()
         return [tuple(flat[o[i]:o[i + 1]]) for i in range(m)]
 
+    def device_bwt(self):
+        """The handle's BWT (uint32[n] in HBM) as a zero-copy int32 torch
+        tensor on the index's device (valid while this index lives; read-only
+        by contract) -- for samplers, traces and the CPU baseline."""
+        import torch
+
+        idx = self
+
+        class _View:
+            __cuda_array_interface__ = {"shape": (self.size(),), "typestr": "<i4",
+                                        "data": (self.device_bwt_ptr(), True), "version": 2, "strides": None}
+
+            def __init__(self):
+                self.owner = idx
+
+        with torch.cuda.device(self._device):
+            t = torch.as_tensor(_View(), device=torch.device("cuda", self._device))
+        return t
+
     def device_bwt_ptr(self) -> int:
         p = c_void_p()
         check(lib().fm_device_bwt(self._h, byref(p)), "device_bwt")

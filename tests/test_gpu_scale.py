@@ -32,16 +32,15 @@ def dev():
 def _build(n_tokens, seed, dev):
     import torch
 
-    from fmidx.fm_index import FMIndex, suffix_sort_device
+    from fmidx.fm_index import FMIndex
     from fmidx.synth import markov_corpus_gpu
 
     torch.cuda.empty_cache()   # blocks torch cached for earlier tests: the index is hipMalloc'd beside them
-    text, _ = markov_corpus_gpu(n_tokens, V, seed, dev)
-    bwt, _ = suffix_sort_device(text)
+    text, beg = markov_corpus_gpu(n_tokens, V, seed, dev)
     fm = FMIndex(device=0)
-    fm.initialize_from_bwt_device(bwt)
+    fm.initialize_from_text_device(text, keep_sa_text=True)     # GPU sort, SA / ISA samples, index
     torch.cuda.synchronize()
-    return fm, text, bwt
+    return fm, text, fm.device_bwt(), beg
 
 
 @pytest.fixture(scope="module")
@@ -52,10 +51,10 @@ def c3(dev):
         pytest.skip("needs a 288 GB MI355X")
     from oracle.cpu_ref import CpuRef
 
-    fm, text, bwt = _build(4_400_000_000, 7, dev)
+    fm, text, bwt, beg = _build(4_400_000_000, 7, dev)
     assert bwt.numel() > (1 << 32)
     ref = CpuRef.from_device_bwt(bwt)
-    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref}
+    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref, "beg": beg}
     del fm, text, bwt, ref
     torch.cuda.empty_cache()
 
@@ -66,9 +65,9 @@ def c2(dev):
 
     from oracle.cpu_ref import CpuRef
 
-    fm, text, bwt = _build(300_000_000, 5, dev)
+    fm, text, bwt, beg = _build(300_000_000, 5, dev)
     ref = CpuRef.from_device_bwt(bwt)
-    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref}
+    yield {"fm": fm, "text": text, "bwt": bwt, "ref": ref, "beg": beg}
     del fm, text, bwt, ref
     torch.cuda.empty_cache()
 
@@ -255,3 +254,45 @@ def test_c2_full_research_equals_incremental(dev, c2):
     gm = fm.allowed_mask(lo_hist[-1], hi_hist[-1], V, SHIFT).cpu().numpy()
     assert np.array_equal(gm, cm)
     del torch
+
+
+@pytest.mark.timeout(900)
+def test_c3_locate_extract_from_samples(dev, c3):
+    """locate / extract_text on the C3 index from SA / ISA samples (no resident
+    suffix array), checked through properties of the text: BWT[r] = T'[SA[r] - 1]
+    for random rows (and every row of a pattern's range, whose text must spell
+    the reversed pattern); get_doc (index.py:69-80) of random docs equals the
+    text slice the reference's LF walk emits."""
+    import torch
+
+    fm, text, bwt, beg = c3["fm"], c3["text"], c3["bwt"], c3["beg"]
+    n = text.numel()
+    st = fm.stats()
+    assert 0 < st["sample_bytes"] < n // 2
+    g = torch.Generator(device=dev)
+    g.manual_seed(21)
+    rows = torch.randint(0, n, (1 << 20,), generator=g, device=dev)
+    pos = fm.locate_batch(rows)
+    assert bool(((pos >= 0) & (pos < n)).all())
+    prev = torch.where(pos > 0, pos - 1, torch.full_like(pos, n - 1))
+    assert torch.equal(text[prev], bwt[rows])
+    # a pattern's occurrences: the text at every located position spells reverse(pattern)
+    pat = (text[(n - 2) - (123456789 + torch.arange(4, device=dev))].to(torch.int64) - SHIFT).tolist()
+    lo = torch.zeros(1, dtype=torch.int64, device=dev)
+    hi = torch.zeros(1, dtype=torch.int64, device=dev)
+    fm.backward_search_batch(torch.tensor(pat, device=dev), torch.tensor([0, 4], device=dev), SHIFT, lo, hi)
+    r = torch.arange(int(lo), int(hi), device=dev)
+    p = fm.locate_batch(r)
+    for j, t in enumerate(reversed(pat)):
+        assert bool((text[p + j] == t + SHIFT).all()), j
+    # extract_text through the ISA samples: get_doc(d) = T'[(end - 2 - j) mod n] - SHIFT
+    begs = beg.cpu().tolist()
+    docs = [int(d) for d in torch.randint(0, len(begs) - 1, (64,), generator=g, device=dev).tolist()] + [0]
+    b = [begs[d] for d in docs]
+    e = [begs[d + 1] for d in docs]
+    got = fm.extract_batch(b, e)
+    for d, x, y, out in zip(docs, b, e, got):
+        idx = (torch.arange(y - x, device=dev) * -1 + (y - 2)) % n
+        assert list(out) == text[idx].tolist(), d
+    assert fm.extract_text(b[0], e[0]) == got[0]
+    assert fm.locate(int(rows[0])) == int(pos[0])
