@@ -421,7 +421,7 @@ class FMIndex:
 
         class _View:
             __cuda_array_interface__ = {"shape": (self.size(),), "typestr": "<i4",
-                                        "data": (self.device_bwt_ptr(), True), "version": 2, "strides": None}
+                                        "data": (self.device_bwt_ptr(), False), "version": 2, "strides": None}
 
             def __init__(self):
                 self.owner = idx
