@@ -58,9 +58,8 @@ void Index::release() {
   cache_tab = nullptr;
   cache_nodes = cache_bytes = 0;
   if (D2) (void)hipFree(D2);
-  for (void* p : {(void*)mark, (void*)mark_cnt, (void*)sa_samp, (void*)isa_samp, (void*)gbar})
+  for (void* p : {(void*)mark, (void*)mark_cnt, (void*)sa_samp, (void*)isa_samp})
     if (p) (void)hipFree(p);
-  gbar = nullptr;
   mark = mark_cnt = isa_samp = nullptr;
   sa_samp = nullptr;
   samp_bytes = 0;

@@ -597,11 +597,6 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   // from the root is), so its probe hits: waiting for the probe alone before
   // any rank load measured 17.5 -> 16.1 us/step cold, 10.4 -> 9.8 warm at C3
   v.probe_first = env_u32("FMIDX_PROBE_FIRST", 1) != 0;
-  if (!h->gbar) {
-    if (dmalloc(&h->gbar, 1)) return -1;
-    FM_HIP(hipMemsetAsync(h->gbar, 0, 8, s));
-  }
-  v.gbar = h->gbar;
   // -- follow-set bitmaps (one per symbol's C-block), built with the mask
   //    kernel itself once the view above is complete
   // (off by default: the range-bitmap cache below holds every C-block of

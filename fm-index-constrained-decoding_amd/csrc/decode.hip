@@ -56,30 +56,6 @@ constexpr int kUnroll = 4;                    // uint4 loads in flight per threa
 // global data, so only LDS (lgkmcnt) is drained.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Grid-wide phase barrier of the decode kernel (read phase -> write phase):
-// one 64-bit word, count in the low half, generation in the high half.  Every
-// workgroup of the launch arrives exactly once; the last arrival resets the
-// count and bumps the generation in one atomic.  A waiter gives up after
-// kBarrierTicks (s_memrealtime, 100 MHz) -- the barrier only orders memory
-// traffic for speed, so a workgroup that is not co-resident (another kernel
-// holding CUs) costs time, never correctness, and can never hang the grid.
-constexpr uint64_t kBarrierTicks = 2000;   // 20 us
-__device__ __forceinline__ bool grid_arrive(uint64_t* bar, uint32_t nwg, uint64_t& gen) {
-  const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long*>(bar), 1ull);
-  gen = old >> 32;
-  if ((uint32_t)old + 1u == nwg) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(bar), (1ull << 32) - nwg);
-    return true;
-  }
-  return false;
-}
-__device__ __forceinline__ void grid_wait(uint64_t* bar, uint64_t gen) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while ((__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == gen &&
-         __builtin_amdgcn_s_memrealtime() - t0 < kBarrierTicks)
-    __builtin_amdgcn_s_sleep(2);
-}
-
 struct Plan {
   uint64_t a0, b0, a1, b1;            // streamed BWT row ranges (partial ends / narrow range)
   uint32_t nb;                        // bitmaps to OR
@@ -309,7 +285,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        uint64_t* __restrict__ hi_out,
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
-                                                       uint64_t early_width, DevView v, uint32_t phase_split) {
+                                                       uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
   // zero-filling waves -- from thread 256, 512 or 768 -- measured the same)
@@ -343,17 +319,9 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   FM_STAMP(v, 0);
   const uint64_t st_lo = (uint64_t)ql.x | ((uint64_t)ql.y << 32), st_hi = (uint64_t)qh.x | ((uint64_t)qh.y << 32);
   const int64_t st_tok = (int64_t)((uint64_t)qt.x | ((uint64_t)qt.y << 32));
-  // phase_split: every workgroup completes its dependent reads (row state, LF
-  // step, range content) before any mask store is issued anywhere in the grid
-  // -- cold, the stores' HBM traffic otherwise queues ahead of the chains'
-  // reads -- then all of them write (host: only when the grid is co-resident)
-  const bool split = phase_split != 0 && v.gbar;
+  if (row >= m) return;
   const uint64_t t0 = (uint64_t)slice * SW;
-  if (row >= m || t0 >= vocab) {
-    uint64_t gen;
-    if (split && threadIdx.x == 0) grid_arrive(v.gbar, gridDim.x, gen);
-    return;
-  }
+  if (t0 >= vocab) return;
   const uint64_t t1 = min(vocab, t0 + SW);
   const uint64_t ntok = t1 - t0;
   const uint64_t nch = (ntok + CH - 1) / CH;
@@ -364,7 +332,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // chunks holding an allowed token.
   const bool reset = DO_LF && st_tok < reset_below;
   const uint64_t in_lo = st_lo, in_hi = min(st_hi, v.n);
-  const bool early_zero = !split && !reset && (in_lo >= in_hi || in_hi - in_lo <= early_width);
+  const bool early_zero = !reset && (in_lo >= in_hi || in_hi - in_lo <= early_width);
   // Incoming ranges of kENarrow+1 .. kEWide rows that the transition table does
   // not serve take their LF step as ONE scan of E[lo, hi) by the whole
   // workgroup (<= kEWide / kDecThreads entries per thread, one round trip)
@@ -501,7 +469,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   //               waves 4.. zero-fill now, overlapping the stream round trip
   //   otherwise   every wave gathers (bitmaps + partial ends), every wave emits
   // The zero-filling waves own their chunks in the final emit (program order).
-  const bool late_zero = !split && kDecThreads >= 512 && !early_zero && lo < hi && plan.nb == 0;
+  const bool late_zero = kDecThreads >= 512 && !early_zero && lo < hi && plan.nb == 0;
   const uint32_t e_first = early_zero ? (uint32_t)kEzFirst : (late_zero ? 256u : 0u);   // emit/zero owners: tid >= e_first
   if (late_zero && threadIdx.x >= e_first) {
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
@@ -518,7 +486,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // One whole bitmap and nothing streamed (a cached range, the full range or a
   // follow set): emitted straight from the bitmap in memory, no LDS pass.
   const bool single = lo < hi && plan.nb == 1 && plan.a0 >= plan.b0 && plan.a1 >= plan.b1;
-  const bool direct = single && kDecThreads >= 1024 && !split;   // split: staged in LDS before the barrier
+  const bool direct = single && kDecThreads >= 1024;
   if (single && !direct) {
     // smaller workgroups: the one bitmap is staged into the LDS window with
     // every load of a batch in flight together (one round trip for a 128k
@@ -603,13 +571,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         gwb = w_lo + 4 * (int64_t)w4b;
         own = w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words;
       }
-    }
-    lds_barrier();
-  }
-  if (split) {   // the read phase of this workgroup is over: wait for the grid's
-    if (threadIdx.x == 0) {
-      uint64_t gen;
-      if (!grid_arrive(v.gbar, gridDim.x, gen)) grid_wait(v.gbar, gen);
     }
     lds_barrier();
   }
@@ -787,20 +748,9 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
   }();
   const size_t lds = (size_t)win_words(SW) * 4;
-  // the read/write phase split (see k_decode): uint8 masks (the packed output
-  // is too small for its stores to crowd the reads), 1024-thread workgroups,
-  // and only while the whole grid fits the chip at once (one workgroup per CU)
-  static const uint32_t split_env = env_u32("FMIDX_PHASE_SPLIT", 1);
-  static const uint32_t n_cu = [] {
-    int dev = 0, cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
-    return (uint32_t)cu;
-  }();
-  const uint32_t split = (split_env && !packed && T == 1024 && v.gbar && g <= n_cu) ? 1u : 0u;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v, split)
+                                        mask, ld, ew, v)
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \

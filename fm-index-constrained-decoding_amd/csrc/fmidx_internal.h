@@ -104,7 +104,6 @@ struct DevView {
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
-  uint64_t* gbar;             // grid-barrier word of the decode kernel (count | generation << 32), or null
   uint32_t probe_first;       // 1: a cached range's LF step waits for its transition probe before
                               //    issuing the descent (a hit needs no rank loads); 0: issued together
 #ifdef FMIDX_STAMPS
@@ -576,7 +575,6 @@ struct Index {
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;         // legacy (v1 files / no samples): full suffix array
   uint32_t* text = nullptr;       // legacy: T' (extract without ISA samples)
-  uint64_t* gbar = nullptr;       // decode kernel's grid-barrier word
   uint64_t* mark = nullptr;       // SA / ISA samples (locate.hip)
   uint64_t* mark_cnt = nullptr;
   uint32_t* sa_samp = nullptr;
