@@ -56,17 +56,6 @@ constexpr int kUnroll = 4;                    // uint4 loads in flight per threa
 // global data, so only LDS (lgkmcnt) is drained.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Store hold: a wave issues its first mask store no earlier than `hold` ticks
-// (s_memrealtime, 100 MHz) after its workgroup started.  All workgroups of a
-// step start within ~1 us of each other, so this separates the grid's
-// dependent reads (row state, LF, range content) from the 33 MB of stores
-// without any cross-workgroup signal: cold, a read queued behind the stores
-// in HBM costs several us per round trip.  Purely a timing knob.
-__device__ __forceinline__ void hold_stores(uint64_t t_entry, uint64_t hold) {
-  if (!hold) return;
-  while (__builtin_amdgcn_s_memrealtime() - t_entry < hold) __builtin_amdgcn_s_sleep(1);
-}
-
 struct Plan {
   uint64_t a0, b0, a1, b1;            // streamed BWT row ranges (partial ends / narrow range)
   uint32_t nb;                        // bitmaps to OR
@@ -296,7 +285,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        uint64_t* __restrict__ hi_out,
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
-                                                       uint64_t early_width, DevView v, uint64_t hold) {
+                                                       uint64_t early_width, DevView v) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
   // zero-filling waves -- from thread 256, 512 or 768 -- measured the same)
@@ -309,7 +298,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // 32 KB maximum): LDS is what bounds the workgroups resident per CU at
   // 256 threads
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
-  const uint64_t t_entry = hold ? __builtin_amdgcn_s_memrealtime() : 0;
   uint64_t row;
   uint32_t slice;
   map_block(blockIdx.x, S, row, slice);
@@ -366,7 +354,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // so a wave with stores in flight cannot wait on a load without also
   // waiting for them -- wave 0 (LF + plan) must stay store-free.
   if (early_zero && threadIdx.x >= kEzFirst) {
-    hold_stores(t_entry, hold);
     for (uint64_t k = threadIdx.x - kEzFirst; k < nch; k += kDecThreads - kEzFirst) {
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
@@ -485,7 +472,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   const bool late_zero = kDecThreads >= 512 && !early_zero && lo < hi && plan.nb == 0;
   const uint32_t e_first = early_zero ? (uint32_t)kEzFirst : (late_zero ? 256u : 0u);   // emit/zero owners: tid >= e_first
   if (late_zero && threadIdx.x >= e_first) {
-    hold_stores(t_entry, hold);
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
@@ -594,7 +580,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // two, no wait for the zero stores' acknowledgements is needed.
   const bool zeroed = early_zero || late_zero;
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
-  if (!direct) hold_stores(t_entry, hold);
   if (direct) {
     // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH).  All of a
     // thread's chunks (kDirectU per round, one round for a 128k-152k vocab)
@@ -616,7 +601,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         wa[u] = (k < nch32 && wi < wlim) ? bm[wi] : 0u;
         wb[u] = (k < nch32 && wi + 1 < wlim) ? bm[wi + 1] : 0u;
       }
-      hold_stores(t_entry, hold);
       uint32_t slow = 0;   // chunks needing byte stores (a short last chunk / unaligned row): after the loop
 #pragma unroll
       for (int u = 0; u < kDirectU; ++u) {
@@ -764,11 +748,9 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
   }();
   const size_t lds = (size_t)win_words(SW) * 4;
-  static const uint64_t hold_env = env_u32("FMIDX_STORE_HOLD", 0);   // ticks of 10 ns
-  const uint64_t hold = packed ? 0 : hold_env;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v, hold)
+                                        mask, ld, ew, v)
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
