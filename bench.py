@@ -480,6 +480,16 @@ def main():
     # region: the fused step cold
     lf_warm = [t / K for t in timed(g_lf, 5)]
     lf_cold = [t / K for t in timed(g_lf, 3, cold=True)]
+    # rank throughput at concurrency: all K x B (state, token) pairs of the
+    # timed steps in ONE k_lf launch (independent rows), cold
+    all_tok = tokens[W:S].reshape(-1).contiguous()
+    all_lo = lo_hist[W - 1:S - 1].reshape(-1).contiguous()
+    all_hi = hi_hist[W - 1:S - 1].reshape(-1).contiguous()
+    big_lo, big_hi = torch.empty_like(all_lo), torch.empty_like(all_hi)
+    g_lfbig = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_lfbig):
+        fm.lf_step_batch(all_tok, all_lo, all_hi, SHIFT, lo_out=big_lo, hi_out=big_hi, reset_below=0)
+    lfbig_cold = timed(g_lfbig, 3, cold=True)
     mask_ms = [t / K for t in timed(g_mask, 5)]
     step_warm = [t / K for t in timed(g_step, 3, reset=True)]
     lo.copy_(state_lo)
@@ -558,6 +568,8 @@ def main():
     lf_us_warm = float(np.median(lf_warm)) * 1e3
     lf_us_cold = float(np.median(lf_cold)) * 1e3
     rank_gbs = float(lf_std.mean()) / (lf_us_cold * 1e-6) / 1e9
+    lfbig_us = float(np.median(lfbig_cold)) * 1e3
+    rank_gbs_big = float(lf_std.sum()) / (lfbig_us * 1e-6) / 1e9
     gather_gbs, chase_ns = (None, None)
     if not args.no_gather:
         gather_gbs, chase_ns = gather_ceiling(dev)
@@ -569,7 +581,8 @@ def main():
     achieved = decode_bytes / (decode_us * 1e-6) / 1e9
     widths = (hi_np - lo_np)
     log(f"step cold {step_ms * 1e3:.1f}us, warm [{', '.join(f'{t * 1e3:.1f}' for t in step_warm)}] "
-        f"(standalone lf cold {lf_us_cold:.1f}us / warm {lf_us_warm:.1f}us, mask {mask_us:.1f}us, "
+        f"(standalone lf cold {lf_us_cold:.1f}us / warm {lf_us_warm:.1f}us, {K * B} rows in one launch "
+        f"{lfbig_us:.1f}us = {rank_gbs_big:.0f} GB/s, mask {mask_us:.1f}us, "
         f"wall/step {wall / K * 1e6:.1f}us, graph) bytes/step {decode_bytes / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
         f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}, "
         f"cached rows {cached.mean():.3f} (cache: {st['cache_nodes']} ranges >= {st['cache_min']}, "
@@ -625,6 +638,10 @@ def main():
                      "gather_ceiling_GBps": gather_gbs,
                      "rank_frac_of_gather_ceiling": (rank_gbs / gather_gbs) if gather_gbs else None,
                      "dependent_hop_ns": chase_ns,
+                     "batched": {"rows": int(K * B), "avg_launch_us_cold": lfbig_us,
+                                 "alg_bytes_per_launch": float(lf_std.sum()), "rank_GBps": rank_gbs_big,
+                                 "rank_frac_of_gather_ceiling": (rank_gbs_big / gather_gbs) if gather_gbs else None,
+                                 "note": "all K x B (state, token) pairs of the timed steps in one launch"},
                      "bytes_model": "64-B lines the LF plan reads per live row (bench.lf_plan_bytes)"},
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},

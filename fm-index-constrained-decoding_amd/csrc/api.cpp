@@ -168,11 +168,13 @@ struct Stage {
 
 int stage_reserve(fm_index* h, const Stage& st) {
   if (h->stage_bytes >= st.need) return 0;
+  // geometric growth: a batch that grows by a few tokens per call (decode) does
+  // not reallocate pinned memory (milliseconds per hipHostMalloc) every call
+  const size_t bytes = std::max<size_t>({st.need, 2 * h->stage_bytes, (size_t)1 << 20});
   if (h->stage) FM_HIP(hipFree(h->stage));
   if (h->hstage) FM_HIP(hipHostFree(h->hstage));
   h->stage = h->hstage = nullptr;
   h->stage_bytes = 0;
-  const size_t bytes = std::max<size_t>(st.need, 1 << 20);
   FM_HIP(hipMalloc(&h->stage, bytes));
   FM_HIP(hipHostMalloc(&h->hstage, bytes, hipHostMallocDefault));
   h->stage_bytes = bytes;
