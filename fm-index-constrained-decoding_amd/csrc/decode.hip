@@ -210,8 +210,15 @@ __device__ __forceinline__ void stream_symbols(const uint32_t* __restrict__ bwt,
     uint4 q[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
+      // unconditional load, its result used unconditionally (a surplus lane
+      // re-reads element 0 of the middles and ORs in all-ones): a select here
+      // let the compiler sink the load into a branch with a vmcnt(0) right
+      // after it -- kUnroll round trips instead of one
       const uint64_t j = base + (uint64_t)u * nthr;
-      q[u] = (j < ntot) ? src[j < n0 ? q0 + j : q1 + (j - n0)] : make_uint4(~0u, ~0u, ~0u, ~0u);
+      const uint64_t jj = j < ntot ? j : 0;
+      const uint4 x = src[jj < n0 ? q0 + jj : q1 + (jj - n0)];
+      const uint32_t pad = j < ntot ? 0u : ~0u;
+      q[u] = make_uint4(x.x | pad, x.y | pad, x.z | pad, x.w | pad);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
@@ -241,6 +248,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// Loads through a bitmap pointer that was handed over in LDS (the plan).  The
+// compiler cannot tell such a pointer's address space and emits FLAT loads,
+// which count in lgkmcnt as well as vmcnt: the LDS read of the next pointer
+// (or any other LDS wait) then drains every earlier load, and a thread's 8-16
+// bitmap loads went out one round trip at a time.  As global loads they only
+// count in vmcnt and are all in flight together.
+typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;
+typedef const __attribute__((address_space(1))) v4u* gptr_v4;
+__device__ __forceinline__ uint32_t gld(const uint32_t* p, uint32_t i) { return ((gptr_u32)p)[i]; }
+__device__ __forceinline__ uint4 gld4(const uint32_t* p, int64_t i) {
+  const v4u x = *(gptr_v4)(p + i);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
 
 
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x) {
@@ -532,8 +553,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       for (int u = 0; u < 4; ++u) {
         const uint32_t w4b = j0 + (uint32_t)u * kDecThreads;
         const int64_t gwb = w_lo + 4 * (int64_t)w4b;
-        x[u] = (w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words)
-                   ? *reinterpret_cast<const uint4*>(bm + gwb) : make_uint4(0, 0, 0, 0);
+        x[u] = (w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words) ? gld4(bm, gwb) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -566,7 +586,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const uint32_t qq = g + (uint32_t)u * G;
-        x[u] = (own && qq < nb) ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
+        x[u] = (own && qq < nb) ? gld4(plan.ptr[qq], gwb) : make_uint4(0, 0, 0, 0);
       }
       stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
       FM_STAMP(v, 4);
@@ -582,7 +602,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const uint32_t qq = q + (uint32_t)u * G;
-                x[u] = qq < nb ? *reinterpret_cast<const uint4*>(plan.ptr[qq] + gwb) : make_uint4(0, 0, 0, 0);
+                x[u] = qq < nb ? gld4(plan.ptr[qq], gwb) : make_uint4(0, 0, 0, 0);
               }
             }
             first = false;
@@ -639,8 +659,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
           wa[u] = pre_a[u];
           wb[u] = pre_b[u];
         } else {
-          wa[u] = (k < nch32 && wi < wlim) ? bm[wi] : 0u;
-          wb[u] = (k < nch32 && wi + 1 < wlim) ? bm[wi + 1] : 0u;
+          wa[u] = (k < nch32 && wi < wlim) ? gld(bm, wi) : 0u;
+          wb[u] = (k < nch32 && wi + 1 < wlim) ? gld(bm, wi + 1) : 0u;
         }
       }
       uint32_t slow = 0;   // chunks needing byte stores (a short last chunk / unaligned row): after the loop
@@ -668,7 +688,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         if (!(slow & 1u)) continue;
         const uint32_t k = k0 + u * nt;
         const uint32_t wi = (bit0 + k * CH) >> 5, o = (bit0 + k * CH) & 31u;
-        const uint32_t a = wi < wlim ? bm[wi] : 0u, b = wi + 1 < wlim ? bm[wi + 1] : 0u;
+        const uint32_t a = wi < wlim ? gld(bm, wi) : 0u, b = wi + 1 < wlim ? gld(bm, wi + 1) : 0u;
         const uint32_t bits = (uint32_t)((((uint64_t)b << 32) | a) >> o);
         const uint64_t t = t0 + (uint64_t)k * CH;
         const uint32_t cnt = (uint32_t)min((uint64_t)CH, t1 - t);

@@ -275,15 +275,20 @@ __device__ __forceinline__ uint64_t rank_w2_at(const uint8_t* blocks, const uint
   uint32_t cnt = 0;
   if (bits > 8) {
     const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
-    uint4 x[4];
+    // A lane's 4 loads are issued together under one lane guard and consumed
+    // unconditionally (a digit group past k counts nothing): a load guarded
+    // per group was sunk into its own branch with a vmcnt(0) behind it, i.e.
+    // up to 4 dependent round trips per level.
+    uint4 x[4] = {};
+    if (first < k) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[u] = (first + 8 * u < k) ? p[u] : make_uint4(0, 0, 0, 0);
+      for (int u = 0; u < 4; ++u) x[u] = p[u];
+    }
     const uint32_t dd = d | (d << 16);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t j0 = first + 8 * u;   // digits j0 .. j0+7
-      if (j0 >= k) continue;
-      const uint32_t nv = min(8u, k - j0);
+      const uint32_t nv = j0 < k ? min(8u, k - j0) : 0u;
       cnt += eq16_count(x[u].x, dd, nv >= 2 ? 3u : (nv >= 1 ? 1u : 0u));
       cnt += eq16_count(x[u].y, dd, nv >= 4 ? 3u : (nv >= 3 ? 1u : 0u));
       cnt += eq16_count(x[u].z, dd, nv >= 6 ? 3u : (nv >= 5 ? 1u : 0u));
@@ -291,15 +296,16 @@ __device__ __forceinline__ uint64_t rank_w2_at(const uint8_t* blocks, const uint
     }
   } else {
     const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 2 * q;
-    uint4 x[2];
+    uint4 x[2] = {};
+    if (first < k) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) x[u] = (first + 16 * u < k) ? p[u] : make_uint4(0, 0, 0, 0);
+      for (int u = 0; u < 2; ++u) x[u] = p[u];
+    }
     const uint32_t dd = d * 0x01010101u;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const uint32_t j0 = first + 16 * u;
-      if (j0 >= k) continue;
-      const uint32_t nv = min(16u, k - j0);
+      const uint32_t nv = j0 < k ? min(16u, k - j0) : 0u;
       cnt += eq8_count(x[u].x, dd, nv >= 4 ? 4u : nv);
       cnt += eq8_count(x[u].y, dd, nv >= 8 ? 4u : (nv > 4 ? nv - 4 : 0u));
       cnt += eq8_count(x[u].z, dd, nv >= 12 ? 4u : (nv > 8 ? nv - 8 : 0u));
@@ -329,8 +335,11 @@ __device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint
   uint64_t e[kENarrow / 64];
 #pragma unroll
   for (uint32_t j = 0; j < kENarrow / 64; ++j) {
+    // clamped, unconditional load, padded afterwards: a guarded load is sunk
+    // into a branch with a vmcnt(0) behind it (one round trip per j)
     const uint64_t idx = lo + lane + 64 * j;
-    e[j] = idx < hi ? v.E[idx] : ~0ull;
+    const uint64_t x = v.E[idx < hi ? idx : hi - 1];
+    e[j] = x | (idx < hi ? 0ull : ~0ull);
   }
   uint64_t fmin = ~0ull, fmax = 0, lfmin = 0, lfmax = 0;   // first / last match (relative index + 1)
 #pragma unroll
