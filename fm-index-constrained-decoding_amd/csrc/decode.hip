@@ -264,6 +264,8 @@ __device__ __forceinline__ uint4 gld4(const uint32_t* p, int64_t i) {
 }
 
 
+
+
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x) {
   v4u v = {x.x, x.y, x.z, x.w};
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
@@ -314,7 +316,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   __shared__ Plan plan;
   __shared__ uint64_t s_lohi[3];              // new range + its only symbol when the transition table knew it (else ~0)
   __shared__ unsigned long long s_scan[2];    // workgroup E scan: first / last occurrence
-  __shared__ uint32_t s_spec;                 // the child-bitmap table held this row's transition
   FM_STAMP_DECL;
   // sized at launch to the slice (16 KB at a 128k vocabulary instead of the
   // 32 KB maximum): LDS is what bounds the workgroups resident per CU at
@@ -367,31 +368,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                        in_hi - in_lo <= kScanMax && !(in_lo == 0 && in_hi == v.n) &&
                        (in_hi - in_lo < v.cache_min || !v.trans_cap);
   FM_PRELOAD_VIEW(v);   // after the state loads are in flight (see above)
-  // A wide incoming range is cached, so its LF step is a transition probe; when
-  // the child is cached too, a copy of the child's bitmap sits at an address
-  // computable from (parent, token) alone (cbt): every thread loads its share
-  // of that bitmap NOW, in the probe's round trip, and the emit needs no
-  // further read when the table held this transition (checked by wave 0).
-  constexpr int kPre = (kDecThreads >= 1024) ? 8 : 1;   // = kDirectU of the direct emit
-  const int64_t c_spec = st_tok + shift;
-  const bool spec = kDecThreads >= 1024 && DO_LF && !reset && v.cbt_mask && in_lo < in_hi &&
-                    in_hi - in_lo >= v.cache_min && !(in_lo == 0 && in_hi == v.n) && c_spec >= 0 &&
-                    (uint64_t)c_spec <= v.max_sym;
-  const uint64_t cslot = spec ? cbt_home(in_lo, in_hi, (uint64_t)c_spec, v.cbt_mask) : 0;
-  uint32_t pre_a[kPre], pre_b[kPre];
-#pragma unroll
-  for (int u = 0; u < kPre; ++u) pre_a[u] = pre_b[u] = 0u;
-  if (spec) {
-    const uint32_t* bm = v.cbt_bm + cslot * v.bm_words;
-    const uint32_t bit0 = (uint32_t)((int64_t)t0 + shift);
-#pragma unroll
-    for (int u = 0; u < kPre; ++u) {
-      const uint32_t k = threadIdx.x + (uint32_t)u * kDecThreads;
-      const uint32_t wi = (bit0 + k * CH) >> 5;
-      pre_a[u] = (k < nch && wi < v.bm_words) ? bm[wi] : 0u;
-      pre_b[u] = (k < nch && wi + 1 < v.bm_words) ? bm[wi + 1] : 0u;
-    }
-  }
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
   // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
   const __amdgpu_buffer_rsrc_t orsrc =
@@ -454,11 +430,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     int64_t follow = -1;
     const uint32_t* tbm = nullptr;   // bitmap of the new range, when the transition table knew it
     int64_t one = -1;                // the new range's only symbol, when the transition table knew it
-    bool hit = false;
     if (DO_LF) {
       const int64_t t = st_tok;
-      uint64_t ck = kTransEmpty;
-      if (spec && threadIdx.x < 2) ck = v.cbt_keys[3 * cslot + threadIdx.x];   // issued with the probe
       if (t < reset_below) {
         l = 0;
         h = v.n;
@@ -476,9 +449,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
       }
-      const uint64_t k0 = __shfl(ck, 0, 64), k1 = __shfl(ck, 1, 64);
-      hit = spec && k0 == (in_lo | ((uint64_t)c_spec << kTransSymShift)) && (k1 & kMask34) == in_hi;
-      if (hit) tbm = v.cbt_bm + cslot * v.bm_words;   // the same bitmap as the child's cache entry
     }
     l = __shfl(l, 0, 64);
     h = __shfl(h, 0, 64);
@@ -489,7 +459,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       s_lohi[0] = l;
       s_lohi[1] = h;
       s_lohi[2] = (uint64_t)one;
-      s_spec = hit ? 1u : 0u;
       plan.nb = 0;
       plan.a0 = plan.b0 = plan.a1 = plan.b1 = 0;
     }
@@ -553,7 +522,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       for (int u = 0; u < 4; ++u) {
         const uint32_t w4b = j0 + (uint32_t)u * kDecThreads;
         const int64_t gwb = w_lo + 4 * (int64_t)w4b;
-        x[u] = (w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words) ? gld4(bm, gwb) : make_uint4(0, 0, 0, 0);
+        x[u] = (w4b < nw4 && gwb >= 0 && gwb + 4 <= (int64_t)v.bm_words)
+                   ? gld4(bm, gwb) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -586,7 +556,12 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const uint32_t qq = g + (uint32_t)u * G;
-        x[u] = (own && qq < nb) ? gld4(plan.ptr[qq], gwb) : make_uint4(0, 0, 0, 0);
+        // unconditional (clamped) load, masked afterwards: under a branch the
+        // compiler put a vmcnt(0) between the first and second load
+        const bool ok = own && qq < nb;
+        const uint4 y = gld4(plan.ptr[ok ? qq : 0], ok ? gwb : 0);
+        const uint32_t m = ok ? ~0u : 0u;
+        x[u] = make_uint4(y.x & m, y.y & m, y.z & m, y.w & m);
       }
       stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
       FM_STAMP(v, 4);
@@ -641,27 +616,23 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     // e_first) when the row was zeroed early.
     const uint32_t* bm = plan.ptr[0];
     const uint32_t wlim = v.bm_words;
+    const __amdgpu_buffer_rsrc_t brs = make_rsrc(bm, wlim * 4u);
     const uint32_t nt = kDecThreads - e_first;
     const uint32_t nch32 = (uint32_t)nch;
     const uint32_t bit0 = (uint32_t)((int64_t)t0 + shift);   // < 2^27: 32-bit chunk arithmetic
     constexpr int kDirectU = (kDecThreads >= 1024) ? 8 : 4;
-    // the first round's words are already in registers when the child-bitmap
-    // table held the transition (spec loads, e_first == 0: wide rows are not zeroed early)
-    const bool pre = s_spec != 0 && e_first == 0;
     for (uint32_t k0 = threadIdx.x - e_first; threadIdx.x >= e_first && k0 < nch32; k0 += nt * kDirectU) {
       uint32_t wa[kDirectU], wb[kDirectU];
-      const bool first = pre && k0 == threadIdx.x;
 #pragma unroll
       for (int u = 0; u < kDirectU; ++u) {
         const uint32_t k = k0 + (uint32_t)u * nt;
         const uint32_t wi = (bit0 + k * CH) >> 5;
-        if (first && u < kPre) {
-          wa[u] = pre_a[u];
-          wb[u] = pre_b[u];
-        } else {
-          wa[u] = (k < nch32 && wi < wlim) ? gld(bm, wi) : 0u;
-          wb[u] = (k < nch32 && wi + 1 < wlim) ? gld(bm, wi + 1) : 0u;
-        }
+        // buffer loads: the descriptor's range check returns 0 past the
+        // bitmap's end, so every load is unconditional and all 2 kDirectU are
+        // in flight together (a guarded first load was followed by a vmcnt(0));
+        // words of chunks k >= nch are loaded and not used
+        wa[u] = __builtin_amdgcn_raw_buffer_load_b32(brs, wi * 4u, 0, 0);
+        wb[u] = __builtin_amdgcn_raw_buffer_load_b32(brs, wi * 4u + 4u, 0, 0);
       }
       uint32_t slow = 0;   // chunks needing byte stores (a short last chunk / unaligned row): after the loop
 #pragma unroll

@@ -104,14 +104,6 @@ struct DevView {
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
-  // child-bitmap table: for a transition (cached parent P, symbol c) whose child
-  // is cached, a copy of the child's bitmap at slot cbt_home(P, c) -- an
-  // address computable before the transition probe returns, so the decode
-  // kernel loads the bitmap in the probe's round trip (keys: the 3 words of the
-  // transition slot; a key whose home slot was taken is simply absent)
-  const uint64_t* cbt_keys;   // [cap][3]
-  const uint32_t* cbt_bm;     // [cap][bm_words]
-  uint64_t cbt_mask;          // cap - 1; 0 = none
   uint32_t probe_first;       // 1: a cached range's LF step waits for its transition probe before
                               //    issuing the descent (a hit needs no rank loads); 0: issued together
 #ifdef FMIDX_STAMPS
@@ -171,8 +163,7 @@ struct DevView {
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
                  "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
-                 "s"((v).trans_cap), "s"((v).cblock), "s"((v).probe_first), "s"((v).cbt_keys), "s"((v).cbt_bm),         \
-                 "s"((v).cbt_mask));                                                                          \
+                 "s"((v).trans_cap), "s"((v).cblock), "s"((v).probe_first));                                               \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
@@ -442,10 +433,6 @@ __host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi
 #endif
 }
 
-__host__ __device__ __forceinline__ uint64_t cbt_home(uint64_t lo, uint64_t hi, uint64_t c, uint64_t mask) {
-  return (trans_hash(lo, hi, c) >> 21) & mask;
-}
-
 // The LF step of the batched kernels, by all 64 lanes of a wave (uniform
 // inputs), with exactly one inlined copy of each path (a kernel's code is
 // fetched cold into the instruction cache at every launch, so duplicated
@@ -594,9 +581,6 @@ struct Index {
   uint64_t* trans_tab = nullptr;
   uint32_t* cblock = nullptr;
   uint64_t cache_nodes = 0, cache_bytes = 0, trans_entries = 0, trans_dropped = 0, trans_bytes = 0;
-  uint64_t* cbt_keys = nullptr;
-  uint32_t* cbt_bm = nullptr;
-  uint64_t cbt_entries = 0, cbt_bytes = 0;
   int64_t* D2 = nullptr;
   uint64_t* sa = nullptr;         // legacy (v1 files / no samples): full suffix array
   uint32_t* text = nullptr;       // legacy: T' (extract without ISA samples)
