@@ -238,15 +238,6 @@ __device__ __forceinline__ void map_block(uint32_t b, uint32_t S, uint64_t& row,
   slice = r >> 3;
 }
 
-// Buffer descriptor over [base, base + bytes) from wave-uniform values.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* b = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(b, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // Loads through a bitmap pointer that was handed over in LDS (the plan).  The

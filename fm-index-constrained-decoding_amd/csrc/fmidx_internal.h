@@ -238,6 +238,24 @@ __device__ __forceinline__ void descend_full(const DevView& v, uint32_t c, uint6
 }
 
 // ---------------------------------------------------------------------------
+// Buffer descriptor over [base, base + bytes) from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* b = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(b, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// One 8-byte element of a per-row array, as a range-checked buffer load: the
+// compiler cannot sink such a load into the branch that uses it, so a row's
+// state loads (token, lo, hi) go out together, one round trip.
+__device__ __forceinline__ uint64_t row_load_u64(const void* base, uint64_t count, uint64_t i) {
+  typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
+  const v2u_ q = __builtin_amdgcn_raw_buffer_load_b64(make_rsrc(base, (uint32_t)(count * 8)), (uint32_t)(i * 8), 0, 0);
+  return (uint64_t)q.x | ((uint64_t)q.y << 32);
+}
+
 // 2-level wavelet matrix rank / LF, computed by 32 lanes (q = lane & 31): lane
 // q covers digits [32 q, 32 q + 32) of the block (64 B of uint16 or 32 B of
 // uint8 digits), the partial counts meet in an xor-shuffle tree.

@@ -34,15 +34,17 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
   const uint64_t i = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63u;
   if (i >= m) return;
-  const int64_t t = tok[i];
-  uint64_t l = lo_in[i], h = hi_in[i];
+  const int64_t t = (int64_t)row_load_u64(tok, m, i);
+  uint64_t l = row_load_u64(lo_in, m, i), h = row_load_u64(hi_in, m, i);
+  // Every row takes the LF step, a reset row's result is replaced after it:
+  // with a branch on the token, the compiler sank the (lo, hi) loads into the
+  // non-reset side, behind the token's round trip.
+  const uint32_t* cbm;
+  int64_t one;
+  lf_step_decode(v, t + shift, l, h, cbm, one);
   if (t < reset_below) {
     l = 0;
     h = v.n;
-  } else {
-    const uint32_t* cbm;
-    int64_t one;
-    lf_step_decode(v, t + shift, l, h, cbm, one);
   }
   if (lane == 0) {
     lo_out[i] = l;
