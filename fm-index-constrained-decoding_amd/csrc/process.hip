@@ -68,9 +68,15 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
   int64_t first = -1;
   uint32_t hits = 0;
   for (int64_t i0 = 0; i0 + M <= n; i0 += 64) {
+    // all 8 candidate tokens loaded at once (clamped, unconditional) and
+    // compared after: a short-circuit compare issued one load per round trip
     const int64_t i = i0 + lane;
     bool m = i + M <= n;
-    for (int64_t j = 0; j < M && m; ++j) m = r[i + j] == cfg.marker[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t x = r[min(i + j, n - 1)];
+      m &= (j >= M) | (x == cfg.marker[j]);
+    }
     const uint64_t bal = __ballot(m);
     hits += (uint32_t)__popcll(bal);
     if (bal && first < 0) first = i0 + __ffsll((long long)bal) - 1;
@@ -112,7 +118,8 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
       bool ft = false;
       for (int64_t i0 = start; i0 + 1 < n; i0 += 64) {
         const int64_t i = i0 + lane;
-        const bool m = i + 1 < n && r[i] == cfg.think[0] && r[i + 1] == cfg.think[1];
+        const int64_t a = r[min(i, n - 1)], b = r[min(i + 1, n - 1)];
+        const bool m = (i + 1 < n) & (a == cfg.think[0]) & (b == cfg.think[1]);
         if (__ballot(m)) {
           ft = true;
           break;
@@ -123,8 +130,12 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
       } else {
         // remove_system_tokens (causal_qwen.py:58-72)
         const int64_t k = L < 4 ? L : 4;
-        bool pre = true;
-        for (int64_t j = 0; j < k; ++j) pre = pre && r[start + j] == cfg.sys[j];
+        bool pre = true;   // n >= 2 here (the think pair was found)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t x = r[min(start + j, n - 1)];
+          pre &= (j >= k) | (x == cfg.sys[j]);
+        }
         if (pre && L < 4) ls = 0;
         else if (pre) {
           s0 += 4;

@@ -105,15 +105,19 @@ class BatchContinuationResponse(BaseModel):
 class RangeBatcher:
     """Collects the patterns of concurrent requests and resolves them with one
     `index.get_ranges` call per batch.  A batch closes when `max_batch`
-    patterns are waiting or `window_s` after its first pattern arrived; the
-    search runs on the (single) index worker thread."""
+    patterns are waiting or `window_s` after its first request arrived; the
+    search runs on the (single) index worker thread.  A request's patterns
+    (one, or many for the batched routes) share one future."""
 
-    def __init__(self, index, worker: ThreadPoolExecutor, window_s: float = 2e-4, max_batch: int = 4096):
+    def __init__(self, index, worker: ThreadPoolExecutor, window_s: float = 2e-4, max_batch: int = 4096,
+                 batching: bool = True):
         self.index = index
+        self.batching = batching   # False: one search per request (the reference's serving model)
         self.worker = worker
         self.window_s = window_s
         self.max_batch = max_batch
-        self._pending: List[Tuple[List[int], asyncio.Future]] = []
+        self._pending: List[Tuple[List[List[int]], asyncio.Future]] = []
+        self._npending = 0
         self._kick: Optional[asyncio.Event] = None
         self._task: Optional[asyncio.Task] = None
         self.batches = 0          # launches issued
@@ -136,6 +140,7 @@ class RangeBatcher:
             if not fut.done():
                 fut.set_exception(RuntimeError("service shutting down"))
         self._pending = []
+        self._npending = 0
 
     async def ranges(self, seqs: List[List[int]]) -> List[Tuple[int, int]]:
         # a pattern the reference's backward_search_step rejects (a symbol
@@ -143,14 +148,19 @@ class RangeBatcher:
         for s in seqs:
             if s and min(s) + SHIFT < 0:
                 raise OverflowError("in method 'FMIndex_backward_search_step', argument 2 of type 'char_type'")
-        loop = asyncio.get_running_loop()
-        futs = []
-        for s in seqs:
-            fut = loop.create_future()
-            self._pending.append((list(s), fut))
-            futs.append(fut)
+        if not seqs:
+            return []
+        if not self.batching:
+            res = await asyncio.get_running_loop().run_in_executor(self.worker, self.index.get_ranges, seqs)
+            self.batches += 1
+            self.patterns += len(seqs)
+            self.largest = max(self.largest, len(seqs))
+            return [(int(lo), int(hi)) for lo, hi in res]
+        fut = asyncio.get_running_loop().create_future()
+        self._pending.append((seqs, fut))
+        self._npending += len(seqs)
         self._kick.set()
-        return list(await asyncio.gather(*futs))
+        return await fut
 
     async def _run(self) -> None:
         loop = asyncio.get_running_loop()
@@ -161,28 +171,36 @@ class RangeBatcher:
                 continue
             # let the requests that are already on their way join this batch
             t_end = loop.time() + self.window_s
-            while len(self._pending) < self.max_batch and loop.time() < t_end:
+            while self._npending < self.max_batch and loop.time() < t_end:
                 await asyncio.sleep(0)
-            batch, self._pending = self._pending[: self.max_batch], self._pending[self.max_batch:]
+            batch, n = [], 0
+            while self._pending and (not batch or n + len(self._pending[0][0]) <= self.max_batch):
+                req = self._pending.pop(0)
+                batch.append(req)
+                n += len(req[0])
+            self._npending -= n
             if self._pending:
                 self._kick.set()
-            seqs = [s for s, _ in batch]
+            seqs = [s for req, _ in batch for s in req]
             try:
                 res = await loop.run_in_executor(self.worker, self.index.get_ranges, seqs)
-                for (_, fut), r in zip(batch, res):
+                pos = 0
+                for req, fut in batch:
+                    part = [(int(lo), int(hi)) for lo, hi in res[pos:pos + len(req)]]
+                    pos += len(req)
                     if not fut.done():
-                        fut.set_result((int(r[0]), int(r[1])))
+                        fut.set_result(part)
             except Exception as e:          # every request of the batch gets the error (500)
                 for _, fut in batch:
                     if not fut.done():
                         fut.set_exception(e)
             self.batches += 1
-            self.patterns += len(batch)
-            self.largest = max(self.largest, len(batch))
+            self.patterns += n
+            self.largest = max(self.largest, n)
 
 
 def create_app(index=None, index_path: Optional[str] = None, window_s: float = 2e-4,
-               max_batch: int = 4096) -> FastAPI:
+               max_batch: int = 4096, batching: bool = True) -> FastAPI:
     """The service around `index` (or the index saved at `index_path` /
     $FM_INDEX_PATH, loaded at startup as in fm_index_api_service.py:68-90)."""
     state = {"index": index, "batcher": None}
@@ -197,7 +215,7 @@ def create_app(index=None, index_path: Optional[str] = None, window_s: float = 2
             t0 = time.time()
             state["index"] = await asyncio.get_running_loop().run_in_executor(worker, FMIndex.load, path)
             logger.info("FM-Index loaded from %s in %.2fs", path, time.time() - t0)
-        b = RangeBatcher(state["index"], worker, window_s, max_batch)
+        b = RangeBatcher(state["index"], worker, window_s, max_batch, batching)
         b.start()
         state["batcher"] = b
         app.state.batcher = b

@@ -1,8 +1,9 @@
 """Query-service throughput (fmidx/service.py) on a device-built index:
 /get_count requests with C clients in flight (in-process ASGI transport, so
 the HTTP stack's serialization is measured but no sockets), the batched route,
-and -- the reference's serving model, one blocking search per request
-(fm_index_api_service.py:147-161) -- `get_count` called once per pattern.
+the same service with batching off (one search per request, the reference's
+serving model, fm_index_api_service.py:147-161), and `get_count` called once
+per pattern without HTTP.
 Usage: python tools/bench_service.py [--tokens N] [--requests R] [--clients C]"""
 import argparse
 import asyncio
@@ -62,8 +63,8 @@ serial_s = time.perf_counter() - t
 assert ser == truth[: args.serial]
 
 
-async def run():
-    app = create_app(index=ix, window_s=2e-4)
+async def run(batching):
+    app = create_app(index=ix, window_s=2e-4, batching=batching)
     async with app.router.lifespan_context(app):
         tr = httpx.ASGITransport(app=app)
         async with httpx.AsyncClient(transport=tr, base_url="http://t") as c:
@@ -89,11 +90,13 @@ async def run():
             return conc_s, batch_s, st1["batches"] - st0["batches"], st1["largest_batch"]
 
 
-conc_s, batch_s, nb, largest = asyncio.run(run())
+conc_s, batch_s, nb, largest = asyncio.run(run(True))
+conc1_s, _, nb1, _ = asyncio.run(run(False))
 res = {"corpus_tokens": n, "index_build_s": round(build_s, 1), "requests": R, "clients": args.clients,
        "serial_get_count": {"calls": args.serial, "us_per_call": round(serial_s / args.serial * 1e6, 1),
                             "req_per_s": round(args.serial / serial_s)},
        "service_get_count": {"req_per_s": round(R / conc_s), "batches": nb, "mean_batch": round(R / max(nb, 1), 1),
                              "largest_batch": largest},
+       "service_get_count_unbatched": {"req_per_s": round(R / conc1_s), "searches": nb1},
        "service_get_count_batch": {"patterns_per_s": round(R / batch_s), "ms": round(batch_s * 1e3, 2)}}
 print(json.dumps(res), flush=True)
