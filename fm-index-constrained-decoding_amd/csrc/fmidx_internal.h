@@ -490,7 +490,9 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   const uint32_t q = lane & 31u;
   const bool side = lane >= 32;
   const uint64_t c = (uint64_t)sym;
-  // (1) transition probe of a cached range: 16 slots x 3 words, one word per lane 0-47
+  // (1) transition probe of a cached range: 16 slots x 3 words, one word per
+  // lane 0-47; lanes 48-63 read the parent's own home run in the range cache
+  // (8 slots x 2 words), in the same round trip
   const bool probe = v.trans_cap && hi - lo >= v.cache_min;
   const uint64_t key0 = lo | (c << kTransSymShift);
   uint64_t tw = kTransEmpty;
@@ -498,7 +500,15 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     uint64_t slot = trans_home(lo, hi, c, v.trans_cap) + lane / 3;
     if (slot >= v.trans_cap) slot -= v.trans_cap;
     tw = v.trans_tab[3 * slot + lane % 3];
+  } else if (probe && v.cache_mask) {
+    const uint32_t k = lane - 3 * kTransProbe;
+    tw = v.cache_tab[2 * ((cache_hash(lo, hi) + k / 2) & v.cache_mask) + (k & 1)];
   }
+  // A probe miss is a symbol the parent lacks -- or one of the few keys the
+  // table left out.  The parent's cached bitmap tells which: its word for c
+  // is loaded with the descent's first level, and an absent c ends the step
+  // there (one round trip after the probe instead of the whole descent).
+  uint32_t pword = ~0u;
   if (probe && v.probe_first) {   // the probe alone: one round trip of 384 B for a hit
     const uint64_t w1n = __shfl_down(tw, 1, 64);
     const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
@@ -515,6 +525,12 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
         cbm = v.cache_bm + (aux - 1) * v.bm_words;
       return;
     }
+    const uint64_t bc = __ballot(lane >= 3 * kTransProbe && ((lane - 3 * kTransProbe) & 1u) == 0 && tw == lo &&
+                                 (w1n & kMask34) == hi);
+    if (bc) {
+      const uint64_t pid = __shfl(w1n, __ffsll((long long)bc) - 1, 64) >> kCacheIdShift;
+      pword = v.cache_bm[pid * v.bm_words + (c32 >> 5)];
+    }
   }
   // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
@@ -527,6 +543,11 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   for (int l = 0; l < (int)v.NL2; ++l) {
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
     const uint64_t r = rank_w2(v.w2[l], pos, d, q);
+    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {   // the parent's bitmap lacks c
+      lo = 0;
+      hi = 0;
+      return;
+    }
     if (l == 0 && probe && !v.probe_first) {   // the probe's loads were issued before this level's
       const uint64_t w1n = __shfl_down(tw, 1, 64);
       const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);

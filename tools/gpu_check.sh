@@ -3,7 +3,8 @@
 # (optionally) its rocprofv3 kernel-trace summary, each under its own time
 # limit.  A test FAILURE (pytest rc 1) still lets the later steps run; a
 # crash, abort, fault or time-out (any other non-zero rc) ends the pass.
-# usage: tools/gpu_check.sh <tag> [tests|smoke|bench|prof]...   (default: all four)
+# usage: tools/gpu_check.sh <tag> [tests|smoke|bench|prof|c2|c5|pmc|pmc_c2|service|proc]...
+#        (default: tests smoke bench prof)
 set -uo pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -23,6 +24,17 @@ for s in "${STEPS[@]}"; do
     bench) timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || exit $?
            cat "$OUT/bench.log" | grep -v amdgpu.ids ;;
     prof)  timeout -k 10 600 tools/profile_bench.sh "$OUT/prof" --no-gather || exit $? ;;
+    c2)    timeout -k 10 300 python -u bench.py --tokens 3e8 --batch 32 --no-gather > "$OUT/c2.json" 2> "$OUT/c2.log" || exit $?
+           grep "step cold" "$OUT/c2.log" ;;
+    c5)    timeout -k 10 300 python -u bench.py --tokens 1.5e9 --batch 2048 --no-gather > "$OUT/c5.json" 2> "$OUT/c5.log" || exit $?
+           grep "step cold" "$OUT/c5.log" ;;
+    pmc)   timeout -k 10 600 tools/pmc_traffic.sh "$OUT/pmc_c3" --no-gather || exit $?
+           cat "$OUT/pmc_c3/pmc_traffic.json" ;;
+    pmc_c2) timeout -k 10 600 tools/pmc_traffic.sh "$OUT/pmc_c2" --tokens 3e8 --batch 32 --no-gather || exit $? ;;
+    service) timeout -k 10 300 python -u tools/bench_service.py > "$OUT/service.json" 2> "$OUT/service.log" || exit $?
+           cat "$OUT/service.json" ;;
+    proc)  timeout -k 10 300 python -u tools/bench_processor.py > "$OUT/proc.json" 2> "$OUT/proc.log" || exit $?
+           cat "$OUT/proc.json" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
