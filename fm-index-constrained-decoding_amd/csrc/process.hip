@@ -21,7 +21,8 @@ namespace fmidx {
 
 namespace {
 
-constexpr int kThreads = 256;   // 4 rows per workgroup, one wave each
+constexpr int64_t kStageBatch = 512;           // row tokens staged per batch (8 loads per lane in flight)
+constexpr int64_t kMaxStaged = 6144;           // rows up to this many tokens are staged in LDS (48 KB)
 enum Kind : uint32_t { kNone = 0, kUni = 1, kSpecial = 2, kBits = 3 };
 
 // all 64 lanes: a[j] == b[j] for j < len
@@ -49,27 +50,57 @@ __device__ __forceinline__ float pow_at(const float* tab, uint64_t len, int64_t 
   return x;
 }
 
-__global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg, const int64_t* __restrict__ ids,
-                                                   uint64_t B, uint64_t Lt, uint64_t ld, const int64_t* __restrict__ fdf,
-                                                   uint64_t fdf_len, const float* __restrict__ pow_tab, uint64_t pow_len,
-                                                   const int64_t* __restrict__ prev_ids, uint64_t prev_ld,
-                                                   uint64_t prev_B, const int64_t* __restrict__ prev_state,
-                                                   fm_row_params* __restrict__ rows, uint64_t* __restrict__ mlo,
-                                                   uint64_t* __restrict__ mhi, int64_t* __restrict__ state,
-                                                   uint32_t* __restrict__ status) {
-  const uint64_t row = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63u;
-  if (row >= B) return;
-  const int64_t* r = ids + row * ld;
+// Round trips: the row's ids (staged into LDS when they fit) and the row's
+// previous state are loaded together first; the end marker, think pair and
+// system prefix are then scanned in LDS.  The LF step from the previous range
+// is issued speculatively together with the token compare that validates it,
+// and the C lookup (count([last]) == 0) is made only for eos / pad rows and
+// rows whose range came out empty -- a non-empty range implies count > 0.
+template <bool STAGED>
+__global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, const int64_t* __restrict__ ids,
+                                             uint64_t B, uint64_t Lt, uint64_t ld, const int64_t* __restrict__ fdf,
+                                             uint64_t fdf_len, const float* __restrict__ pow_tab, uint64_t pow_len,
+                                             const int64_t* __restrict__ prev_ids, uint64_t prev_ld,
+                                             uint64_t prev_B, const int64_t* __restrict__ prev_state,
+                                             fm_row_params* __restrict__ rows, uint64_t* __restrict__ mlo,
+                                             uint64_t* __restrict__ mhi, int64_t* __restrict__ state,
+                                             uint32_t* __restrict__ status) {
+  extern __shared__ int64_t srow[];   // STAGED: [npad] the row, then [4] its previous state
+  const uint64_t row = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const int64_t* g = ids + row * ld;
   const int64_t n = (int64_t)Lt;
+  const int64_t npad = (n + kStageBatch - 1) / kStageBatch * kStageBatch;
+  const bool have_prev = prev_ids && row < prev_B;
+  int64_t ps[4] = {-1, -1, 0, 0};   // previous (start, len, lo, hi) of this row
+  if (STAGED) {
+    // every load issued before any is stored: clamped, unconditional
+    int64_t y = -1;
+    if (have_prev && lane < 4) y = prev_state[lane * prev_B + row];
+    for (int64_t i0 = 0; i0 < n; i0 += kStageBatch) {
+      int64_t x[kStageBatch / 64];
+#pragma unroll
+      for (int u = 0; u < kStageBatch / 64; ++u) x[u] = g[min(i0 + u * 64 + (int64_t)lane, n - 1)];
+#pragma unroll
+      for (int u = 0; u < kStageBatch / 64; ++u) srow[i0 + u * 64 + lane] = x[u];
+    }
+    if (lane < 4) srow[npad + lane] = y;
+    __syncthreads();
+    if (have_prev) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ps[k] = srow[npad + k];
+    }
+  } else if (have_prev) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ps[k] = prev_state[k * prev_B + row];
+  }
+  const int64_t* r = STAGED ? srow : g;
   uint32_t bad = 0;
   // remove_end_marker (causal_qwen.py:44-56): the tokens after the marker
   const int64_t M = cfg.marker_len;
   int64_t first = -1;
   uint32_t hits = 0;
   for (int64_t i0 = 0; i0 + M <= n; i0 += 64) {
-    // all 8 candidate tokens loaded at once (clamped, unconditional) and
-    // compared after: a short-circuit compare issued one load per round trip
     const int64_t i = i0 + lane;
     bool m = i + M <= n;
 #pragma unroll
@@ -147,10 +178,15 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
       // get_trailing_corpus_ngram: only count([last]) matters (causal_qwen.py:95-99)
       const int64_t last = r[s0 + ls - 1];
       const int64_t c = last + cfg.shift;
-      const uint64_t cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
-      if (cnt1 == 0) {
+      bool counted = false;   // cnt1 known
+      uint64_t cnt1 = 0;
+      if (last == cfg.eos || last == cfg.pad) {
+        cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
+        counted = true;
+      }
+      if (counted && cnt1 == 0) {
         ls = 0;
-      } else if (last == cfg.eos || last == cfg.pad) {   // count 0 (causal_qwen.py:125-128, 161-174)
+      } else if (counted) {   // count 0 (causal_qwen.py:125-128, 161-174)
         kind = kSpecial;
         p.special = (cfg.stop_at_count > 0) ? cfg.eos : cfg.pad;
       } else {
@@ -161,8 +197,25 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
         if (prev_ids && ls >= 2) {
           const uint64_t beams = cfg.num_beams > 0 ? (uint64_t)cfg.num_beams : 1;
           const uint64_t g0 = row / beams * beams;
-          for (uint64_t k = 0; k < beams && !found; ++k) {
-            const uint64_t b2 = k == 0 ? row : (g0 + k - 1 < row ? g0 + k - 1 : g0 + k);
+          // the row itself first: the LF step from its previous range is issued
+          // with the first chunk of the token compare that validates it
+          if (have_prev && ps[1] == ls - 1 && ps[0] >= 0) {
+            const int64_t* pr = prev_ids + row * prev_ld + ps[0];
+            const int64_t x = lane < ls - 1 ? pr[lane] : 0;
+            uint64_t l2 = (uint64_t)ps[2], h2 = (uint64_t)ps[3];
+            const uint32_t* cbm;
+            int64_t one;
+            lf_step_decode(v, c, l2, h2, cbm, one);
+            bool eq = !__ballot(lane < ls - 1 && x != r[s0 + lane]);
+            if (eq && ls - 1 > 64) eq = wave_equal(pr + 64, r + s0 + 64, ls - 1 - 64);
+            if (eq) {
+              lo = l2;
+              hi = h2;
+              found = true;
+            }
+          }
+          for (uint64_t k = 1; k < beams && !found; ++k) {
+            const uint64_t b2 = g0 + k - 1 < row ? g0 + k - 1 : g0 + k;
             if (b2 >= prev_B || b2 >= g0 + beams) continue;
             const int64_t pstart = prev_state[b2], plen = prev_state[prev_B + b2];
             if (plen != ls - 1 || pstart < 0) continue;
@@ -171,7 +224,7 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
               hi = (uint64_t)prev_state[3 * prev_B + b2];
               const uint32_t* cbm;
               int64_t one;
-              lf_step_decode(v, last + cfg.shift, lo, hi, cbm, one);
+              lf_step_decode(v, c, lo, hi, cbm, one);
               found = true;
             }
           }
@@ -180,20 +233,31 @@ __global__ void __launch_bounds__(kThreads) k_prep(DevView v, fm_prep_config cfg
           lo = 0;
           hi = v.n;
           for (int64_t j = 0; j < (int64_t)fdf_len + ls; ++j) {
-            const int64_t t = j < (int64_t)fdf_len ? fdf[j] : r[s0 + j - (int64_t)fdf_len];
+            // both candidates loaded from their own address spaces (a select of
+            // the pointers would make one generic pointer and FLAT loads)
+            const int64_t jf = j < (int64_t)fdf_len ? j : 0, jr = j < (int64_t)fdf_len ? 0 : j - (int64_t)fdf_len;
+            const int64_t tf = fdf_len ? fdf[jf] : 0, tr = r[s0 + jr];
+            const int64_t t = j < (int64_t)fdf_len ? tf : tr;
             const uint32_t* cbm;
             int64_t one;
             lf_step_decode(v, t + cfg.shift, lo, hi, cbm, one);
             if (lo == 0 && hi == 0) break;   // index.py:111-112
           }
         }
-        pattern = true;
-        const uint64_t count = hi - lo;
-        if (cfg.stop_at_count > 0 && count <= (uint64_t)cfg.stop_at_count) {
-          kind = kSpecial;
-          p.special = cfg.eos;
+        // a non-empty range implies count([last]) > 0; an empty one asks C
+        if (hi <= lo) cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
+        if (hi <= lo && cnt1 == 0) {
+          ls = 0;
+          lo = hi = 0;
         } else {
-          kind = kBits;
+          pattern = true;
+          const uint64_t count = hi - lo;
+          if (cfg.stop_at_count > 0 && count <= (uint64_t)cfg.stop_at_count) {
+            kind = kSpecial;
+            p.special = cfg.eos;
+          } else {
+            kind = kBits;
+          }
         }
       }
     }
@@ -252,9 +316,14 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
   FM_HIP(hipMemsetAsync(status, 0, 16, s));
   FM_HIP(hipMemsetAsync(status + 1, 0xFF, 4, s));
   if (B == 0) return 0;
-  k_prep<<<(unsigned)((B * 64 + kThreads - 1) / kThreads), kThreads, 0, s>>>(
-      v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids, prev_ld, prev_B, prev_state, rows, mlo, mhi,
-      state, status);
+  if (L <= (uint64_t)kMaxStaged) {
+    const size_t lds = ((L + kStageBatch - 1) / kStageBatch * kStageBatch + 4) * sizeof(int64_t);
+    k_prep<true><<<(unsigned)B, 64, lds, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
+                                              prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status);
+  } else {
+    k_prep<false><<<(unsigned)B, 64, 0, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
+                                             prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status);
+  }
   FM_HIP(hipGetLastError());
   return 0;
 }
