@@ -1085,6 +1085,35 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
                                       d_state, d_status, reinterpret_cast<hipStream_t>(stream));
 }
 
+int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* a, void* stream) {
+  static_assert(sizeof(fm_processor_args) == 240, "fm_processor_args layout");
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  if (!cfg || !a) {
+    set_error("null config or arguments");
+    return -1;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // 1. row bookkeeping + pattern ranges
+  if (fmidx::launch_processor_step(h->idx.view, *cfg, a->ids, a->B, a->L, a->ld, a->fdf, a->fdf_len, a->pow_tab,
+                                   a->pow_len, a->prev_ids, a->prev_ld, a->prev_B, a->prev_state, a->rows, a->mask_lo,
+                                   a->mask_hi, a->state, a->status, s))
+    return -1;
+  // 2. the allowed bits of the rows that need them (empty ranges give zero rows)
+  if (a->B && fmidx::launch_mask(h->idx.view, a->mask_lo, a->mask_hi, a->B, reinterpret_cast<uint8_t*>(a->bits),
+                                 a->bits_ld * 4, a->V, cfg->shift, 1, s))
+    return -1;
+  // 3. scores + mask
+  if (a->B && fmidx::launch_epilogue(a->dtype, a->scores, a->out, a->B, a->V, a->ld_scores, a->ld_out, a->bits,
+                                     a->bits_ld, a->unigram_bits, a->rows, a->eos, s))
+    return -1;
+  // 4. this call's ids for the next call's incremental ranges, and the status to the host
+  if (a->ids_copy && a->B && a->L)
+    FM_HIP(hipMemcpy2DAsync(a->ids_copy, a->copy_ld * 8, a->ids, a->ld * 8, a->L * 8, a->B, hipMemcpyDeviceToDevice, s));
+  if (a->status_host) FM_HIP(hipMemcpyAsync(a->status_host, a->status, 16, hipMemcpyDeviceToHost, s));
+  return 0;
+}
+
 int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
                uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream) {
   return fmidx::launch_or_bits(d_parts, nparts, part_stride, B, words_per_row, vocab, d_out, ld_out, unpack,

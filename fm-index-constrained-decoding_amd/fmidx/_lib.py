@@ -63,6 +63,7 @@ SIGNATURES = {
     "fm_processor_step": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint64,
                                   c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fm_processor_call": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_or_bits": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p, c_uint64, c_int,
                             c_void_p]),
     "fm_probe_gather": (c_int, [c_void_p, c_uint64, c_int, c_uint64, c_uint32, c_void_p, c_void_p]),

@@ -26,7 +26,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import math
-from ctypes import c_float, c_int32, c_int64, c_uint32, c_void_p
+from ctypes import c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -79,15 +79,32 @@ def _boost_table(boost: float, lrf: float, dtype, n: int) -> List[float]:
     return out
 
 
+class _ProcessorArgs(ctypes.Structure):
+    """fm_processor_args (include/fmidx.h)."""
+    _fields_ = [("ids", c_void_p), ("B", c_uint64), ("L", c_uint64), ("ld", c_uint64), ("fdf", c_void_p),
+                ("fdf_len", c_uint64), ("pow_tab", c_void_p), ("pow_len", c_uint64), ("prev_ids", c_void_p),
+                ("prev_ld", c_uint64), ("prev_B", c_uint64), ("prev_state", c_void_p), ("rows", c_void_p),
+                ("mask_lo", c_void_p), ("mask_hi", c_void_p), ("state", c_void_p), ("status", c_void_p),
+                ("bits", c_void_p), ("bits_ld", c_uint64), ("dtype", c_int32), ("reserved", c_int32),
+                ("scores", c_void_p), ("out", c_void_p), ("V", c_uint64), ("ld_scores", c_uint64),
+                ("ld_out", c_uint64), ("unigram_bits", c_void_p), ("eos", c_int64), ("ids_copy", c_void_p),
+                ("copy_ld", c_uint64), ("status_host", c_void_p)]
+
+
+assert ctypes.sizeof(_ProcessorArgs) == 240
+
+
 class _DeviceStep:
-    """One soft-processor call on the device: fm_processor_step (per-row
-    bookkeeping + pattern ranges, csrc/process.hip), the packed allowed bits of
-    the rows that need them, the fused epilogue.  Keeps the previous call's
-    input_ids and per-row (pattern, range) state on the device so a row whose
-    pattern grew by one token costs ONE LF step.  Returns None when a row does
-    not have exactly one end marker at a common position (or a boost overflows):
-    the caller then runs the host path, which reproduces the reference's
-    behaviour for such inputs."""
+    """One soft-processor call on the device, ONE C call (fm_processor_call):
+    the per-row bookkeeping + pattern ranges (csrc/process.hip), the packed
+    allowed bits of the rows that need them, the fused epilogue, this call's
+    input_ids kept for the next call and the status copied to pinned memory.
+    Buffers persist across calls (the row state and the kept ids ping-pong
+    between two sets), so a row whose pattern grew by one token costs ONE LF
+    step and a call allocates only its output.  Returns None when a row does
+    not have exactly one end marker at a common position (or a boost
+    overflows): the caller then runs the host path, which reproduces the
+    reference's behaviour for such inputs."""
 
     def __init__(self, core: "_BatchedCore", boost: float, lrf: float, fdf: Optional[List[int]]):
         self.core = core
@@ -98,11 +115,16 @@ class _DeviceStep:
         self.fdf = torch.tensor(list(fdf or []) + [0], dtype=torch.int64, device=self.dev)
         self.fdf_len = len(fdf or [])
         self._pow = {}
-        self.prev_ids = None          # device [B, Lcap] of the last call
-        self.prev_state = None
-        self.prev_B = 0
         self.status = torch.zeros(4, dtype=torch.int32, device=self.dev)
         self.status_h = torch.zeros(4, dtype=torch.int32).pin_memory()
+        self._status_np = self.status_h.numpy()
+        self._args = _ProcessorArgs()
+        self._B = -1
+        self._bufs = None
+        self._ids = [None, None]      # kept input_ids, ping-pong
+        self._state = [None, None]
+        self._cur = 0                 # the set the next call writes
+        self._prev_ok = False         # the other set holds a valid previous call
 
     def _pow_table(self, dtype, need: int):
         t = self._pow.get(dtype)
@@ -112,43 +134,71 @@ class _DeviceStep:
             self._pow[dtype] = t
         return t
 
+    def _buffers(self, B: int, V: int):
+        words = (V + 31) // 32
+        if self._bufs is None or self._B != B or self._bufs["words"] < words:
+            dev = self.dev
+            self._bufs = {"rows": torch.empty(B * ROW_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+                          "mlo": torch.empty(B, dtype=torch.int64, device=dev),
+                          "mhi": torch.empty(B, dtype=torch.int64, device=dev),
+                          "bits": torch.empty((B, words), dtype=torch.int32, device=dev), "words": words}
+            self._state = [torch.empty((4, B), dtype=torch.int64, device=dev) for _ in range(2)]
+            self._B = B
+            self._prev_ok = False
+        return self._bufs
+
     def __call__(self, input_ids, scores, cfg: _PrepConfig):
         dev = self.dev
-        ids = input_ids.to(dev, torch.int64).contiguous()
+        ids = input_ids if (input_ids.device == dev and input_ids.dtype == torch.int64
+                            and input_ids.is_contiguous()) else input_ids.to(dev, torch.int64).contiguous()
         if ids.dim() != 2:
             return None
         B, Lt = ids.shape
         if B != scores.shape[0] or B % max(1, cfg.num_beams):
             return None
+        dtype = scores.dtype
+        if dtype not in _DTYPE_CODE:
+            raise TypeError(f"unsupported scores dtype {dtype}")
         V = scores.shape[1]
-        pow_t = self._pow_table(scores.dtype, Lt + 1)
-        rows = torch.empty(B * ROW_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        mlo = torch.empty(B, dtype=torch.int64, device=dev)
-        mhi = torch.empty(B, dtype=torch.int64, device=dev)
-        state = torch.empty((4, B), dtype=torch.int64, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        prev = self.prev_ids
-        with torch.cuda.device(dev):
-            check(lib().fm_processor_step(
-                self.index._h, ctypes.byref(cfg), c_void_p(ids.data_ptr()), B, Lt, Lt,
-                c_void_p(self.fdf.data_ptr()), self.fdf_len, c_void_p(pow_t.data_ptr()), pow_t.numel(),
-                c_void_p(prev.data_ptr()) if prev is not None else None, prev.stride(0) if prev is not None else 0,
-                self.prev_B if prev is not None else 0,
-                c_void_p(self.prev_state.data_ptr()) if prev is not None else None,
-                c_void_p(rows.data_ptr()), c_void_p(mlo.data_ptr()), c_void_p(mhi.data_ptr()),
-                c_void_p(state.data_ptr()), c_void_p(self.status.data_ptr()), c_void_p(stream)), "processor_step")
-            bits = self.index.allowed_mask(mlo, mhi, V, SHIFT, packed=True)
-            out = self.core.epilogue_device(scores, rows, bits, int(cfg.eos))
-            self.status_h.copy_(self.status, non_blocking=True)
-            torch.cuda.current_stream(dev).synchronize()
-        st = self.status_h.tolist()
+        src = scores if (scores.device == dev and scores.is_contiguous()) else scores.to(dev).contiguous()
+        out = torch.empty_like(src)
+        pow_t = self._pow_table(dtype, Lt + 1)
+        bufs = self._buffers(B, V)
+        cur, oth = self._cur, 1 - self._cur
+        keep = self._ids[cur]
+        if keep is None or keep.shape[0] != B or keep.shape[1] < Lt:
+            keep = torch.empty((B, max(Lt + 64, 2 * (keep.shape[1] if keep is not None else 0))), dtype=torch.int64,
+                               device=dev)
+            self._ids[cur] = keep
+        prev = self._ids[oth] if self._prev_ok else None
+        a = self._args
+        a.ids, a.B, a.L, a.ld = ids.data_ptr(), B, Lt, Lt
+        a.fdf, a.fdf_len = self.fdf.data_ptr(), self.fdf_len
+        a.pow_tab, a.pow_len = pow_t.data_ptr(), pow_t.numel()
+        if prev is not None:
+            a.prev_ids, a.prev_ld, a.prev_B, a.prev_state = prev.data_ptr(), prev.stride(0), prev.shape[0], \
+                self._state[oth].data_ptr()
+        else:
+            a.prev_ids, a.prev_ld, a.prev_B, a.prev_state = None, 0, 0, None
+        a.rows, a.mask_lo, a.mask_hi = bufs["rows"].data_ptr(), bufs["mlo"].data_ptr(), bufs["mhi"].data_ptr()
+        a.state, a.status = self._state[cur].data_ptr(), self.status.data_ptr()
+        a.bits, a.bits_ld = bufs["bits"].data_ptr(), bufs["words"]
+        a.dtype = _DTYPE_CODE[dtype]
+        a.scores, a.out, a.V, a.ld_scores, a.ld_out = src.data_ptr(), out.data_ptr(), V, src.stride(0), out.stride(0)
+        a.unigram_bits = self.core.unigram_bits(V, dev).data_ptr()
+        a.eos = int(cfg.eos)
+        a.ids_copy, a.copy_ld = keep.data_ptr(), keep.stride(0)
+        a.status_host = self.status_h.data_ptr()
+        stream = torch.cuda.current_stream(dev)
+        check(lib().fm_processor_call(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
+                                      c_void_p(stream.cuda_stream)), "processor_call")
+        stream.synchronize()
+        st = self._status_np
         if st[0] != 0 or st[1] != st[2]:
-            self.prev_ids = None
+            self._prev_ok = False
             return None
-        self.prev_ids = ids.clone()     # the caller may reuse its input_ids buffer
-        self.prev_state = state
-        self.prev_B = B
-        return out
+        self._cur, self._prev_ok = oth, True
+        return out if out.device == scores.device else out.to(scores.device)
 
 
 class _BatchedCore:

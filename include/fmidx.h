@@ -303,6 +303,45 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
                       fm_row_params* d_rows, uint64_t* d_mask_lo, uint64_t* d_mask_hi, int64_t* d_state,
                       uint32_t* d_status, void* stream);
 
+/* One whole soft-processor call (the three launches of the device path plus
+ * the hand-offs), so the host makes one call per decode step:
+ *   fm_processor_step -> fm_allowed_mask_batch(packed) of (mask_lo, mask_hi)
+ *   into bits -> fm_apply_boosts(scores -> out) -> ids copied to ids_copy (the
+ *   next call's prev_ids, optional) -> status copied to status_host (pinned,
+ *   optional).  Stream-ordered; the caller synchronizes before reading
+ *   status_host.  Replaces the per-call work of
+ *   document_constrained_generation_causal_qwen.py:101-214 / causal.py:62-180. */
+typedef struct fm_processor_args {
+  const int64_t* ids;          /* [B][ld] input_ids */
+  uint64_t B, L, ld;
+  const int64_t* fdf;          /* force_decoding_from tokens */
+  uint64_t fdf_len;
+  const float* pow_tab;        /* boost table (fm_processor_step) */
+  uint64_t pow_len;
+  const int64_t* prev_ids;     /* previous call's ids [prev_B][prev_ld], or null */
+  uint64_t prev_ld, prev_B;
+  const int64_t* prev_state;   /* previous call's state [4][prev_B] */
+  fm_row_params* rows;         /* [B] out */
+  uint64_t* mask_lo;           /* [B] out */
+  uint64_t* mask_hi;           /* [B] out */
+  int64_t* state;              /* [4][B] out */
+  uint32_t* status;            /* [4] device */
+  uint32_t* bits;              /* [B][bits_ld] packed allowed bits (scratch) */
+  uint64_t bits_ld;            /* uint32 words per row, >= ceil(V/32) */
+  int32_t dtype;               /* of scores / out: 0 = f32, 1 = bf16, 2 = f16 */
+  int32_t reserved;
+  const void* scores;          /* [B][ld_scores] */
+  void* out;                   /* [B][ld_out] */
+  uint64_t V, ld_scores, ld_out;
+  const uint32_t* unigram_bits;
+  int64_t eos;
+  int64_t* ids_copy;           /* [B][copy_ld] or null */
+  uint64_t copy_ld;
+  uint32_t* status_host;       /* pinned [4] or null */
+} fm_processor_args;
+
+int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* args, void* stream);
+
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
 /* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip
