@@ -126,6 +126,12 @@ class _DeviceStep:
         self._cur = 0                 # the set the next call writes
         self._prev_ok = False         # the other set holds a valid previous call
 
+    @property
+    def prev_ids(self):
+        """The previous call's input_ids as kept on the device (None after a
+        host-path call or before the first call)."""
+        return self._ids[1 - self._cur] if self._prev_ok else None
+
     def _pow_table(self, dtype, need: int):
         t = self._pow.get(dtype)
         if t is None or t.numel() < need:
