@@ -170,7 +170,7 @@ def index_from_sequences(sequences: Iterable[Sequence[int]], device: Optional[in
     index = FMIndex(device=device)
     dev = torch.device("cuda", index.device)
     text = torch.from_numpy(corpus.text().view(np.int32)).to(dev)
-    index.initialize_from_text_device(text)
+    index.initialize_from_text_device(text, keep_sa_text=True)   # SA kept only to sample it (locate / get_doc)
     del text
     index.beginnings = corpus.beginnings
     index.occurring = sorted(corpus.occurring)
