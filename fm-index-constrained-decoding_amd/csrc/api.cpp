@@ -47,6 +47,8 @@ void Index::release() {
   if (w2_Z) (void)hipFree(w2_Z);
   if (E) (void)hipFree(E);
   E = nullptr;
+  if (E2) (void)hipFree(E2);
+  E2 = nullptr;
   if (cache_bm) (void)hipFree(cache_bm);
   if (cache_tab) (void)hipFree(cache_tab);
   if (trans_tab) (void)hipFree(trans_tab);
@@ -1017,7 +1019,7 @@ int fm_extract_batch(fm_index* h, const uint64_t* d_begin, const uint64_t* d_end
 int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, uint64_t* total_bytes) {
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
-  const uint64_t e = x.E ? x.n * 8 : 0;
+  const uint64_t e = (x.E ? x.n * 8 : 0) + (x.E2 ? x.n * 4 : 0);
   const uint64_t K = (1ull << x.L) + 1;
   if (e_bytes) *e_bytes = e;
   if (sample_bytes) *sample_bytes = x.samp_bytes;

@@ -381,6 +381,13 @@ __global__ void __launch_bounds__(kThreads) k_write_e(const uint64_t* __restrict
     E[pos[k]] = (base + k) | ((uint64_t)(key[k] + c0) << kESymShift);
 }
 
+// E2[i] = BWT[LF(i)]
+__global__ void __launch_bounds__(kThreads) k_write_e2(const uint64_t* __restrict__ E, const uint32_t* __restrict__ bwt,
+                                                      uint64_t n, uint32_t* __restrict__ E2) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads)
+    E2[i] = bwt[E[i] & kELfMask];
+}
+
 template <typename T>
 int dmalloc(T** p, size_t count) {
   *p = nullptr;
@@ -779,6 +786,21 @@ int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s)
   FM_HIP(hipFree(key2));
   FM_HIP(hipFree(d_cnt));
   h->view.E = h->E;
+  // E2 (FMIDX_LF_E2=1, off by default): the decode kernel's narrow rows read
+  // their new range's content with the LF scan instead of streaming it after
+  // the plan.  Measured (profiles/r02_cold_sweep/r02e2b_*): C3 13.5 vs 13.4 us
+  // cold, C2 8.4 vs 8.5, C5 46.7 vs 48.1 -- the second array's cold misses
+  // lengthen the scan about as much as the stream round trip it removes, so
+  // its 4n bytes (17 GiB at C3) are not spent by default.
+  h->view.E2 = nullptr;
+  if (env_u32("FMIDX_LF_E2", 0) != 0) {
+    if (dmalloc(&h->E2, n)) return -1;
+    k_write_e2<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 18), kThreads, 0, s>>>(
+        h->E, d_bwt, n, h->E2);
+    FM_HIP(hipGetLastError());
+    FM_HIP(hipStreamSynchronize(s));
+    h->view.E2 = h->E2;
+  }
   return 0;
 }
 

@@ -415,7 +415,12 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     lds_barrier();
   }
   // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
-  // (all 64 lanes), published with the range by a single barrier.
+  // (all 64 lanes), published with the range by a single barrier.  A range
+  // whose LF step was an E scan gets its content with the scan (E2): wave 0
+  // keeps the matched entries' symbols in registers and sets their bits after
+  // the barrier -- nothing is planned or streamed for it.
+  uint32_t content[kENarrow / 64];
+  uint32_t cmask = 0;
   if (threadIdx.x < 64) {
     uint64_t l = st_lo, h = st_hi;
     int64_t follow = -1;
@@ -435,7 +440,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
           l = b ? (a & kELfMask) : 0;
           h = b ? (b & kELfMask) + 1 : 0;
         } else {
-          lf_step_decode(v, t + shift, l, h, tbm, one);
+          lf_step_decode<true>(v, t + shift, l, h, tbm, one, content, &cmask);
         }
         if (l >= h) follow = -1;
         FM_STAMP(v, 2);
@@ -453,7 +458,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       plan.nb = 0;
       plan.a0 = plan.b0 = plan.a1 = plan.b1 = 0;
     }
-    if (l < h && one < 0) {
+    if (l < h && one < 0 && !(cmask & kContentPath)) {
       // a wide range is looked up in the range-bitmap cache first (one
       // bitmap, nothing streamed); otherwise the aligned-bitmap plan
       const uint32_t* cb = tbm ? tbm : cache_find(v, l, h);
@@ -533,6 +538,11 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       if (threadIdx.x < nthr)
         stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
       if (threadIdx.x == 0 && (int64_t)s_lohi[2] >= 0) set_bit(win, (uint32_t)s_lohi[2], base_bit, lim);   // one-row range
+      if (cmask & kContentPath) {   // wave 0: the content read with the E scan
+#pragma unroll
+        for (uint32_t j = 0; j < kENarrow / 64; ++j)
+          if ((cmask >> j) & 1u) set_bit(win, content[j], base_bit, lim);
+      }
       FM_STAMP(v, 4);
     } else {
       // The first batch of bitmap words (<= 8 per thread) is loaded before the

@@ -51,6 +51,7 @@ constexpr uint32_t kESymShift = 36;
 constexpr uint64_t kELfMask = (1ull << kESymShift) - 1;
 constexpr uint32_t kENarrow = 512;             // widest range whose LF step scans E (8 entries per lane)
 constexpr uint32_t kEWide = 4096;              // widest range the decode kernel's workgroup scans E for
+constexpr uint32_t kContentPath = 1u << 31;    // lf_step_decode<true>: the content came with the E scan
 
 // One level of the 2-level wavelet matrix.  Block b (digits [1024 b, 1024 b +
 // 1024)) = [R x uint16 count of each digit before the block, relative to its
@@ -95,6 +96,7 @@ struct DevView {
   uint64_t trans_cap;         // slots; 0 = none
   const uint32_t* cblock;     // per symbol c: cache id + 1 of its C-block [C[c], C[c+1]) (0 = not cached), or null
   const uint64_t* E;          // [n] LF(i) | BWT[i] << kESymShift (narrow-range LF + streaming), or null
+  const uint32_t* E2;         // [n] BWT[LF(i)]: the content of a narrow range's LF image, read with E, or null
   W2Level w2[kW2MaxLevels];   // 2-level wavelet matrix (LF path)
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
   uint32_t NL2;               // its levels (0 = not built)
@@ -162,7 +164,7 @@ struct DevView {
                  "s"((v).bm_count[0]), "s"((v).L), "s"((v).NL), "s"((v).max_sym), "s"((v).bm_words),       \
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
-                 "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).trans_tab),                  \
+                 "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).E2), "s"((v).trans_tab),                  \
                  "s"((v).trans_cap), "s"((v).cblock), "s"((v).probe_first));                                               \
     asm volatile("" ::"s"((v).w2[0].blocks), "s"((v).w2[0].sb), "s"((v).w2[0].Z), "s"((v).w2[0].blk_bytes), \
                  "s"((v).w2[0].bits), "s"((v).w2[0].shift));                                               \
@@ -338,7 +340,12 @@ __device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32
 // the previous decode step streamed): the occurrences of c map to consecutive
 // LF values, so the new range is [LF(first c), LF(last c) + 1).
 // (precondition: v.E, 0 < hi - lo <= kENarrow, hi <= n, 0 <= sym <= max_sym)
-__device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi) {
+// CONTENT: also read E2 with E, and return in content[j] / bit j of cmask the
+// symbols BWT[LF(i)] of this lane's matching entries -- the new range's whole
+// content (LF maps the matches onto it one to one), with no further load.
+template <bool CONTENT>
+__device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
+                                             uint32_t* content, uint32_t& cmask) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t c = (uint64_t)sym;
   uint64_t e[kENarrow / 64];
@@ -348,7 +355,20 @@ __device__ __forceinline__ void lf_step_fast(const DevView& v, int64_t sym, uint
     // into a branch with a vmcnt(0) behind it (one round trip per j)
     const uint64_t idx = lo + lane + 64 * j;
     const uint64_t x = v.E[idx < hi ? idx : hi - 1];
+    if (CONTENT) content[j] = v.E2[idx < hi ? idx : hi - 1];
     e[j] = x | (idx < hi ? 0ull : ~0ull);
+  }
+  if (CONTENT) {
+    // the E2 words are consumed here, with E's (zeroed unless matched): left
+    // unused until the emit, their loads were sunk past the plan barrier --
+    // one more round trip, which is what E2 exists to remove
+    cmask = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kENarrow / 64; ++j) {
+      const bool m = e[j] != ~0ull && (e[j] >> kESymShift) == c;
+      cmask |= m ? (1u << j) : 0u;
+      content[j] = m ? content[j] : 0u;
+    }
   }
   uint64_t fmin = ~0ull, fmax = 0, lfmin = 0, lfmax = 0;   // first / last match (relative index + 1)
 #pragma unroll
@@ -463,10 +483,13 @@ __host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi
 //     -- a hit ends the step after one round trip and names the child's
 //     bitmap in *cbm (else null) or, for a one-row child, its only symbol in
 //     *one (else -1).
+template <bool CONTENT = false>
 __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, uint64_t& lo, uint64_t& hi,
-                                               const uint32_t*& cbm, int64_t& one) {
+                                               const uint32_t*& cbm, int64_t& one, uint32_t* content = nullptr,
+                                               uint32_t* cmask = nullptr) {
   cbm = nullptr;
   one = -1;
+  if (CONTENT) *cmask = 0;
   if (hi > v.n) hi = v.n;
   if (lo >= hi || sym < 0 || (uint64_t)sym > v.max_sym) {
     lo = 0;
@@ -483,7 +506,13 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     return;
   }
   if (v.E && hi - lo <= kENarrow) {
-    lf_step_fast(v, sym, lo, hi);
+    uint32_t cm = 0;
+    if (CONTENT && v.E2) {
+      lf_step_fast<true>(v, sym, lo, hi, content, cm);
+      *cmask = cm | kContentPath;
+    } else {
+      lf_step_fast<false>(v, sym, lo, hi, nullptr, cm);
+    }
     return;
   }
   const uint32_t lane = threadIdx.x & 63u;
@@ -615,6 +644,7 @@ struct Index {
   uint64_t* w2_sb[kW2MaxLevels] = {nullptr, nullptr, nullptr};
   uint64_t* w2_Z = nullptr;
   uint64_t* E = nullptr;
+  uint32_t* E2 = nullptr;
   uint32_t* cache_bm = nullptr;
   uint64_t* cache_tab = nullptr;
   uint64_t* trans_tab = nullptr;

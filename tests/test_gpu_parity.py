@@ -224,10 +224,13 @@ def test_incremental_lf_equals_full_research(dev):
         assert got == want, s
 
 
-@pytest.mark.parametrize("cache_min", [None, 4])
-def test_decode_step_fused_and_reset(dev, cache_min):
+@pytest.mark.parametrize("cache_min,e2", [(None, "0"), (4, "0"), (None, "1"), (4, "1")])
+def test_decode_step_fused_and_reset(dev, cache_min, e2, monkeypatch):
+    """Fused LF + mask against the oracle, with and without E2 (the narrow
+    rows' content read with their E scan instead of streamed afterwards)."""
     import torch
 
+    monkeypatch.setenv("FMIDX_LF_E2", e2)
     docs = markov_docs(11, 80, 40, 90)
     ours = ours_index(docs, bm_log2=5, cache_min=cache_min)
     ora = OracleIndex()

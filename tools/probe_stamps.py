@@ -20,7 +20,7 @@ from fmidx.synth import decode_trace  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
-V, B, W = 128256, 256, 5
+V, B, W = 128256, int(os.environ.get("BATCH", "256")), 5
 fm, text, bwt, _ = build_index(int(float(os.environ.get("TOKENS", "4.5e9"))), V, 20250905, dev)
 n = bwt.numel()
 tokens, init, lo_hist, hi_hist, _ = decode_trace(fm, text, bwt, B, V, W + 12, 20250905, dev)
