@@ -97,10 +97,11 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
   const int64_t* r = STAGED ? srow : g;
   uint32_t bad = 0;
   // remove_end_marker (causal_qwen.py:44-56): the tokens after the marker
-  const int64_t M = cfg.marker_len;
+  const bool hard = (cfg.flags & FM_PREP_HARD) != 0;
+  const int64_t M = hard ? 0 : cfg.marker_len;
   int64_t first = -1;
-  uint32_t hits = 0;
-  for (int64_t i0 = 0; i0 + M <= n; i0 += 64) {
+  uint32_t hits = hard ? 1u : 0u;
+  for (int64_t i0 = 0; M > 0 && i0 + M <= n; i0 += 64) {
     const int64_t i = i0 + lane;
     bool m = i + M <= n;
 #pragma unroll
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
     if (bal && first < 0) first = i0 + __ffsll((long long)bal) - 1;
   }
   if (hits != 1) bad |= FM_PREP_BAD_MARKER;
-  int64_t start = first < 0 ? 0 : first + M;
+  int64_t start = hard ? min((int64_t)max(cfg.skip, 0), n) : (first < 0 ? 0 : first + M);
   if (lane == 0) {
     atomicMin(&status[1], (uint32_t)start);
     atomicMax(&status[2], (uint32_t)start);
@@ -181,7 +182,8 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
       bool counted = false;   // cnt1 known
       uint64_t cnt1 = 0;
       if (last == cfg.eos || last == cfg.pad) {
-        cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
+        // hard variants: no trailing n-gram rule, the eos / pad rule applies as is
+        cnt1 = hard ? 1 : ((c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0);
         counted = true;
       }
       if (counted && cnt1 == 0) {
@@ -194,6 +196,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
         // call's range of a row (same beam group) whose pattern is this one's
         // pattern without its last token, else a full search
         bool found = false;
+        uint64_t pw = 0;   // count of the pattern without its last token (the hard variants' stop rule)
         if (prev_ids && ls >= 2) {
           const uint64_t beams = cfg.num_beams > 0 ? (uint64_t)cfg.num_beams : 1;
           const uint64_t g0 = row / beams * beams;
@@ -211,6 +214,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
             if (eq) {
               lo = l2;
               hi = h2;
+              pw = (uint64_t)(ps[3] - ps[2]);
               found = true;
             }
           }
@@ -222,6 +226,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
             if (wave_equal(prev_ids + b2 * prev_ld + pstart, r + s0, ls - 1)) {
               lo = (uint64_t)prev_state[2 * prev_B + b2];
               hi = (uint64_t)prev_state[3 * prev_B + b2];
+              pw = hi - lo;
               const uint32_t* cbm;
               int64_t one;
               lf_step_decode(v, c, lo, hi, cbm, one);
@@ -233,6 +238,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
           lo = 0;
           hi = v.n;
           for (int64_t j = 0; j < (int64_t)fdf_len + ls; ++j) {
+            if (j == (int64_t)fdf_len + ls - 1) pw = hi - lo;
             // both candidates loaded from their own address spaces (a select of
             // the pointers would make one generic pointer and FLAT loads)
             const int64_t jf = j < (int64_t)fdf_len ? j : 0, jr = j < (int64_t)fdf_len ? 0 : j - (int64_t)fdf_len;
@@ -245,13 +251,14 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
           }
         }
         // a non-empty range implies count([last]) > 0; an empty one asks C
-        if (hi <= lo) cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
-        if (hi <= lo && cnt1 == 0) {
+        // (the hard variants have no trailing n-gram rule)
+        if (hi <= lo && !hard) cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
+        if (hi <= lo && !hard && cnt1 == 0) {
           ls = 0;
           lo = hi = 0;
         } else {
           pattern = true;
-          const uint64_t count = hi - lo;
+          const uint64_t count = hard ? pw : hi - lo;
           if (cfg.stop_at_count > 0 && count <= (uint64_t)cfg.stop_at_count) {
             kind = kSpecial;
             p.special = cfg.eos;
@@ -268,7 +275,9 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
     } else if (kind == kSpecial || kind == kBits) {
       p.v_dist = pow_at(pow_tab, pow_len, ls, bad);
       bool empty = false;
-      if (kind == kBits) {
+      if (hard) {   // vllm.py:118-131: the distinct set only, on -inf
+        p.flags = kind == kBits ? FM_ROW_BITS : FM_ROW_SPECIAL;
+      } else if (kind == kBits) {
         // distinct (sentinel dropped, index.py:170) is empty iff the range is
         // empty or its one row holds the sentinel
         empty = hi == lo || (hi - lo == 1 && v.bwt[lo] == 0);
@@ -305,7 +314,7 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
                           const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
                           fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
                           hipStream_t s) {
-  if (cfg.marker_len < 1 || cfg.marker_len > 8) {
+  if (!(cfg.flags & FM_PREP_HARD) && (cfg.marker_len < 1 || cfg.marker_len > 8)) {
     set_error("processor step: marker length %d not in 1..8", cfg.marker_len);
     return -1;
   }

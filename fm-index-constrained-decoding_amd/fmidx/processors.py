@@ -57,11 +57,11 @@ class _PrepConfig(ctypes.Structure):
                 ("pad", c_int64), ("stop_at_count", c_int64), ("min_new_tokens", c_int64), ("forced_bos", c_int64),
                 ("shift", c_int64), ("marker_len", c_int32), ("num_beams", c_int32), ("flags", c_uint32),
                 ("base", c_float), ("v_uni_full", c_float), ("v_uni_half", c_float), ("v_forced", c_float),
-                ("reserved", c_int32)]
+                ("skip", c_int32)]
 
 
 assert ctypes.sizeof(_PrepConfig) == 192
-PREP_THINK, PREP_SKIP_FIRST, PREP_EOS, PREP_EOS_ALL, PREP_UNI_HALF = 1, 2, 4, 8, 16
+PREP_THINK, PREP_SKIP_FIRST, PREP_EOS, PREP_EOS_ALL, PREP_UNI_HALF, PREP_HARD = 1, 2, 4, 8, 16, 32
 
 
 def _boost_table(boost: float, lrf: float, dtype, n: int) -> List[float]:
@@ -596,7 +596,28 @@ class CausalIndexBasedLogitsProcessor:
 
 
 class _HardMaskBase:
-    """Shared by the hard-mask (-inf) variants."""
+    """Shared by the hard-mask (-inf) variants.  With this engine's index a
+    call runs on the device (fm_processor_call with FM_PREP_HARD: the pattern
+    is every token from ``skip`` on, the range one LF step from the previous
+    call's, stop_at_count against the count of the pattern without its last
+    token -- which is the previous call's range width); otherwise, and for
+    inputs the device path refuses, the batched host path below."""
+
+    SKIP = 0   # leading tokens that are not pattern (seq: the decoder start)
+
+    def _prep_config(self, dtype) -> _PrepConfig:
+        c = _PrepConfig()
+        c.eos, c.pad = self.eos_token_id, self.pad_token_id
+        c.stop_at_count, c.shift = self.stop_at_count, SHIFT
+        c.num_beams = self._num_beams
+        c.flags = PREP_HARD | ((PREP_EOS | PREP_EOS_ALL) if self.always_allow_eos else 0)
+        c.skip = self.SKIP
+        if self.forced_bos_token_id is not None:
+            c.flags |= PREP_SKIP_FIRST
+            c.forced_bos = self.forced_bos_token_id
+        c.base = float("-inf")
+        c.v_uni_full = c.v_uni_half = c.v_forced = _round(self.BOOST, dtype)
+        return c
 
     def _hard(self, sents: List[List[int]], pattern_of, count_of, V: int, dt, B: int):
         rows = np.zeros(B, dtype=ROW_DTYPE)
@@ -647,6 +668,7 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
         self.forced_bos_token_id = forced_bos_token_id
         self.BOOST = 0.0
         self._core = _BatchedCore(index)
+        self._dev = _device_step(self._core, self.BOOST, 1.0, force_decoding_from)
 
     def clone(self):
         return VllmIndexBasedLogitsProcessor(num_beams=self._num_beams, index=self.index,
@@ -659,6 +681,10 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
     def __call__(self, input_ids, scores):
         input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
         scores = scores.unsqueeze(0)
+        if self._dev is not None:
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            if out is not None:
+                return out
         B, V = scores.shape
         dt = scores.dtype
         boost = _round(self.BOOST, dt)
@@ -690,6 +716,8 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
 class SeqIndexBasedLogitsProcessor(_HardMaskBase):
     """document_constrained_generation_seq.py:6-123 (seq2seq hard mask; decoder start skipped)."""
 
+    SKIP = 1
+
     def __init__(self, index, num_beams: int, pad_token_id: int = 0, eos_token_id: int = 2,
                  force_decoding_from: Optional[List[int]] = None, stop_at_count: int = 0,
                  always_allow_eos: bool = False, forced_bos_token_id: Optional[int] = None):
@@ -703,11 +731,16 @@ class SeqIndexBasedLogitsProcessor(_HardMaskBase):
         self.forced_bos_token_id = forced_bos_token_id
         self.BOOST = 0.0
         self._core = _BatchedCore(index)
+        self._dev = _device_step(self._core, self.BOOST, 1.0, force_decoding_from)
 
     def __call__(self, input_ids, scores):
         return self._process(input_ids, scores)
 
     def _process(self, input_ids, scores):
+        if self._dev is not None:
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            if out is not None:
+                return out
         B, V = scores.shape
         dt = scores.dtype
         boost = _round(self.BOOST, dt)

@@ -271,7 +271,7 @@ typedef struct fm_prep_config {
   float v_uni_full;        /* BOOST rounded to the scores dtype */
   float v_uni_half;        /* BOOST / 2 rounded */
   float v_forced;          /* BOOST rounded (forced bos) */
-  int32_t reserved;
+  int32_t skip;            /* FM_PREP_HARD: leading tokens that are not pattern (seq: the decoder start) */
 } fm_prep_config;
 
 #define FM_PREP_THINK 1u       /* think gating + system-token removal (Qwen) */
@@ -279,6 +279,9 @@ typedef struct fm_prep_config {
 #define FM_PREP_EOS 4u         /* always_allow_eos */
 #define FM_PREP_EOS_ALL 8u     /* the eos boost on every row, no min_new_tokens gate (causal.py:173-178) */
 #define FM_PREP_UNI_HALF 16u   /* BOOST / 2 for the other unigrams even when distinct is empty (causal.py:171) */
+#define FM_PREP_HARD 32u       /* the hard-mask variants (vllm.py:46-137, seq.py:35-123): no end marker, the
+                                  pattern is every token from `skip` on, no trailing n-gram rule, and
+                                  stop_at_count tests the count of the pattern without its last token */
 
 #define FM_PREP_BAD_MARKER 1u  /* status: a row without exactly one end marker */
 #define FM_PREP_BAD_POW 2u     /* status: a boost BOOST * lrf^k outside the table (Python float overflow) */
