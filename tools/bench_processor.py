@@ -30,6 +30,8 @@ ap.add_argument("--vocab", type=int, default=128256)
 ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--steps", type=int, default=24)
 ap.add_argument("--host-steps", type=int, default=6)
+ap.add_argument("--variant", default="qwen", choices=["qwen", "seq"],
+                help="qwen: QwenIndexBasedLogitsProcessor (soft); seq: SeqIndexBasedLogitsProcessor (hard mask)")
 args = ap.parse_args()
 B, V = args.batch, args.vocab
 DT = {"f32": torch.float32, "bf16": torch.bfloat16}[args.dtype]
@@ -62,7 +64,8 @@ ids_seq = []
 for s in range(steps):
     for b in range(B):
         sents[b].append(int(true[b, len(sents[b])]) if rng.random() < 0.9 else int(rng.integers(3, V - 20)))
-    ids_seq.append(torch.tensor([head + x for x in sents], dtype=torch.int64, device=dev))
+    pre = head if args.variant == "qwen" else [1]     # seq2seq rows start with the decoder start token
+    ids_seq.append(torch.tensor([pre + x for x in sents], dtype=torch.int64, device=dev))
 scores = torch.randn(B, V, device=dev).to(DT)
 
 
@@ -79,16 +82,17 @@ def run(proc, seq, warm):
 
 
 kw = dict(index=ix, num_beams=1, pad_token_id=0, eos_token_id=2)
-proc = P.QwenIndexBasedLogitsProcessor(**kw)
+Proc = P.QwenIndexBasedLogitsProcessor if args.variant == "qwen" else P.SeqIndexBasedLogitsProcessor
+proc = Proc(**kw)
 assert proc._dev is not None
 td, out_d = run(proc, ids_seq[: 4 + args.steps], 4)
-host = P.QwenIndexBasedLogitsProcessor(**kw)
+host = Proc(**kw)
 host._dev = None
 th, out_h = run(host, ids_seq[: 4 + args.host_steps], 2)
 same = bool(torch.equal(out_d.view(torch.int16 if DT != torch.float32 else torch.int32),
-                        P.QwenIndexBasedLogitsProcessor(**kw)(ids_seq[3 + args.steps], scores)
+                        Proc(**kw)(ids_seq[3 + args.steps], scores)
                         .view(torch.int16 if DT != torch.float32 else torch.int32)))
-res = {"B": B, "V": V, "dtype": args.dtype, "corpus_tokens": n, "index_build_s": round(build_s, 1),
+res = {"variant": args.variant, "B": B, "V": V, "dtype": args.dtype, "corpus_tokens": n, "index_build_s": round(build_s, 1),
        "device_path": {"steps": len(td), "ms_per_call_mean": round(float(td.mean()), 4),
                        "ms_per_call_median": round(float(np.median(td)), 4), "ms_per_call_min": round(float(td.min()), 4),
                        "ms_per_call_max": round(float(td.max()), 4), "rows_per_s": round(B / (td.mean() / 1e3))},
