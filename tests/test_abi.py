@@ -76,3 +76,31 @@ def test_encode_corpus_matches_reference_encoding():
     data, beg, occ = encode_corpus(docs)
     d2, b2, o2 = oracle_encode(docs)
     assert data.tolist() == d2 and beg == b2 and occ == o2
+
+
+def _header_struct_fields(name):
+    import re
+
+    hdr = open(os.path.join(REPO, "include", "fmidx.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        names = decl.split(None, 1)[1] if not decl.startswith("const") else decl.split(None, 2)[2]
+        for n in names.split(","):
+            n = n.strip().lstrip("*").strip()
+            fields.append(re.sub(r"\[.*\]", "", n))
+    return fields
+
+
+def test_ctypes_structs_match_header():
+    """The ctypes mirrors of fm_prep_config / fm_processor_args list the
+    header's fields in the header's order (their sizes are asserted at import
+    and in api.cpp)."""
+    import fmidx.processors as P
+
+    assert [f[0] for f in P._PrepConfig._fields_] == _header_struct_fields("fm_prep_config")
+    assert [f[0] for f in P._ProcessorArgs._fields_] == _header_struct_fields("fm_processor_args")
