@@ -1,12 +1,15 @@
-// process.hip -- the per-row bookkeeping of the soft logits processors on the
-// device (fm_processor_step), so a processor call is three launches and no
-// per-row host work:
+// process.hip -- the per-row bookkeeping of the logits processors on the
+// device (fm_processor_step; fm_processor_call runs it and the two launches
+// after it in one host call), so a processor call has no per-row host work:
 //   k_prep      one wave per row: remove_end_marker, finished_thinking,
 //               remove_system_tokens, the trailing n-gram rule, the eos / pad
 //               / stop_at_count rules and the pattern's range
 //               (document_constrained_generation_causal_qwen.py:44-99,
-//               :101-214; document_constrained_generation_causal.py:62-180),
-//               writing the epilogue's fm_row_params
+//               :101-214; document_constrained_generation_causal.py:62-180);
+//               FM_PREP_HARD: the hard-mask variants (vllm.py:46-137,
+//               seq.py:35-123) -- pattern from `skip` on, no trailing n-gram
+//               rule, stop_at_count on the count of the pattern without its
+//               last token; writes the epilogue's fm_row_params
 //   fm_allowed_mask_batch(packed)   the allowed bits of the rows that need them
 //   fm_apply_boosts                 scores + mask in the scores dtype
 // The pattern's range is ONE LF step from the previous call's range when the
