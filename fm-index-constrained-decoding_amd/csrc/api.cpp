@@ -53,11 +53,6 @@ void Index::release() {
   if (cache_tab) (void)hipFree(cache_tab);
   if (trans_tab) (void)hipFree(trans_tab);
   trans_tab = nullptr;
-  if (cbt_keys) (void)hipFree(cbt_keys);
-  if (cbt_bm) (void)hipFree(cbt_bm);
-  cbt_keys = nullptr;
-  cbt_bm = nullptr;
-  cbt_entries = cbt_bytes = 0;
   if (cblock) (void)hipFree(cblock);
   cblock = nullptr;
   trans_entries = trans_dropped = trans_bytes = 0;

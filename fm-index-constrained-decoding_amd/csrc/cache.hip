@@ -121,99 +121,6 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
   if (drop) atomicAdd(&stats[1], drop);
 }
 
-// Child-bitmap table (see DevView::cbt_*): every transition slot whose child
-// is cached claims its home slot by CAS (a taken home = the key is left out),
-// then one workgroup per claimed slot copies the child's bitmap there.
-__global__ void __launch_bounds__(256) k_cbt_count(const uint64_t* __restrict__ tab, uint64_t cap,
-                                                   unsigned long long* __restrict__ cnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  bool cached = false;
-  if (i < cap && tab[3 * i] != kTransEmpty) {
-    const uint64_t aux = tab[3 * i + 2] >> 38;
-    cached = aux != 0 && !(aux & kTransOne);
-  }
-  const uint64_t b = __ballot(cached);
-  if ((threadIdx.x & 63u) == 0 && b) atomicAdd(cnt, (unsigned long long)__popcll(b));
-}
-
-__global__ void __launch_bounds__(256) k_cbt_claim(const uint64_t* __restrict__ tab, uint64_t cap,
-                                                   uint64_t* __restrict__ keys, uint32_t* __restrict__ src,
-                                                   uint64_t mask, unsigned long long* __restrict__ cnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= cap) return;
-  const uint64_t w0 = tab[3 * i];
-  if (w0 == kTransEmpty) return;
-  const uint64_t w1 = tab[3 * i + 1], w2 = tab[3 * i + 2];
-  const uint64_t aux = w2 >> 38;
-  if (aux == 0 || (aux & kTransOne)) return;
-  const uint64_t slot = cbt_home(w0 & kMask34, w1 & kMask34, w0 >> kTransSymShift, mask);
-  if (atomicCAS(reinterpret_cast<unsigned long long*>(keys + 3 * slot), (unsigned long long)kTransEmpty,
-                (unsigned long long)w0) == kTransEmpty) {
-    keys[3 * slot + 1] = w1;
-    keys[3 * slot + 2] = w2;
-    src[slot] = (uint32_t)aux;   // cache id + 1
-    atomicAdd(cnt, 1ull);
-  }
-}
-
-__global__ void __launch_bounds__(256) k_cbt_copy(const uint32_t* __restrict__ src, const uint32_t* __restrict__ cache_bm,
-                                                  uint64_t words, uint32_t* __restrict__ bm) {
-  const uint64_t slot = blockIdx.x;
-  const uint32_t id1 = src[slot];
-  if (!id1) return;
-  const uint4* from = reinterpret_cast<const uint4*>(cache_bm + (uint64_t)(id1 - 1) * words);
-  uint4* to = reinterpret_cast<uint4*>(bm + slot * words);
-  for (uint64_t j = threadIdx.x; j < words / 4; j += 256) to[j] = from[j];
-}
-
-int build_child_bitmaps(Index* h, hipStream_t s) {
-  DevView& v = h->view;
-  v.cbt_mask = 0;
-  v.cbt_keys = nullptr;
-  v.cbt_bm = nullptr;
-  const uint64_t factor = env_u64("FMIDX_CBT", 4);   // capacity / entries; 0 = no table
-  if (!factor || !v.trans_cap || !v.bm_words) return 0;
-  DBuf<unsigned long long> d_cnt;
-  if (d_cnt.alloc(2)) return -1;
-  FM_HIP(hipMemsetAsync(d_cnt.p, 0, 16, s));
-  const unsigned g = (unsigned)((v.trans_cap + 255) / 256);
-  k_cbt_count<<<g, 256, 0, s>>>(v.trans_tab, v.trans_cap, d_cnt.p);
-  FM_HIP(hipGetLastError());
-  unsigned long long cnt = 0;
-  FM_HIP(hipMemcpyAsync(&cnt, d_cnt.p, 8, hipMemcpyDeviceToHost, s));
-  FM_HIP(hipStreamSynchronize(s));
-  if (cnt == 0) return 0;
-  uint64_t cap = 1024;
-  while (cap < factor * cnt) cap <<= 1;
-  const uint64_t words = v.bm_words;
-  const uint64_t budget = env_u64("FMIDX_CBT_MB", 8ull << 10) << 20;
-  if (cap * words * 4 > budget) return 0;
-  DBuf<uint32_t> d_src;
-  if (d_src.alloc(cap)) return -1;
-  if (hipMalloc(reinterpret_cast<void**>(&h->cbt_keys), cap * 24) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&h->cbt_bm), cap * words * 4) != hipSuccess) {
-    (void)hipGetLastError();
-    if (h->cbt_keys) (void)hipFree(h->cbt_keys);
-    h->cbt_keys = nullptr;
-    return 0;   // no room: the probe + bitmap round trips serve every step
-  }
-  FM_HIP(hipMemsetAsync(h->cbt_keys, 0xFF, cap * 24, s));
-  FM_HIP(hipMemsetAsync(d_src.p, 0, cap * 4, s));
-  k_cbt_claim<<<g, 256, 0, s>>>(v.trans_tab, v.trans_cap, h->cbt_keys, d_src.p, cap - 1, d_cnt.p + 1);
-  k_cbt_copy<<<(unsigned)cap, 256, 0, s>>>(d_src.p, v.cache_bm, words, h->cbt_bm);
-  FM_HIP(hipGetLastError());
-  unsigned long long got = 0;
-  FM_HIP(hipMemcpyAsync(&got, d_cnt.p + 1, 8, hipMemcpyDeviceToHost, s));
-  FM_HIP(hipStreamSynchronize(s));
-  h->cbt_entries = got;
-  h->cbt_bytes = cap * (24 + words * 4);
-  h->cache_bytes += h->cbt_bytes;
-  v.cbt_keys = h->cbt_keys;
-  v.cbt_bm = h->cbt_bm;
-  v.cbt_mask = cap - 1;
-  return 0;
-}
-
 // Transition table of the cached ranges (all their children, or -- when that
 // would exceed FMIDX_TRANS_MB -- only the cached ones), built on the GPU from
 // two k_distinct passes over the cached parents: one to count the entries,
@@ -540,8 +447,7 @@ int device_build_cache(Index* h, hipStream_t s) {
     h->cache_bytes += cb.size() * 4;
   }
 
-  if (build_transitions(h, nodes, s)) return -1;
-  return build_child_bitmaps(h, s);
+  return build_transitions(h, nodes, s);
 }
 
 }  // namespace fmidx
