@@ -118,35 +118,36 @@ def lf_plan_bytes(prev_lo, prev_hi, tok, n, parent_cached, st, kernel: str):
     count, the block header entry and the block prefix up to the position
     (level 0 exact from the position; level 1's position is data-dependent: its
     expected prefix, half a block).  Restarted / dead rows read nothing."""
-    lines = lambda a, b: ((b + 63) // 64) - (a // 64)     # noqa: E731  (byte span [a, b))
-    out = np.zeros(prev_lo.size, dtype=np.int64)
-    has_e = st.get("lf_e", True)
+    lo = np.asarray(prev_lo, dtype=np.int64)
+    hi = np.minimum(np.asarray(prev_hi, dtype=np.int64), n)
+    t = np.asarray(tok, dtype=np.int64)
+    pc = np.asarray(parent_cached, dtype=bool)
+    out = np.zeros(lo.size, dtype=np.int64)
+    has_e = bool(st.get("lf_e", True))
     trans = st["trans_entries"] > 0
     cmin = st["cache_min"] or (1 << 62)
-    scan_max = 4096 if kernel == "decode" and prev_lo.size <= 256 else 1024
-    for i in range(prev_lo.size):
-        lo, hi, t = int(prev_lo[i]), min(int(prev_hi[i]), n), int(tok[i])
-        if t < 0 or lo >= hi:
-            continue
-        w = hi - lo
-        if lo == 0 and hi == n:
-            out[i] = 128
-        elif has_e and w <= 512:
-            out[i] = 64 * lines(8 * lo, 8 * hi)
-        elif kernel == "decode" and has_e and w <= scan_max and (w < cmin or not trans):
-            out[i] = 64 * lines(8 * lo, 8 * hi)
-        else:
-            b = 0
-            if trans and w >= cmin:
-                b += 384
-                if parent_cached[i]:
-                    out[i] = b
-                    continue
-            b += 3 * 64                                    # D2[c], Z[0][d0], Z[1][d1]
-            for pos in (lo, hi):
-                b += 2 * 64 + 64 * lines(0, 2 * (pos % 1024))    # level 0: sb + header + uint16 prefix
-                b += 2 * 64 + 64 * lines(0, 512)                 # level 1: sb + header + uint8 prefix (expected)
-            out[i] = b
+    scan_max = 4096 if kernel == "decode" and lo.size <= 256 else 1024
+    w = hi - lo
+    e_bytes = 64 * (((8 * hi + 63) // 64) - (8 * lo) // 64)   # 64-B lines of E[lo, hi)
+    rest = (t >= 0) & (lo < hi)
+    full = rest & (lo == 0) & (hi == n)
+    out[full] = 128
+    rest &= ~full
+    if has_e:
+        narrow = rest & (w <= 512)
+        if kernel == "decode":
+            narrow |= rest & (w <= scan_max) & ((w < cmin) | (not trans))
+        out[narrow] = e_bytes[narrow]
+        rest &= ~narrow
+    probe = rest & trans & (w >= cmin)
+    hit = probe & pc
+    out[hit] = 384
+    desc = rest & ~hit
+    b = 384 * probe.astype(np.int64) + 3 * 64                # D2[c], Z[0][d0], Z[1][d1]
+    for pos in (lo, hi):
+        b = b + 2 * 64 + 64 * ((2 * (pos % 1024) + 63) // 64)  # level 0: sb + header + uint16 prefix
+        b = b + 2 * 64 + 64 * ((512 + 63) // 64)             # level 1: sb + header + uint8 prefix (expected)
+    out[desc] = b[desc]
     return out
 
 
