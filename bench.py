@@ -151,6 +151,18 @@ def lf_plan_bytes(prev_lo, prev_hi, tok, n, parent_cached, st, kernel: str):
     return out
 
 
+def rank_pairs(fm, text, bwt, V, seed, dev, rows=65536, steps=9):
+    """(tokens, lo, hi) of rows x (steps - 1) independent LF steps taken from
+    a decode trace (the same generator as the bench's), plus the ranges the
+    fused decode kernel computed for them (the exactness check)."""
+    tokens, _, lo_h, hi_h, _ = decode_trace(fm, text, bwt, rows, V, steps, seed, dev)
+    tok = tokens[1:steps].reshape(-1).contiguous()
+    lo = lo_h[:steps - 1].reshape(-1).contiguous()
+    hi = hi_h[:steps - 1].reshape(-1).contiguous()
+    ref = (lo_h[1:steps].reshape(-1).contiguous(), hi_h[1:steps].reshape(-1).contiguous())
+    return tok, lo, hi, ref
+
+
 def gather_ceiling(dev, nbytes=8 << 30):
     """The random 64-B gather ceiling of HBM, measured live
     with csrc/probe.hip: (GB/s of independent random 64-B lines over an 8 GiB
@@ -407,6 +419,9 @@ def main():
     # the CPU legs replay the same trace past the GPU's steps (bounded by time)
     S_trace = S + (args.cpu_steps if cpu_leg else 0)
     tokens, init, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
+    # rank throughput at scale: RS_ROWS x (RS_STEPS - 1) independent (state,
+    # token) pairs of a wider trace, for one k_lf launch (the grouped kernel)
+    rs_tok, rs_lo, rs_hi, rs_ref = rank_pairs(fm, text, bwt, V, args.seed + 17 + rank, dev)
     del text
     torch.cuda.empty_cache()
     PK = bool(args.packed)
@@ -491,6 +506,12 @@ def main():
     with torch.cuda.graph(g_lfbig):
         fm.lf_step_batch(all_tok, all_lo, all_hi, SHIFT, lo_out=big_lo, hi_out=big_hi, reset_below=0)
     lfbig_cold = timed(g_lfbig, 3, cold=True)
+    rs_olo, rs_ohi = torch.empty_like(rs_lo), torch.empty_like(rs_hi)
+    g_rs = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_rs):
+        fm.lf_step_batch(rs_tok, rs_lo, rs_hi, SHIFT, lo_out=rs_olo, hi_out=rs_ohi, reset_below=0)
+    rs_cold = timed(g_rs, 3, cold=True)
+    rs_ok = bool(torch.equal(rs_olo, rs_ref[0]) and torch.equal(rs_ohi, rs_ref[1]))
     mask_ms = [t / K for t in timed(g_mask, 5)]
     step_warm = [t / K for t in timed(g_step, 3, reset=True)]
     lo.copy_(state_lo)
@@ -571,6 +592,11 @@ def main():
     rank_gbs = float(lf_std.mean()) / (lf_us_cold * 1e-6) / 1e9
     lfbig_us = float(np.median(lfbig_cold)) * 1e3
     rank_gbs_big = float(lf_std.sum()) / (lfbig_us * 1e-6) / 1e9
+    rs_pc = fm.cache_contains(rs_lo, rs_hi).cpu().numpy()
+    rs_bytes = float(lf_plan_bytes(rs_lo.cpu().numpy(), rs_hi.cpu().numpy(), rs_tok.cpu().numpy(), n, rs_pc, st,
+                                   "lf").sum())
+    rs_us = float(np.median(rs_cold)) * 1e3
+    rank_gbs_scale = rs_bytes / (rs_us * 1e-6) / 1e9
     gather_gbs, chase_ns = (None, None)
     if not args.no_gather:
         gather_gbs, chase_ns = gather_ceiling(dev)
@@ -583,7 +609,8 @@ def main():
     widths = (hi_np - lo_np)
     log(f"step cold {step_ms * 1e3:.1f}us, warm [{', '.join(f'{t * 1e3:.1f}' for t in step_warm)}] "
         f"(standalone lf cold {lf_us_cold:.1f}us / warm {lf_us_warm:.1f}us, {K * B} rows in one launch "
-        f"{lfbig_us:.1f}us = {rank_gbs_big:.0f} GB/s, mask {mask_us:.1f}us, "
+        f"{lfbig_us:.1f}us = {rank_gbs_big:.0f} GB/s, {rs_tok.numel()} rows {rs_us:.1f}us = {rank_gbs_scale:.0f} GB/s "
+        f"(exact {rs_ok}), mask {mask_us:.1f}us, "
         f"wall/step {wall / K * 1e6:.1f}us, graph) bytes/step {decode_bytes / 1e6:.2f}MB -> {achieved:.0f} GB/s; "
         f"live rows {(widths > 0).mean():.2f}, median width {np.median(widths[widths > 0]) if (widths > 0).any() else 0}, "
         f"cached rows {cached.mean():.3f} (cache: {st['cache_nodes']} ranges >= {st['cache_min']}, "
@@ -643,6 +670,14 @@ def main():
                                  "alg_bytes_per_launch": float(lf_std.sum()), "rank_GBps": rank_gbs_big,
                                  "rank_frac_of_gather_ceiling": (rank_gbs_big / gather_gbs) if gather_gbs else None,
                                  "note": "all K x B (state, token) pairs of the timed steps in one launch"},
+                     "at_scale": {"rows": int(rs_tok.numel()), "avg_launch_us_cold": rs_us,
+                                  "alg_bytes_per_launch": rs_bytes, "rank_GBps": rank_gbs_scale,
+                                  "rank_frac_of_peak": rank_gbs_scale / HBM_PEAK_GBS,
+                                  "rank_frac_of_gather_ceiling": (rank_gbs_scale / gather_gbs) if gather_gbs else None,
+                                  "M_lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6) / 1e6,
+                                  "matches_decode_kernel": rs_ok,
+                                  "note": "2^19 independent (state, token) pairs of a 65536-row trace in one k_lf launch "
+                                          "(grouped kernel: 2 lanes per row, wide rows by the whole wave), cold"},
                      "bytes_model": "64-B lines the LF plan reads per live row (bench.lf_plan_bytes)"},
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},

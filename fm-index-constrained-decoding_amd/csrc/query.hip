@@ -75,6 +75,195 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
   }
 }
 
+// ------------------------------------------------------------ grouped LF
+// Throughput form of k_lf / k_search for launches with more rows than the chip
+// has wave slots (256 CUs x 32 waves): a wave is latency-bound on its dependent
+// round trips, so at one row per wave the rows in flight per CU cap the rate
+// (Little's law: 32 rows x ~3 cold hops).  Here a group of G lanes owns a row,
+// 64 / G rows per wave: a full range takes its C lookup, a range of <= 8 G rows
+// its E scan inside the group (8 entries per lane, one round trip), and the
+// rest -- wider ranges (transition probe / wavelet descent / wave-wide E
+// scan) -- are taken one at a time by the whole wave through lf_step_decode.
+
+// One LF step for every group of the wave.  `live` = the group takes a step
+// (false: the row is left as it is).  Every lane executes the same loads (the
+// E scan is unconditional with a clamped index, as in lf_step_fast: a guarded
+// load is sunk into a branch with a vmcnt(0) behind it).
+template <int G, bool GP>
+__device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h,
+                                           uint64_t& lo, uint64_t& hi) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t j = lane & (G - 1);
+  const uint64_t h0 = h;
+  if (h > v.n) h = v.n;
+  const bool dead = !live || l >= h || sym < 0 || (uint64_t)sym > v.max_sym;
+  const bool full = !dead && l == 0 && h == v.n;
+  const bool narrow = !dead && !full && v.E && h - l <= 8u * G;
+  bool wide = live && !dead && !full && !narrow;
+  const uint64_t c = dead ? 0 : (uint64_t)sym;
+  // C lookup (full range), the group's E scan and (GP) its transition probe,
+  // issued together
+  const uint64_t ca = v.C[c], cb = v.C[c + 1];
+  uint64_t pw[GP ? 3 * (16 / G) : 1];
+  const bool probe = GP && wide && v.trans_cap && h - l >= v.cache_min;
+  if (GP) {
+    // the 16-slot probe of lf_step_decode, 16 / G slots (3 words each) per lane;
+    // unconditional loads (slot 0 for rows that do not probe; C[0..2] when
+    // the index has no transition table)
+    const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;
+    const uint64_t home = probe ? trans_home(l, h, c, v.trans_cap) : 0;
+#pragma unroll
+    for (int k = 0; k < 16 / G; ++k) {
+      uint64_t slot = probe ? home + j * (16 / G) + k : 0;
+      if (slot >= v.trans_cap) slot -= v.trans_cap;
+#pragma unroll
+      for (int w = 0; w < 3; ++w) pw[3 * k + w] = tt[3 * slot + w];
+    }
+  }
+  uint64_t e[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint64_t idx = l + j + (uint64_t)G * k;
+    const uint64_t x = v.E ? v.E[narrow ? (idx < h ? idx : h - 1) : 0] : 0;
+    e[k] = (narrow && idx < h) ? x : ~0ull;
+  }
+  uint64_t fmin = ~0ull, fmax = 0, lfmin = 0, lfmax = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    if (e[k] != ~0ull && (e[k] >> kESymShift) == c) {
+      const uint64_t r = j + (uint64_t)G * k + 1;
+      if (r < fmin) {
+        fmin = r;
+        lfmin = e[k] & kELfMask;
+      }
+      fmax = r;      // k ascends: the last match of the lane
+      lfmax = e[k] & kELfMask;
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < G; d <<= 1) {
+    const uint64_t om = __shfl_xor(fmin, d, 64), ol = __shfl_xor(lfmin, d, 64);
+    const uint64_t xm = __shfl_xor(fmax, d, 64), xl = __shfl_xor(lfmax, d, 64);
+    if (om < fmin) {
+      fmin = om;
+      lfmin = ol;
+    }
+    if (xm > fmax) {
+      fmax = xm;
+      lfmax = xl;
+    }
+  }
+  if (!live) {
+    lo = l;
+    hi = h0;
+  } else if (dead) {
+    lo = 0;
+    hi = 0;
+  } else if (full) {
+    lo = ca < cb ? ca : 0;
+    hi = ca < cb ? cb : 0;
+  } else if (narrow) {
+    lo = fmax ? lfmin : 0;
+    hi = fmax ? lfmax + 1 : 0;
+  }
+  if (GP) {   // a probe hit (at most one slot of the group holds the key) ends a wide row's step
+    const uint64_t key0 = l | (c << kTransSymShift);
+    uint64_t hit = 0, clo = 0, cw = 0;
+#pragma unroll
+    for (int k = 0; k < 16 / G; ++k) {
+      const bool m = probe && pw[3 * k] == key0 && (pw[3 * k + 1] & kMask34) == h;
+      hit |= m ? 1u : 0u;
+      clo |= m ? ((pw[3 * k + 1] >> kTransSymShift) | ((pw[3 * k + 2] & 0xFu) << 30)) : 0;
+      cw |= m ? ((pw[3 * k + 2] >> 4) & kMask34) : 0;
+    }
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) {
+      hit |= __shfl_xor(hit, d, 64);
+      clo |= __shfl_xor(clo, d, 64);
+      cw |= __shfl_xor(cw, d, 64);
+    }
+    if (hit) {
+      lo = clo;
+      hi = clo + cw;
+      wide = false;
+    }
+  }
+  // wide rows: one at a time by the whole wave (wave-uniform loop)
+  uint64_t wb = __ballot(wide && j == 0);
+  while (wb) {
+    const int src = __ffsll((long long)wb) - 1;
+    wb &= wb - 1;
+    uint64_t wl = __shfl(l, src, 64), wh = __shfl(h, src, 64);
+    const int64_t ws = __shfl(sym, src, 64);
+    const uint32_t* cbm;
+    int64_t one;
+    lf_step_decode(v, ws, wl, wh, cbm, one);
+    if ((lane / G) == ((uint32_t)src / G)) {
+      lo = wl;
+      hi = wh;
+    }
+  }
+}
+
+template <int G, bool GP>
+__global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_t* __restrict__ tok,
+                                                        int64_t shift, int64_t reset_below,
+                                                        const uint64_t* lo_in, const uint64_t* hi_in,
+                                                        uint64_t* lo_out, uint64_t* hi_out, uint64_t m) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  if (wave * (64 / G) >= m) return;      // wave-uniform
+  const uint64_t i = wave * (64 / G) + lane / G;
+  const bool valid = i < m;
+  const uint64_t ii = valid ? i : m - 1;
+  const int64_t t = (int64_t)row_load_u64(tok, m, ii);
+  const uint64_t l = row_load_u64(lo_in, m, ii), h = row_load_u64(hi_in, m, ii);
+  uint64_t nl, nh;
+  group_step<G, GP>(v, valid, t + shift, l, h, nl, nh);
+  if (t < reset_below) {
+    nl = 0;
+    nh = v.n;
+  }
+  if (valid && (lane & (G - 1)) == 0) {
+    lo_out[i] = nl;
+    hi_out[i] = nh;
+  }
+}
+
+template <int G, bool GP>
+__global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const int64_t* __restrict__ tok,
+                                                            const int64_t* __restrict__ off, uint64_t m,
+                                                            int64_t shift, const uint64_t* lo_in,
+                                                            const uint64_t* hi_in, uint64_t* lo_out,
+                                                            uint64_t* hi_out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  if (wave * (64 / G) >= m) return;      // wave-uniform
+  const uint64_t i = wave * (64 / G) + lane / G;
+  const bool valid = i < m;
+  const uint64_t ii = valid ? i : m - 1;
+  uint64_t l = lo_in ? lo_in[ii] : 0;
+  uint64_t h = hi_in ? hi_in[ii] : v.n;
+  int64_t j = off[ii];
+  const int64_t b = valid ? off[ii + 1] : j;
+  bool active = j < b;
+  while (__ballot(active)) {           // wave-uniform: until every group's pattern is done
+    const int64_t t = tok[active ? j : 0];   // some group is active: tok has an element
+    uint64_t nl, nh;
+    group_step<G, GP>(v, active, t + shift, l, h, nl, nh);
+    if (active) {
+      l = nl;
+      h = nh;
+      ++j;
+      if ((l == 0 && h == 0) || j >= b) active = false;   // index.py:111-112
+    }
+  }
+  if (valid && (lane & (G - 1)) == 0) {
+    lo_out[i] = l;
+    hi_out[i] = h;
+  }
+}
+
 // [sdsl] backward_search on an inclusive range with unsigned wrap-around.
 __device__ void sdsl_backward_search(const DevView& v, uint64_t c, uint64_t l, uint64_t r,
                                      uint64_t& lr, uint64_t& rr) {
@@ -323,6 +512,29 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
   return (uint32_t)std::strtoul(s, nullptr, 10);
 }
 
+// Lanes per row of the LF / search launches: 64 (one wave per row) while the
+// rows fit the chip's wave slots (latency: no row waits behind another's wide
+// step), else FMIDX_LF_GROUP lanes (default 2; 64 = never group) above
+// FMIDX_LF_GROUP_MIN rows (default 8192 = 256 CUs x 32 waves).  Measured on
+// the C3 index (tools/probe_rank.py, 2^19 pairs, cold): one wave per row 308 us,
+// G = 16 / 8 / 4 / 2 / 1: 179 / 125 / 99 / 90 / 100 us; get_range of 2^18
+// patterns 2658 us -> 539 us at G = 2.
+uint32_t lf_group(uint64_t m) {
+  static const uint32_t G = [] {
+    const uint32_t g = env_u32("FMIDX_LF_GROUP", 2);
+    return (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 64u;
+  }();
+  static const uint64_t min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
+  return m > min_rows ? G : 64u;
+}
+
+// Grouped launches (G >= 4) probe the transition table inside the group
+// (FMIDX_LF_GPROBE, default 1): a cached range's hit then needs no wave-wide step.
+bool lf_gprobe() {
+  static const bool on = env_u32("FMIDX_LF_GPROBE", 1) != 0;
+  return on;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -330,8 +542,24 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s) {
   if (m == 0) return 0;
-  const unsigned g = (unsigned)((m * 64 + kLfThreads - 1) / kLfThreads);
-  k_lf<<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  const uint32_t G = lf_group(m);
+  const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
+  if (G == 1)
+    k_lf_group<1, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 2)
+    k_lf_group<2, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 4 && lf_gprobe())
+    k_lf_group<4, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 4)
+    k_lf_group<4, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 8 && lf_gprobe())
+    k_lf_group<8, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 8)
+    k_lf_group<8, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 16)
+    k_lf_group<16, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else
+    k_lf<<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   FM_HIP(hipGetLastError());
   return 0;
 }
@@ -340,8 +568,24 @@ int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,
                   uint64_t* hi_out, hipStream_t s) {
   if (m == 0) return 0;
-  const unsigned g = (unsigned)((m * 64 + kLfThreads - 1) / kLfThreads);
-  k_search<<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  const uint32_t G = lf_group(m);
+  const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
+  if (G == 1)
+    k_search_group<1, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 2)
+    k_search_group<2, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 4 && lf_gprobe())
+    k_search_group<4, true><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 4)
+    k_search_group<4, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 8 && lf_gprobe())
+    k_search_group<8, true><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 8)
+    k_search_group<8, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else if (G == 16)
+    k_search_group<16, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+  else
+    k_search<<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   FM_HIP(hipGetLastError());
   return 0;
 }

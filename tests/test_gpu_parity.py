@@ -224,6 +224,65 @@ def test_incremental_lf_equals_full_research(dev):
         assert got == want, s
 
 
+@pytest.mark.parametrize("cache_min", [None, 4])
+def test_grouped_lf_and_search_vs_oracle(dev, cache_min):
+    """Launches above FMIDX_LF_GROUP_MIN (8192) rows take the grouped kernels
+    (G lanes per row, wide rows by the whole wave): get_range of 20000
+    patterns (index.py:103-114 with its early exit) and one LF step of 20000
+    (state, token) pairs, against the oracle -- dead, empty, full-range,
+    narrow, wide and cached rows, unknown ids, hi past n, reset rows."""
+    import torch
+
+    docs = markov_docs(17, 400, 60, 100)
+    ours = ours_index(docs, bm_log2=6, cache_min=cache_min)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ours.size()
+    F = [t for d in reversed(docs) for t in d]
+    rng = np.random.default_rng(23)
+    m = 20000
+    pats = []
+    for i in range(m):
+        ln = int(rng.integers(0, 7))
+        s = int(rng.integers(0, len(F) - ln))
+        p = list(F[s:s + ln])
+        for j in range(ln):
+            r = rng.random()
+            if r < 0.1:
+                p[j] = int(rng.integers(0, 70))
+            elif r < 0.12:
+                p[j] = 1000 + int(rng.integers(0, 5))     # beyond the largest symbol
+        pats.append(p)
+    toks = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=dev)
+    offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), dtype=torch.int64, device=dev)
+    lo = torch.zeros(m, dtype=torch.int64, device=dev)
+    hi = torch.zeros(m, dtype=torch.int64, device=dev)
+    ours.backward_search_batch(toks, offs, 10, lo, hi)
+    got = list(zip(lo.cpu().tolist(), hi.cpu().tolist()))
+    want = [ora.get_range(p) if p else (0, n) for p in pats]
+    bad = [i for i in range(m) if got[i] != want[i]]
+    assert not bad, [(pats[i], got[i], want[i]) for i in bad[:5]]
+    # one LF step from every pattern's range (some states past n, some reset)
+    nxt = np.where(rng.random(m) < 0.8, [F[int(rng.integers(0, len(F)))] for _ in range(m)],
+                   rng.integers(-3, 80, m)).astype(np.int64)
+    lo_in = lo.clone()
+    hi_in = hi.clone()
+    hi_in[::97] = n + 5
+    lo_out, hi_out = torch.empty_like(lo), torch.empty_like(hi)
+    ours.lf_step_batch(torch.tensor(nxt, device=dev), lo_in, hi_in, 10, lo_out=lo_out, hi_out=hi_out,
+                       reset_below=-2)
+    got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
+    li, hv = lo_in.cpu().tolist(), hi_in.cpu().tolist()
+    for i in range(m):
+        t = int(nxt[i])
+        if t < -2:
+            w = (0, n)
+        else:
+            a, b = li[i], min(hv[i], n)
+            w = (0, 0) if a >= b else ora.backward_search_step(t + 10, a, b - 1)
+        assert got[i] == w, (i, t, li[i], hv[i], got[i], w)
+
+
 @pytest.mark.parametrize("cache_min,e2", [(None, "0"), (4, "0"), (None, "1"), (4, "1")])
 def test_decode_step_fused_and_reset(dev, cache_min, e2, monkeypatch):
     """Fused LF + mask against the oracle, with and without E2 (the narrow

@@ -218,6 +218,61 @@ def test_c3_index_properties(dev, c3):
     assert bool((hi > lo).all()), int((hi <= lo).sum())
 
 
+@pytest.mark.timeout(900)
+def test_c3_grouped_lf_and_search(dev, c3):
+    """Above 8192 rows LF / get_range launches take the grouped kernels (G
+    lanes per row).  On the > 2^32 index: get_range of 16384 true patterns
+    (U{1..32} tokens) == the same patterns in two launches of 8192 (one wave
+    per row); one LF step over 3 x 16384 trace pairs == the fused decode
+    kernel's ranges, and a sample of 512 pairs == cpu_ref."""
+    import torch
+
+    from fmidx.synth import decode_trace
+
+    fm, text, bwt, ref = c3["fm"], c3["text"], c3["bwt"], c3["ref"]
+    n = text.numel()
+    g = torch.Generator(device=dev)
+    g.manual_seed(31)
+    P = 16384
+    lens = torch.randint(1, 33, (P,), generator=g, device=dev)
+    q = torch.randint(0, n - 40, (P,), generator=g, device=dev)
+    offs = torch.zeros(P + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=offs[1:])
+    row_of = torch.repeat_interleave(torch.arange(P, device=dev), lens)
+    k = torch.arange(int(offs[-1]), device=dev) - offs[:-1][row_of]
+    toks = text[(n - 2) - (q[row_of] + k)].to(torch.int64) - SHIFT
+    toks[::53] = torch.randint(0, V, toks[::53].shape, generator=g, device=dev)   # some patterns go empty
+    lo = torch.zeros(P, dtype=torch.int64, device=dev)
+    hi = torch.zeros(P, dtype=torch.int64, device=dev)
+    fm.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    lo2, hi2 = torch.zeros_like(lo), torch.zeros_like(hi)
+    for a in (0, P // 2):
+        o = offs[a:a + P // 2 + 1]
+        t = toks[int(o[0]):int(o[-1])]
+        l_, h_ = torch.zeros(P // 2, dtype=torch.int64, device=dev), torch.zeros(P // 2, dtype=torch.int64, device=dev)
+        fm.backward_search_batch(t, (o - o[0]).contiguous(), SHIFT, l_, h_)
+        lo2[a:a + P // 2], hi2[a:a + P // 2] = l_, h_
+    assert torch.equal(lo, lo2) and torch.equal(hi, hi2)
+    assert bool((hi > lo).any()) and bool((hi == 0).any())
+    B, S = 16384, 4
+    tokens, _, lo_h, hi_h, _ = decode_trace(fm, text, bwt, B, V, S, 515, dev)
+    t = tokens[1:S].reshape(-1).contiguous()
+    pl = lo_h[:S - 1].reshape(-1).contiguous()
+    ph = hi_h[:S - 1].reshape(-1).contiguous()
+    ol, oh = torch.empty_like(pl), torch.empty_like(ph)
+    fm.lf_step_batch(t, pl, ph, SHIFT, lo_out=ol, hi_out=oh, reset_below=0)
+    assert torch.equal(ol, lo_h[1:S].reshape(-1)) and torch.equal(oh, hi_h[1:S].reshape(-1))
+    sel = torch.randint(0, t.numel(), (512,), generator=g, device=dev)
+    clo = pl[sel].cpu().numpy().astype(np.uint64)
+    chi = ph[sel].cpu().numpy().astype(np.uint64)
+    cm = np.zeros((512, 8), dtype=np.uint8)
+    ref.decode_step(np.ascontiguousarray(t[sel].cpu().numpy()), SHIFT, 0, clo, chi, cm, 16)   # ranges (+ 8 mask columns)
+    assert np.array_equal(clo, ol[sel].cpu().numpy().astype(np.uint64))
+    assert np.array_equal(chi, oh[sel].cpu().numpy().astype(np.uint64))
+    widths = (ph - pl).cpu().numpy()
+    assert (widths > 4096).any() and ((widths > 0) & (widths <= 64)).any()
+
+
 @pytest.mark.timeout(600)
 def test_c2_decode_b32_vs_cpu_ref(dev, c2):
     """C2 shape (simplewiki scale n = 3e8, B = 32), 12 steps."""
