@@ -371,6 +371,32 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     if (threadIdx.x == 0) k_out[row] = empty ? 0 : ~0ull;
     return;
   }
+  if (lo == 0 && hi == v.n) {
+    // The full range: its symbols and counts are the C array itself (symbol c
+    // occurs C[c+1] - C[c] times, its child range starts at C[c]) -- one pass
+    // over sigma instead of a BFS whose last level holds every symbol.  Each
+    // thread takes a contiguous run of symbols; a block scan orders the output.
+    const uint64_t sigma = (uint64_t)v.max_sym + 1;
+    const uint64_t per = (sigma + 255) / 256;
+    const uint64_t c0 = min<uint64_t>(sigma, threadIdx.x * per), c1 = min<uint64_t>(sigma, c0 + per);
+    uint32_t mine = 0;
+    for (uint64_t c = c0; c < c1; ++c) mine += (v.C[c + 1] - v.C[c] >= min_count) ? 1u : 0u;
+    uint32_t tot;
+    uint64_t pos = block_scan_u32(mine, wave_tot, tot);
+    if (tot <= cap) {
+      for (uint64_t c = c0; c < c1; ++c) {
+        const uint64_t a = v.C[c], b = v.C[c + 1];
+        if (b - a >= min_count) {
+          syms[base + pos] = c;
+          counts[base + pos] = b - a;
+          if (child_lo) child_lo[base + pos] = a;
+          ++pos;
+        }
+      }
+    }
+    if (threadIdx.x == 0) k_out[row] = tot <= cap ? tot : ~0ull;
+    return;
+  }
   uint64_t* alo = fr.lo[0] + base;
   uint64_t* ahi = fr.hi[0] + base;
   uint32_t* apre = fr.pre[0] + base;

@@ -24,7 +24,7 @@ from typing import Iterable, Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .fm_index import FMIndex as _FMIndex
-from .fm_index import load_FMIndex
+from .fm_index import _u64_vec, load_FMIndex
 
 SHIFT = 10                      # index.py:16
 
@@ -145,13 +145,21 @@ class FMIndex(_FMIndex):
         return [syms[i] - SHIFT for i in keep], [cnts[i] for i in keep]
 
     def get_distinct_count_multi(self, lows: List[int], highs: List[int]) -> List[Tuple[List[int], List[int]]]:
-        ret = []
-        for data in self.distinct_count_multi(lows, highs):
-            syms = data[0::2]
-            cnts = data[1::2]
-            keep = [i for i, d in enumerate(syms) if d > 0]
-            ret.append(([syms[i] - SHIFT for i in keep], [cnts[i] for i in keep]))
-        return ret
+        """index.py:161-174: per range, its symbols > 0 (the sentinel dropped)
+        minus SHIFT and their counts -- filtered and shifted on the result
+        arrays of the one batched launch, not per symbol in Python."""
+        lo = _u64_vec(lows, "distinct_count_multi", 2)
+        hi = _u64_vec(highs, "distinct_count_multi", 3)
+        if lo.size != hi.size:
+            raise ValueError("lows and highs differ in length")
+        out, offs = self._distinct_count_multi_arrays(lo, hi)
+        tot = int(offs[-1]) if offs.size else 0
+        pairs = out[: 2 * tot].reshape(-1, 2)
+        keep = pairs[:, 0] > 0
+        syms = (pairs[keep, 0].astype(np.int64) - SHIFT).tolist()
+        cnts = pairs[keep, 1].astype(np.int64).tolist()
+        ko = np.concatenate([[0], np.cumsum(keep)]).astype(np.int64)[offs.astype(np.int64)].tolist()
+        return [(syms[ko[i]:ko[i + 1]], cnts[ko[i]:ko[i + 1]]) for i in range(lo.size)]
 
     def __len__(self) -> int:
         return self.beginnings[-1]

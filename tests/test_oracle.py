@@ -123,3 +123,34 @@ def test_extract_unbounded_case_rejected():
     idx.initialize([11, 12, 13])
     with pytest.raises(ValueError):
         idx.extract_text(4, 9)
+
+
+def test_get_distinct_count_multi_postprocessing(golden_index_cases):
+    """fmidx.index.FMIndex.get_distinct_count_multi filters and shifts the
+    batched launch's result arrays (sentinel dropped, ids - SHIFT) instead of
+    walking SWIG tuples per symbol; fed the oracle's raw distinct_count output
+    in the launch's layout it must give the golden multi results (index.py:161-174)."""
+    import numpy as np
+
+    from fmidx.index import FMIndex
+
+    checked = 0
+    for case in golden_index_cases:
+        if "docs" not in case or not case["multi"]["lows"]:
+            continue
+        ora = OracleIndex()
+        ora.initialize(case["docs"], in_memory=case["in_memory"])
+        lows, highs = case["multi"]["lows"], case["multi"]["highs"]
+        raws = [ora.distinct_count(a, b) for a, b in zip(lows, highs)]
+
+        def arrays(lo, hi, raws=raws):
+            flat = [x for r in raws for x in r]
+            offs = np.concatenate([[0], np.cumsum([len(r) // 2 for r in raws])]).astype(np.uint64)
+            return np.asarray(flat + [0, 0], dtype=np.uint64), offs
+
+        idx = object.__new__(FMIndex)        # no device: only the host post-processing runs
+        idx._distinct_count_multi_arrays = arrays
+        multi = idx.get_distinct_count_multi(lows, highs)
+        assert [[list(a), list(b)] for a, b in multi] == case["multi"]["out"], case["name"]
+        checked += 1
+    assert checked >= 5
