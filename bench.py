@@ -696,6 +696,17 @@ def main():
                     result["standalone_kernels"]["k_lf"]["pmc_bytes_per_launch"] = t["k_lf_bytes_per_launch"]
         except Exception:
             pass
+    pr = os.path.join(REPO, "profiles", "r02_rank", "pmc", "pmc_rank.json")
+    if os.path.exists(pr) and n > 4e9:
+        try:   # tools/pmc_rank.sh: the 2^19-row grouped launches of tools/probe_rank.py on a C3 index
+            with open(pr) as f:
+                t = json.load(f)
+            big = [(a, b) for a, b in zip(t["fetch_bytes"], t["write_bytes"]) if b >= 8e6]
+            if big:
+                result["standalone_kernels"]["k_lf"]["at_scale"]["pmc_bytes_per_launch"] = float(
+                    np.median([a + b for a, b in big]))
+        except Exception:
+            pass
     if cpu_leg:
         try:
             result["cpu_baseline"] = cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, W,
