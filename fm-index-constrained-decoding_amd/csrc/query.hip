@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
 // (false: the row is left as it is).  Every lane executes the same loads (the
 // E scan is unconditional with a clamped index, as in lf_step_fast: a guarded
 // load is sunk into a branch with a vmcnt(0) behind it).
-template <int G, bool GP>
+template <int G, bool GP, bool Q>
 __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h,
                                            uint64_t& lo, uint64_t& hi) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -188,8 +188,102 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
       wide = false;
     }
   }
-  // wide rows: one at a time by the whole wave (wave-uniform loop)
-  uint64_t wb = __ballot(wide && j == 0);
+  uint64_t wb;
+  if (Q) {
+    // Wide rows four at a time, 16 lanes each: a cached parent's transition
+    // probe (its 16 slots, one per lane) or the E scan of a range <= 128 rows
+    // (8 entries per lane), one round trip per four rows.  Rows neither settles
+    // (a probe miss, an uncached range > 128 rows) go to the serial loop below.
+    const uint32_t seg = lane >> 4, sl = lane & 15u;
+    const bool elig = wide && ((v.E && h - l <= 128) || (v.trans_cap && h - l >= v.cache_min));
+    uint64_t qb = __ballot(elig && j == 0);
+    uint64_t keep = __ballot(wide && !elig && j == 0);
+    const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;   // C[0..2]: a valid dummy address
+    while (qb) {
+      int sv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sv[k] = qb ? __ffsll((long long)qb) - 1 : -1;
+        if (qb) qb &= qb - 1;
+      }
+      const int my = seg == 0 ? sv[0] : (seg == 1 ? sv[1] : (seg == 2 ? sv[2] : sv[3]));
+      const bool act = my >= 0;
+      const int srcl = act ? my : 0;
+      const uint64_t ql = __shfl(l, srcl, 64), qh = __shfl(h, srcl, 64);
+      const int64_t qs = __shfl(sym, srcl, 64);
+      const uint64_t qc = act ? (uint64_t)qs : 0;
+      const bool qscan = act && v.E && qh - ql <= 128;
+      const bool qprobe = act && !qscan && v.trans_cap && qh - ql >= v.cache_min;
+      uint64_t slot = qprobe ? trans_home(ql, qh, qc, v.trans_cap) + sl : 0;
+      if (slot >= v.trans_cap) slot -= v.trans_cap;
+      const uint64_t p0 = tt[3 * slot], p1 = tt[3 * slot + 1], p2 = tt[3 * slot + 2];
+      uint64_t qe[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint64_t idx = ql + sl + 16ull * k;
+        const uint64_t x = v.E ? v.E[qscan ? (idx < qh ? idx : qh - 1) : 0] : 0;
+        qe[k] = (qscan && idx < qh) ? x : ~0ull;
+      }
+      uint64_t fmn = ~0ull, fmx = 0, lmn = 0, lmx = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        if (qe[k] != ~0ull && (qe[k] >> kESymShift) == qc) {
+          const uint64_t r = sl + 16ull * k + 1;
+          if (r < fmn) {
+            fmn = r;
+            lmn = qe[k] & kELfMask;
+          }
+          fmx = r;
+          lmx = qe[k] & kELfMask;
+        }
+      }
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        const uint64_t om = __shfl_xor(fmn, d, 64), ol = __shfl_xor(lmn, d, 64);
+        const uint64_t xm = __shfl_xor(fmx, d, 64), xl = __shfl_xor(lmx, d, 64);
+        if (om < fmn) {
+          fmn = om;
+          lmn = ol;
+        }
+        if (xm > fmx) {
+          fmx = xm;
+          lmx = xl;
+        }
+      }
+      const uint64_t key0 = ql | (qc << kTransSymShift);
+      const uint64_t hb = __ballot(qprobe && p0 == key0 && (p1 & kMask34) == qh) & (0xFFFFull << (16 * seg));
+      const int hl = hb ? __ffsll((long long)hb) - 1 : 0;
+      const uint64_t w1 = __shfl(p1, hl, 64), w2 = __shfl(p2, hl, 64);
+      uint64_t rlo = 0, rhi = 0;
+      int done = 0;
+      if (qscan) {
+        rlo = fmx ? lmn : 0;
+        rhi = fmx ? lmx + 1 : 0;
+        done = 1;
+      } else if (qprobe && hb) {
+        rlo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
+        rhi = rlo + ((w2 >> 4) & kMask34);
+        done = 1;
+      }
+      // hand each row's result to its group (the loop and sv[] are wave-uniform)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sk = sv[k];
+        if (sk < 0) break;
+        const uint64_t xl = __shfl(rlo, 16 * k, 64), xh = __shfl(rhi, 16 * k, 64);
+        const int xd = __shfl(done, 16 * k, 64);
+        if (xd && (lane / G) == ((uint32_t)sk / G)) {
+          lo = xl;
+          hi = xh;
+        }
+        if (!xd) keep |= 1ull << sk;
+      }
+    }
+    wb = keep;
+  } else {
+    wb = __ballot(wide && j == 0);
+  }
+  // the remaining wide rows: one at a time by the whole wave (wave-uniform loop)
   while (wb) {
     const int src = __ffsll((long long)wb) - 1;
     wb &= wb - 1;
@@ -205,7 +299,7 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
   }
 }
 
-template <int G, bool GP>
+template <int G, bool GP, bool Q>
 __global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_t* __restrict__ tok,
                                                         int64_t shift, int64_t reset_below,
                                                         const uint64_t* lo_in, const uint64_t* hi_in,
@@ -219,7 +313,7 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_
   const int64_t t = (int64_t)row_load_u64(tok, m, ii);
   const uint64_t l = row_load_u64(lo_in, m, ii), h = row_load_u64(hi_in, m, ii);
   uint64_t nl, nh;
-  group_step<G, GP>(v, valid, t + shift, l, h, nl, nh);
+  group_step<G, GP, Q>(v, valid, t + shift, l, h, nl, nh);
   if (t < reset_below) {
     nl = 0;
     nh = v.n;
@@ -230,7 +324,7 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_
   }
 }
 
-template <int G, bool GP>
+template <int G, bool GP, bool Q>
 __global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const int64_t* __restrict__ tok,
                                                             const int64_t* __restrict__ off, uint64_t m,
                                                             int64_t shift, const uint64_t* lo_in,
@@ -250,7 +344,7 @@ __global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const in
   while (__ballot(active)) {           // wave-uniform: until every group's pattern is done
     const int64_t t = tok[active ? j : 0];   // some group is active: tok has an element
     uint64_t nl, nh;
-    group_step<G, GP>(v, active, t + shift, l, h, nl, nh);
+    group_step<G, GP, Q>(v, active, t + shift, l, h, nl, nh);
     if (active) {
       l = nl;
       h = nh;
@@ -561,6 +655,15 @@ bool lf_gprobe() {
   return on;
 }
 
+// G = 2 LF launches settle wide rows four at a time (16 lanes each: a probe or
+// a <= 128-row E scan) before the serial loop (FMIDX_LF_QUAD, default 1):
+// 2^19 cold pairs 87 vs 93 us.  Not in k_search_group, where the extra
+// registers (155 VGPRs: 3 waves per SIMD) cost more than it saves (565 vs 548 us).
+bool lf_quad() {
+  static const bool on = env_u32("FMIDX_LF_QUAD", 1) != 0;
+  return on;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -571,19 +674,21 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
   const uint32_t G = lf_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
   if (G == 1)
-    k_lf_group<1, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<1, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+  else if (G == 2 && lf_quad())
+    k_lf_group<2, false, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 2)
-    k_lf_group<2, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<2, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 4 && lf_gprobe())
-    k_lf_group<4, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<4, true, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 4)
-    k_lf_group<4, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<4, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 8 && lf_gprobe())
-    k_lf_group<8, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<8, true, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 8)
-    k_lf_group<8, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<8, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 16)
-    k_lf_group<16, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    k_lf_group<16, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else
     k_lf<<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   FM_HIP(hipGetLastError());
@@ -597,19 +702,19 @@ int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint
   const uint32_t G = lf_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
   if (G == 1)
-    k_search_group<1, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<1, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 2)
-    k_search_group<2, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<2, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 4 && lf_gprobe())
-    k_search_group<4, true><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<4, true, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 4)
-    k_search_group<4, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<4, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 8 && lf_gprobe())
-    k_search_group<8, true><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<8, true, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 8)
-    k_search_group<8, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<8, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 16)
-    k_search_group<16, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
+    k_search_group<16, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else
     k_search<<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   FM_HIP(hipGetLastError());
