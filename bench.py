@@ -677,7 +677,7 @@ def main():
                                   "M_lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6) / 1e6,
                                   "matches_decode_kernel": rs_ok,
                                   "note": "2^19 independent (state, token) pairs of a 65536-row trace in one k_lf launch "
-                                          "(grouped kernel: 2 lanes per row, wide rows by the whole wave), cold"},
+                                          "(grouped kernel: 2 lanes per row; wide rows four at a time, then by the whole wave), cold"},
                      "bytes_model": "64-B lines the LF plan reads per live row (bench.lf_plan_bytes)"},
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},
