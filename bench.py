@@ -684,6 +684,15 @@ def main():
         },
         "index": {"build": build_t, **st},
         "trace_check": ok,
+        # the metric's second half ("rank GB/s vs HBM roofline"), summarised: LF throughput at
+        # concurrency (2^19 independent steps, one grouped launch, cold) against 8 TB/s and the live
+        # random-64-B gather ceiling; at B = 256 the LF launch is a latency chain (k_lf above)
+        "rank": {"GBps": rank_gbs_scale, "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                 "frac_of_peak": rank_gbs_scale / HBM_PEAK_GBS,
+                 "gather_ceiling_GBps": gather_gbs,
+                 "frac_of_gather_ceiling": (rank_gbs_scale / gather_gbs) if gather_gbs else None,
+                 "lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6),
+                 "b256_GBps": rank_gbs, "b256_avg_launch_us_cold": lf_us_cold},
     }
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
