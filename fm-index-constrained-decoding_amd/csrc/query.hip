@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
                                                  uint64_t* __restrict__ syms,
                                                  uint64_t* __restrict__ counts,
                                                  uint64_t* __restrict__ k_out, Frontier fr,
-                                                 uint64_t min_count, uint64_t* __restrict__ child_lo) {
+                                                 uint64_t min_count, uint64_t* __restrict__ child_lo,
+                                                 bool cached_path) {
   __shared__ uint32_t wave_tot[4];
   const uint64_t row = blockIdx.x;
   if (row >= m) return;
@@ -465,6 +466,8 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     if (threadIdx.x == 0) k_out[row] = empty ? 0 : ~0ull;
     return;
   }
+  if (cached_path && ((lo == 0 && hi == v.n) ? v.bm_full != nullptr : cache_find(v, lo, hi) != nullptr))
+    return;   // k_distinct_cached's row
   if (lo == 0 && hi == v.n) {
     // The full range: its symbols and counts are the C array itself (symbol c
     // occurs C[c+1] - C[c] times, its child range starts at C[c]) -- one pass
@@ -584,6 +587,108 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
   }
   if (threadIdx.x == 0) k_out[row] = fc;
+}
+
+// interval_symbols of a cached range or the full range (k_distinct leaves these rows to it):
+// its symbols are the set bits of its cached bitmap, already in ascending
+// order, and the count of symbol c is the width of the child range the
+// transition table holds for (range, c) -- or, for a key the table left out,
+// the width of the 16-ary descent of both ends.  A row is split over
+// kDcChunks workgroups of 256 words (8192 symbols); a workgroup's output
+// offset is the popcount of the bitmap words before its chunk.  Only for
+// min_count == 1 with a transition table (not while the table is being built).
+constexpr uint32_t kDcWords = 256;
+
+__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint64_t& clo,
+                                         uint64_t& cnt) {
+  const uint64_t key0 = lo | ((uint64_t)c << kTransSymShift);
+  uint64_t slot = trans_home(lo, hi, c, v.trans_cap);
+  for (uint32_t d = 0; d < kTransProbe; ++d) {
+    const uint64_t w0 = v.trans_tab[3 * slot], w1 = v.trans_tab[3 * slot + 1];
+    if (w0 == key0 && (w1 & kMask34) == hi) {
+      const uint64_t w2 = v.trans_tab[3 * slot + 2];
+      clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
+      cnt = (w2 >> 4) & kMask34;
+      return;
+    }
+    if (w0 == kTransEmpty) break;     // slots are claimed first-empty-from-home and never freed
+    if (++slot == v.trans_cap) slot = 0;
+  }
+  uint64_t pl = lo, pr = hi;           // a key the table left out: the descent
+  descend_full(v, c, pl, pr);
+  clo = (uint64_t)((int64_t)pl + v.D[c]);
+  cnt = pr - pl;
+}
+
+__global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64_t* __restrict__ lo_a,
+                                                        const uint64_t* __restrict__ hi_a, uint64_t m,
+                                                        const uint64_t* __restrict__ cap_off,
+                                                        uint64_t* __restrict__ syms, uint64_t* __restrict__ counts,
+                                                        uint64_t* __restrict__ k_out,
+                                                        uint64_t* __restrict__ child_lo, uint32_t chunks) {
+  __shared__ uint32_t wave_tot[4];
+  const uint64_t row = blockIdx.x / chunks;
+  const uint32_t ch = blockIdx.x % chunks;
+  if (row >= m) return;
+  uint64_t lo = lo_a[row], hi = hi_a[row];
+  if (lo == hi || cap_off[row + 1] == cap_off[row]) return;
+  if (hi > v.n) hi = v.n;
+  if (lo >= hi) return;
+  // the same test as k_distinct's (workgroup-uniform); the full range's bitmap
+  // is bm_full and its counts come from C
+  const bool fullr = lo == 0 && hi == v.n;
+  const uint32_t* bm = fullr ? v.bm_full : cache_find(v, lo, hi);
+  if (!bm) return;
+  const uint64_t base = cap_off[row];
+  const uint64_t cap = cap_off[row + 1] - base;
+  const uint32_t W = v.bm_words;
+  const uint32_t w0 = ch * kDcWords;
+  // output offset of this chunk: set bits before it (chunk 0: also the row's total)
+  uint32_t pre = 0;
+  const uint32_t lim = ch == 0 ? W : min(w0, W);
+  for (uint32_t w = threadIdx.x; w < lim; w += 256) pre += __popc(bm[w]);
+  uint32_t all;
+  (void)block_scan_u32(pre, wave_tot, all);
+  if (ch == 0 && threadIdx.x == 0) k_out[row] = all;
+  const uint32_t before = ch == 0 ? 0u : all;
+  const uint32_t wi = w0 + threadIdx.x;
+  const uint32_t word = wi < W ? bm[wi] : 0u;
+  uint32_t tot;
+  uint64_t pos = base + before + block_scan_u32((uint32_t)__popc(word), wave_tot, tot);
+  uint32_t rest = word;
+  while (rest) {
+    // up to 4 symbols' probes issued together (child_of is inlined per symbol)
+    uint32_t cs[4];
+    int nb = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rest) {
+        cs[u] = wi * 32u + (uint32_t)(__ffs(rest) - 1);
+        rest &= rest - 1;
+        nb = u + 1;
+      } else {
+        cs[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u < nb) {
+        uint64_t clo, cnt;
+        if (fullr) {
+          clo = v.C[cs[u]];
+          cnt = v.C[cs[u] + 1] - clo;
+        } else {
+          child_of(v, lo, hi, cs[u], clo, cnt);
+        }
+        if (pos - base < cap) {
+          syms[pos] = cs[u];
+          counts[pos] = cnt;
+          if (child_lo) child_lo[pos] = clo;
+        }
+        ++pos;
+      }
+    }
+  }
 }
 
 // Dense CSR of k_distinct's output for the host API: off[i] = sum of k[< i]
@@ -750,9 +855,17 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
   fr.hi[1] = fr.lo[1] + T;
   fr.pre[0] = reinterpret_cast<uint32_t*>(fr.hi[1] + T);
   fr.pre[1] = fr.pre[0] + T;
+  const bool cached_path = v.trans_cap && v.cache_mask && (min_count ? min_count : 1) == 1 &&
+                           env_u32("FMIDX_DISTINCT_CACHED", 1) != 0;
   k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr,
-                                         min_count ? min_count : 1, child_lo);
+                                         min_count ? min_count : 1, child_lo, cached_path);
   FM_HIP(hipGetLastError());
+  if (cached_path) {
+    const uint32_t chunks = (v.bm_words + kDcWords - 1) / kDcWords;
+    k_distinct_cached<<<(unsigned)(m * chunks), 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, child_lo,
+                                                             chunks);
+    FM_HIP(hipGetLastError());
+  }
   return 0;
 }
 
