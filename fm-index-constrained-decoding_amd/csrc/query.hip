@@ -599,11 +599,12 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
 // min_count == 1 with a transition table (not while the table is being built).
 constexpr uint32_t kDcWords = 256;
 
-__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint64_t& clo,
-                                         uint64_t& cnt) {
+// the child of (lo, hi) by symbol c: from slot `slot` + d of its probe run on
+// (the caller has checked the first `d0` slots)
+__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint64_t slot,
+                                         uint32_t d0, uint64_t& clo, uint64_t& cnt) {
   const uint64_t key0 = lo | ((uint64_t)c << kTransSymShift);
-  uint64_t slot = trans_home(lo, hi, c, v.trans_cap);
-  for (uint32_t d = 0; d < kTransProbe; ++d) {
+  for (uint32_t d = d0; d < kTransProbe; ++d) {
     const uint64_t w0 = v.trans_tab[3 * slot], w1 = v.trans_tab[3 * slot + 1];
     if (w0 == key0 && (w1 & kMask34) == hi) {
       const uint64_t w2 = v.trans_tab[3 * slot + 2];
@@ -670,6 +671,23 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
         cs[u] = 0;
       }
     }
+    // the first two slots of every symbol's probe run, issued together
+    // (linear probing at load <= 0.57: most keys sit in one of them)
+    uint64_t sl0[4], q[4][6];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool pr = !fullr && u < nb;
+      uint64_t a = pr ? trans_home(lo, hi, cs[u], v.trans_cap) : 0;
+      uint64_t b = a + 1 == v.trans_cap ? 0 : a + 1;
+      sl0[u] = a;
+      const uint64_t* tt = pr ? v.trans_tab : v.C;   // C[0..2]: a valid dummy address
+      if (!pr) a = b = 0;
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        q[u][w] = tt[3 * a + w];
+        q[u][3 + w] = tt[3 * b + w];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (u < nb) {
@@ -678,7 +696,23 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
           clo = v.C[cs[u]];
           cnt = v.C[cs[u] + 1] - clo;
         } else {
-          child_of(v, lo, hi, cs[u], clo, cnt);
+          const uint64_t key0 = lo | ((uint64_t)cs[u] << kTransSymShift);
+          if (q[u][0] == key0 && (q[u][1] & kMask34) == hi) {
+            clo = (q[u][1] >> kTransSymShift) | ((q[u][2] & 0xFu) << 30);
+            cnt = (q[u][2] >> 4) & kMask34;
+          } else if (q[u][3] == key0 && (q[u][4] & kMask34) == hi) {
+            clo = (q[u][4] >> kTransSymShift) | ((q[u][5] & 0xFu) << 30);
+            cnt = (q[u][5] >> 4) & kMask34;
+          } else if (q[u][0] == kTransEmpty || q[u][3] == kTransEmpty) {
+            uint64_t pl = lo, pr2 = hi;    // not in the table (left out): the descent
+            descend_full(v, cs[u], pl, pr2);
+            clo = (uint64_t)((int64_t)pl + v.D[cs[u]]);
+            cnt = pr2 - pl;
+          } else {
+            uint64_t s2 = sl0[u] + 2;
+            if (s2 >= v.trans_cap) s2 -= v.trans_cap;
+            child_of(v, lo, hi, cs[u], s2, 2, clo, cnt);
+          }
         }
         if (pos - base < cap) {
           syms[pos] = cs[u];
