@@ -240,7 +240,7 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min):
     n = ours.size()
     F = [t for d in reversed(docs) for t in d]
     rng = np.random.default_rng(23)
-    m = 20000
+    m = 20011          # not a multiple of the 32 rows a two-lane wave holds
     pats = []
     for i in range(m):
         ln = int(rng.integers(0, 7))
