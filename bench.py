@@ -47,6 +47,13 @@ HBM_STREAM_GBS = 6290.0   # measured stream rate (MI355X_MICROARCH.md)
 METRIC = "allowed-token masks/sec @ B=256, 128k vocab"
 
 
+def lib_sha16():
+    import hashlib
+
+    with open(os.path.join(PKG, "fmidx", "libfmidx.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
@@ -163,25 +170,36 @@ def rank_pairs(fm, text, bwt, V, seed, dev, rows=65536, steps=9):
     return tok, lo, hi, ref
 
 
+GATHER_MODES = {0: ("lane_64B", 1, 64), 2: ("coop4_64B", 4, 64), 3: ("coop8_128B", 8, 128), 4: ("lane_8B", 1, 8)}
+
+
 def gather_ceiling(dev, nbytes=8 << 30):
-    """The random 64-B gather ceiling of HBM, measured live
-    with csrc/probe.hip: (GB/s of independent random 64-B lines over an 8 GiB
-    buffer, ns per dependent hop with 256 chains = one chain per row at B = 256)."""
+    """The random-gather ceilings of HBM, measured live with
+    csrc/probe.hip over an 8 GiB buffer: GB/s of independent random lines for
+    each access shape (GATHER_MODES: every lane its own 64-B line, 4 lanes per
+    64-B line, 8 lanes per 128-B line, every lane its own 8-B word -- bytes are
+    the line bytes delivered), and ns per dependent hop with 256 chains (one
+    chain per row at B = 256).  Returns (best 64-B-line ceiling, ns per hop,
+    {mode: GB/s})."""
     buf = torch.randint(0, 1 << 62, (nbytes // 8,), dtype=torch.int64, device=dev)
     sink = torch.zeros(1024, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     threads, loads = 256 * 4096, 64
-    best = None
-    for _ in range(4):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
-        check(lib().fm_probe_gather(buf.data_ptr(), nbytes, 0, loads, threads, sink.data_ptr(), stream), "probe")
-        b.record()
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b)
-        best = ms if best is None else min(best, ms)
-    gbs = threads * loads * 64 / (best * 1e-3) / 1e9
+    rates = {}
+    for mode, (name, lpl, line) in GATHER_MODES.items():
+        best = None
+        for _ in range(4):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            check(lib().fm_probe_gather(buf.data_ptr(), nbytes, mode, loads, threads, sink.data_ptr(), stream),
+                  "probe")
+            b.record()
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b)
+            best = ms if best is None else min(best, ms)
+        rates[name] = threads // lpl * loads * line / (best * 1e-3) / 1e9
+    gbs = max(rates["lane_64B"], rates["coop4_64B"])
     hops, chains = 4000, 256
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
@@ -192,7 +210,7 @@ def gather_ceiling(dev, nbytes=8 << 30):
     ns_hop = a.elapsed_time(b) * 1e6 / hops
     del buf
     torch.cuda.empty_cache()
-    return gbs, ns_hop
+    return gbs, ns_hop, rates
 
 
 # ---------------------------------------------------------------------------
@@ -207,14 +225,19 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, seconds, dev):
+def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, reps, dev):
     """The sdsl-faithful C++ restatement (oracle/cpu_ref.cpp) on the host
-    cores, replaying the same trace from step `warmup`, four legs of about
-    `seconds` each: {incremental (one LF step per row per step, as the engine),
-    full re-search (the reference's processors: get_count([last]), get_range(sent),
-    get_count(sent) from scratch, document_constrained_generation_causal_qwen.py:
-    97,135,138)} x {1 thread, every core this process may use}.  Each leg's
-    final ranges and final step's [B, V] masks are compared with the GPU's."""
+    cores, replaying the same trace, four legs: {incremental (one LF step per
+    row per step, as the engine), full re-search (the reference's processors:
+    get_count([last]), get_range(sent), get_count(sent) from scratch,
+    document_constrained_generation_causal_qwen.py:97,135,138)} x {1 thread,
+    every core this process may use}.  SURVEY §8(d): every leg times the SAME
+    fixed window of `window` trace steps (steps warmup + 1 .. warmup + window),
+    after one untimed warm-up step (step `warmup`: first touch of the index
+    pages and the leg's buffers), `reps` times from the same state; the value
+    is the median repetition (masks/s), with the min / max beside it.  Each
+    leg's final ranges and final step's [B, V] masks are compared with the
+    GPU's."""
     from oracle.cpu_ref import CpuRef
 
     t0 = time.time()
@@ -222,66 +245,109 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, seconds, d
     log(f"cpu_ref build {time.time() - t0:.1f}s")
     all_cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     B = tokens.shape[1]
-    S = tokens.shape[0]
     tok_np = tokens.cpu().numpy()
     lo_all = lo_hist.cpu().numpy().astype(np.uint64)
     hi_all = hi_hist.cpu().numpy().astype(np.uint64)
+    first, last = warmup + 1, warmup + window           # the timed window, inclusive
+    assert last < tokens.shape[0]
+    # the full re-search legs' flat patterns per step (host bookkeeping, outside every timed region)
+    pats = trace_patterns(pats0, tok_np, warmup - 1)
+    flat_by_step = {}
+    for s in range(warmup, last + 1):
+        for b, t in enumerate(tok_np[s].tolist()):
+            if t < 0:
+                pats[b] = []
+            else:
+                pats[b].append(t)
+        offs = np.zeros(B + 1, dtype=np.int64)
+        np.cumsum([len(p) for p in pats], out=offs[1:])
+        flat_by_step[s] = (np.fromiter((t for p in pats for t in p), dtype=np.int64), offs)
+
+    def one_step(mode, s, lo, hi, mask, threads):
+        if mode == "incremental":
+            ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, lo, hi, mask, threads)
+        else:
+            flat, offs = flat_by_step[s]
+            ref.full_step(flat, offs, SHIFT, lo, hi, mask, threads, faithful=True)
+
+    # every leg: one untimed warm-up step, then `reps` timed passes over the same window; the
+    # repetitions are interleaved across the legs (A B C D A B C D ...), so drift of the shared
+    # host (frequency, other tenants) lands on every leg alike
+    names = [(mode, threads) for mode in ("incremental", "full_research") for threads in (1, all_cores)]
+    state = {}
+    for mode, threads in names:
+        mask = np.zeros((B, V), dtype=np.uint8)
+        lo = lo_all[warmup - 1].copy()
+        hi = hi_all[warmup - 1].copy()
+        one_step(mode, warmup, lo, hi, mask, threads)          # untimed warm-up step
+        state[(mode, threads)] = (lo, hi, mask, lo.copy(), hi.copy(), [])
+    for _ in range(reps):
+        for key in names:
+            lo, hi, mask, lo_w, hi_w, rates = state[key]
+            lo[:] = lo_w
+            hi[:] = hi_w
+            a = time.perf_counter()
+            for s in range(first, last + 1):
+                one_step(key[0], s, lo, hi, mask, key[1])
+            rates.append(window * B / (time.perf_counter() - a))
     legs = {}
-    for mode in ("incremental", "full_research"):
-        for threads in (1, all_cores):
-            mask = np.zeros((B, V), dtype=np.uint8)
-            lo = lo_all[warmup - 1].copy()
-            hi = hi_all[warmup - 1].copy()
-            pats = trace_patterns(pats0, tok_np, warmup - 1) if mode == "full_research" else None
-            steps = 0
-            el = 0.0
-            s = warmup
-            while s < S:
-                if mode == "incremental":
-                    tk = np.ascontiguousarray(tok_np[s])
-                    a = time.time()
-                    ref.decode_step(tk, SHIFT, 0, lo, hi, mask, threads)
-                    el += time.time() - a
-                else:
-                    for b, t in enumerate(tok_np[s].tolist()):      # untimed: the pattern bookkeeping
-                        if t < 0:
-                            pats[b] = []
-                        else:
-                            pats[b].append(t)
-                    flat = np.fromiter((t for p in pats for t in p), dtype=np.int64)
-                    offs = np.zeros(B + 1, dtype=np.int64)
-                    np.cumsum([len(p) for p in pats], out=offs[1:])
-                    a = time.time()
-                    ref.full_step(flat, offs, SHIFT, lo, hi, mask, threads, faithful=True)
-                    el += time.time() - a
-                steps += 1
-                s += 1
-                if el >= seconds:
-                    break
-            last = s - 1
-            ok = bool(np.array_equal(lo, lo_all[last]) and np.array_equal(hi, hi_all[last]))
-            gmask = fm.allowed_mask(lo_hist[last], hi_hist[last], V, SHIFT).cpu().numpy()
-            mok = bool(np.array_equal(mask, gmask))
-            legs[f"{mode}_{'1' if threads == 1 else 'all'}"] = {
-                "value": steps * B / el, "threads": threads, "steps": steps, "seconds": round(el, 2),
-                "ranges_match_gpu": ok, "masks_match_gpu": mok}
-            log(f"cpu {mode} x{threads}: {steps * B / el:.0f} masks/s over {steps} steps ({el:.1f}s); "
-                f"ranges ok {ok}, masks ok {mok}")
+    for (mode, threads), (lo, hi, mask, _, _, rates) in state.items():
+        ok = bool(np.array_equal(lo, lo_all[last]) and np.array_equal(hi, hi_all[last]))
+        gmask = fm.allowed_mask(lo_hist[last], hi_hist[last], V, SHIFT).cpu().numpy()
+        mok = bool(np.array_equal(mask, gmask))
+        med = float(np.median(rates))
+        legs[f"{mode}_{'1' if threads == 1 else 'all'}"] = {
+            "value": med, "min": float(min(rates)), "max": float(max(rates)),
+            "spread": float((max(rates) - min(rates)) / med), "reps": reps, "threads": threads,
+            "steps": window, "ranges_match_gpu": ok, "masks_match_gpu": mok}
+        log(f"cpu {mode} x{threads}: median {med:.0f} masks/s ({min(rates):.0f}-{max(rates):.0f}) over "
+            f"{reps} x {window} steps; ranges ok {ok}, masks ok {mok}")
+    # where a single-thread step goes: distinct_count (fm_index.cpp:119-144: three sigma-sized
+    # zeroed vectors + the interval_symbols DFS) of the window's last ranges alone, vs the legs'
+    # whole steps -- the searches of either mode are a small part of a step
+    dts = []
+    for _ in range(3):
+        a = time.perf_counter()
+        for l_, h_ in zip(lo_all[last].tolist(), hi_all[last].tolist()):
+            ref.distinct_count(int(l_), int(h_))
+        dts.append(time.perf_counter() - a)
+    per_step = {"distinct_count_only": float(np.median(dts)),
+                "incremental": B / legs["incremental_1"]["value"],
+                "full_research": B / legs["full_research_1"]["value"]}
+    log(f"cpu 1-thread seconds per step: {per_step}")
     head = legs["incremental_all"]
     return {"value": head["value"], "unit": "masks/s", "cores": all_cores, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "sample": f"{head['steps']} decode steps x {B} rows of the same trace from step {warmup}, same "
-                      f"n={bwt.numel()} index; sdsl-faithful wt_int + rank_support_v restatement "
-                      f"(oracle/cpu_ref.cpp); value = the incremental leg on all {all_cores} cores this "
-                      f"process may use (the fastest CPU mode); the reference's own per-step work is the "
-                      f"full_research legs",
+            "sample": f"trace steps {first}..{last} ({window} steps x {B} rows) of the same trace and "
+                      f"n={bwt.numel()} index, after one untimed warm-up step, median of {reps} repetitions; "
+                      f"sdsl-faithful wt_int + rank_support_v restatement (oracle/cpu_ref.cpp); value = the "
+                      f"incremental leg on all {all_cores} cores this process may use (the fastest CPU mode); "
+                      f"the reference's own per-step work is the full_research legs",
             "legs": legs,
+            "one_thread_s_per_step": per_step,
             "ranges_match_gpu": all(v["ranges_match_gpu"] for v in legs.values()),
             "masks_match_gpu": all(v["masks_match_gpu"] for v in legs.values())}
 
 
 # ---------------------------------------------------------------------------
-def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, halo=128):
+def mem_log(tag, dev):
+    free, total = torch.cuda.mem_get_info(dev)
+    log(f"[mem] {tag}: {free / 2**30:.1f} GiB free of {total / 2**30:.1f}")
+
+
+def shard_trace(fm, text, bwt, B, V, S, dev):
+    """The trace every rank of the sharded mode decodes (the same rows on every
+    rank: seeded identically), taken from the replica while it and the corpus
+    are resident, with the replica's uint8 masks of the last step (the
+    exactness reference).  Computing it here lets the legs free the replica
+    before they regenerate the corpus (replica + corpus + a build would not fit
+    in HBM together at C3)."""
+    tokens, _, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S, 777, dev)
+    ref = fm.allowed_mask(lo_hist[S - 1], hi_hist[S - 1], V, SHIFT)
+    return tokens, pats0, ref
+
+
+def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, halo=128):
     """Doc-range sharded decode, measured after the
     replica run at N > 1.  The trace (tokens + initial patterns) and the
     reference masks of its last step come from the replica (unsharded) index;
@@ -295,17 +361,15 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, halo=
     from fmidx.sharding import or_bits, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
-    text, beg = markov_corpus_gpu(n_tokens, V, text_seed, dev)
     S = W + K
-    tokens, _, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S, 777, dev)
-    del bwt
-    ref = fm.allowed_mask(lo_hist[S - 1], hi_hist[S - 1], V, SHIFT)   # unsharded masks of the last step
-    del fm
+    tokens, pats0, ref = sh                   # shard_trace: the same rows on every rank
+    del bwt, fm
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     t0 = time.time()
     ix, err = None, ""
     try:
+        text, beg = markov_corpus_gpu(n_tokens, V, text_seed, dev)
         shard, (a, b) = shard_text_device(text, beg, world, rank, halo)
         del text
         torch.cuda.empty_cache()
@@ -371,6 +435,176 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, halo=
                     "fused OR + unpack (fm_or_bits) to uint8 [B, V]; eager launches"}
 
 
+COMPACT_ENV = {"FMIDX_TRANS": "1", "FMIDX_LF_E": "0", "FMIDX_PROBE_FIRST": "0"}
+
+
+def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace, sh, world=8, halo=128):
+    """Legs that need the replica index gone (N = 1, C3): the compact memory
+    profile of the same corpus, then C4 on one GPU.  Returns
+    (compact, c4) result dicts.
+
+    Compact: the index rebuilt with COMPACT_ENV (transitions to cached children
+    only, no E array, no probe-first) -- the same BWT, so the headline trace's K
+    steps replay from the same state and must end in the same ranges; timed
+    cold like the headline.
+
+    C4 (the corpus doc-range sharded 8 ways) rehearsed on ONE
+    GPU: the 8 shards are built one after another, each decodes the B rows of
+    the replica's trace with its K timed steps captured in a HIP graph (cold
+    replay after a 1 GiB eviction, as the headline), writing bit-packed rows --
+    the per-rank kernel work of the 8-GPU run at n/8 rows -- and the OR of the
+    8 shards' last-step rows (fm_or_bits, the only post-exchange pass) is timed
+    the same way and checked against the replica's uint8 mask.  The exchange
+    itself (all_gather of 8 x B x V/8 bytes over xGMI) cannot run on one GPU;
+    ``predicted_step_us`` adds a stated model of it."""
+    from fmidx.sharding import or_bits, shard_text_device
+
+    fm, bwt = holder.pop(), holder.pop()
+    S = W + K
+    tokens, pats0, ref = sh                   # shard_trace, taken while the replica was resident
+    del bwt, fm
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    mem_log("replica freed", dev)
+    text, beg = markov_corpus_gpu(n_tokens, V, text_seed, dev)
+    flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+
+    def replay(g, cold):
+        if cold:
+            flush.add_(1)
+        torch.cuda.synchronize()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b)
+
+    # ---- the compact memory profile, same corpus and trace as the headline
+    compact = {}
+    try:
+        m_tok, m_lo, m_hi, f_lo, f_hi = main_trace
+        old = {k: os.environ.get(k) for k in COMPACT_ENV}
+        os.environ.update(COMPACT_ENV)
+        try:
+            t0 = time.time()
+            cx = FMIndex(device=dev.index)
+            cx.initialize_from_text_device(text)
+            torch.cuda.synchronize()
+            cbuild = time.time() - t0
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+        lo, hi = m_lo.clone(), m_hi.clone()
+        bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(K):
+                src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+                cx.decode_step(m_tok[i], src[0], src[1], mask, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1])
+        warm = []
+        for _ in range(3):
+            lo.copy_(m_lo)
+            hi.copy_(m_hi)
+            warm.append(replay(g, False) / K * 1e3)
+        lo.copy_(m_lo)
+        hi.copy_(m_hi)
+        cold = replay(g, True) / K * 1e3
+        fin = bufs[K % 2]
+        cst = cx.stats()
+        compact = {"env": dict(COMPACT_ENV), "device_bytes": int(cst["device_bytes"]), "build_s": round(cbuild, 1),
+                   "cold_ms_per_step": cold / 1e3, "warm_ms_per_step": float(np.median(warm)) / 1e3,
+                   "value_cold": B / (cold * 1e-6),
+                   "ranges_equal_default_profile": bool(torch.equal(fin[0], f_lo) and torch.equal(fin[1], f_hi))}
+        log(f"compact profile: {cst['device_bytes'] / 2**30:.1f} GiB, step cold {cold:.1f}us warm {np.median(warm):.1f}us, "
+            f"exact {compact['ranges_equal_default_profile']}")
+        del g, cx, bufs, lo, hi, mask
+        torch.cuda.empty_cache()
+    except Exception as e:      # the C4 leg and the line still run
+        compact = {"error": repr(e)}
+
+    def c4_part():
+        lens = [len(p) for p in pats0]
+        assert max(lens) + S <= halo - 1, "trace patterns would outgrow the halo"
+        offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
+        toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
+        Wd = (V + 31) // 32
+        parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
+        shards = []
+        for r in range(world):
+            t0 = time.time()
+            t_r, (a, b) = shard_text_device(text, beg, world, r, halo)
+            ix = FMIndex(device=dev.index)
+            ix.initialize_from_text_device(t_r)
+            rows = t_r.numel()
+            del t_r
+            torch.cuda.synchronize()
+            build_s = time.time() - t0
+            lo = torch.zeros(B, dtype=torch.int64, device=dev)
+            hi = torch.zeros(B, dtype=torch.int64, device=dev)
+            ix.backward_search_batch(toks, offs, SHIFT, lo, hi)
+            lo[1], hi[1] = 0, 0                    # the trace's eos row (its pattern ends with an unknown id)
+            for i in range(W):
+                ix.decode_step(tokens[i], lo, hi, parts[r], V, SHIFT, reset_below=0, packed=True)
+            s_lo, s_hi = lo.clone(), hi.clone()
+            bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(K):
+                    src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+                    ix.decode_step(tokens[W + i], src[0], src[1], parts[r], V, SHIFT, reset_below=0,
+                                   lo_out=dst[0], hi_out=dst[1], packed=True)
+            warm = []
+            for _ in range(3):
+                lo.copy_(s_lo)
+                hi.copy_(s_hi)
+                warm.append(replay(g, False) / K * 1e3)
+            lo.copy_(s_lo)
+            hi.copy_(s_hi)
+            cold = replay(g, True) / K * 1e3          # leaves parts[r] = this shard's last-step rows
+            st = ix.stats()
+            shards.append({"docs": [int(a), int(b)], "rows": int(rows), "device_bytes": int(st["device_bytes"]),
+                           "build_s": round(build_s, 2), "cold_us_per_step": cold,
+                           "warm_us_per_step": float(np.median(warm))})
+            mem_log(f"c4 shard {r} built", dev)
+            log(f"c4 shard {r}: rows {rows}, build {build_s:.1f}s, step cold {cold:.1f}us warm {np.median(warm):.1f}us")
+            del g, ix, bufs, lo, hi, s_lo, s_hi
+            torch.cuda.empty_cache()
+        out = torch.empty((B, V), dtype=torch.uint8, device=dev)
+        g_or = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_or):
+            or_bits(parts, V, out=out)
+        or_warm = float(np.median([replay(g_or, False) for _ in range(5)])) * 1e3
+        or_cold = replay(g_or, True) * 1e3
+        exact = bool(torch.equal(out, ref))
+        # exchange model: every rank receives (world - 1) packed slices of B x 4 ceil(V/32)
+        # bytes over its 7 point-to-point xGMI links (~153 GB/s each, direct: one slice per
+        # link in parallel) plus a ~15 us collective latency; a ring (one link, 7 hops) is the
+        # pessimistic bound.  The driver's 8-GPU run measures the real figure.
+        slice_b = B * Wd * 4
+        ag_direct = slice_b / 153e9 * 1e6 + 15.0
+        ag_ring = (world - 1) * slice_b / 153e9 * 1e6 + 15.0
+        slow = max(s["cold_us_per_step"] for s in shards)
+        return {"shards": world, "halo": halo, "global_batch": B, "steps": K, "per_shard": shards,
+                "slowest_shard_cold_us": slow, "or_pass_cold_us": or_cold, "or_pass_warm_us": or_warm,
+                "or_pass_bytes": world * slice_b + B * V, "masks_equal_unsharded": exact,
+                "allgather_model_us": {"direct_7_links": ag_direct, "ring": ag_ring,
+                                       "slice_bytes": slice_b, "link_GBps_assumed": 153.0, "latency_us_assumed": 15.0},
+                "predicted_step_us": {"direct": slow + ag_direct + or_cold, "ring": slow + ag_ring + or_cold},
+                "note": "one GPU: shards built and timed in turn (graph-captured K steps, cold), packed rows of all 8 "
+                        "ORed by fm_or_bits and compared with the replica's uint8 mask of the same step"}
+
+    try:
+        return compact, c4_part()
+    except Exception as e:      # the compact result still reaches the line
+        return compact, {"error": repr(e)}
+
+
 # ---------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -381,13 +615,16 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--vocab", type=int, default=128256)
     ap.add_argument("--seed", type=int, default=20250905)
-    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="per CPU-baseline leg (four legs)")
-    ap.add_argument("--cpu-steps", type=int, default=400)
+    ap.add_argument("--cpu-window", type=int, default=3,
+                    help="CPU baseline: trace steps every leg times (after one untimed warm-up step)")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="CPU baseline: repetitions per leg (median reported)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the gather-ceiling probe")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the doc-range sharded leg")
     ap.add_argument("--sharded-at-1", action="store_true",
                     help="run the sharded leg at N = 1 too (one shard; exercises the path on a one-GPU box)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N = 1: skip the one-GPU rehearsal of the 8-way doc-range sharded config (C4)")
     ap.add_argument("--packed", action="store_true",
                     help="bit-packed masks (uint32[B, ceil(V/32)]) instead of uint8[B, V] (not the headline)")
     ap.add_argument("--dump-trace", default="", help="write the timed trace states to this .npz")
@@ -415,13 +652,16 @@ def main():
     st = fm.stats()
     st["lf_e"] = os.environ.get("FMIDX_LF_E", "1") != "0" and n < (1 << 36)
     S = W + K
-    cpu_leg = rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0
-    # the CPU legs replay the same trace past the GPU's steps (bounded by time)
-    S_trace = S + (args.cpu_steps if cpu_leg else 0)
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu and args.cpu_window > 0 and args.cpu_reps > 0
+    # the CPU legs replay steps W .. W + cpu_window of the same trace
+    S_trace = max(S, W + args.cpu_window + 1) if cpu_leg else S
     tokens, init, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
     # rank throughput at scale: RS_ROWS x (RS_STEPS - 1) independent (state,
     # token) pairs of a wider trace, for one k_lf launch (the grouped kernel)
     rs_tok, rs_lo, rs_hi, rs_ref = rank_pairs(fm, text, bwt, V, args.seed + 17 + rank, dev)
+    want_sharded = (world > 1 and not args.no_sharded) or args.sharded_at_1
+    want_c4 = world == 1 and not args.no_c4 and not args.sharded_at_1 and n > 2e9
+    sh = shard_trace(fm, text, bwt, B, V, S, dev) if (want_sharded or want_c4) else None
     del text
     torch.cuda.empty_cache()
     PK = bool(args.packed)
@@ -597,10 +837,11 @@ def main():
                                    "lf").sum())
     rs_us = float(np.median(rs_cold)) * 1e3
     rank_gbs_scale = rs_bytes / (rs_us * 1e-6) / 1e9
-    gather_gbs, chase_ns = (None, None)
+    gather_gbs, chase_ns, gather_modes = (None, None, None)
     if not args.no_gather:
-        gather_gbs, chase_ns = gather_ceiling(dev)
-        log(f"gather ceiling: {gather_gbs:.0f} GB/s independent random 64-B lines; "
+        gather_gbs, chase_ns, gather_modes = gather_ceiling(dev)
+        log(f"gather ceiling: {gather_gbs:.0f} GB/s best independent random 64-B lines "
+            f"({', '.join(f'{k} {v:.0f}' for k, v in gather_modes.items())}); "
             f"dependent chase {chase_ns:.0f} ns/hop (256 chains)")
     # dominant kernel = the fused k_decode (one launch per step)
     decode_bytes = mask_bytes_per_launch + float(lf_dec.mean())
@@ -682,6 +923,7 @@ def main():
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},
         },
+        "device_bytes": st["device_bytes"],
         "index": {"build": build_t, **st},
         "trace_check": ok,
         # the metric's second half ("rank GB/s vs HBM roofline"), summarised: LF throughput at
@@ -690,27 +932,40 @@ def main():
         "rank": {"GBps": rank_gbs_scale, "unit": "GB/s", "peak": HBM_PEAK_GBS,
                  "frac_of_peak": rank_gbs_scale / HBM_PEAK_GBS,
                  "gather_ceiling_GBps": gather_gbs,
+                 "gather_ceiling_by_shape_GBps": gather_modes,
                  "frac_of_gather_ceiling": (rank_gbs_scale / gather_gbs) if gather_gbs else None,
                  "lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6),
                  "b256_GBps": rank_gbs, "b256_avg_launch_us_cold": lf_us_cold},
     }
+    # PMC traffic (tools/pmc_traffic.sh) is collected in a separate rocprofv3 run and committed;
+    # it is used only when it was counted on this very library build, config and mask layout
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    lib_hash = lib_sha16()
+    result["roofline"]["lib_sha16"] = lib_hash
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
                 t = json.load(f)
-            if t.get("corpus_tokens") == n and t.get("batch") == B and not PK:
+            same = t.get("lib_sha16") == lib_hash and t.get("corpus_tokens") == n and t.get("batch") == B and not PK
+            if same:
                 result["roofline"]["traffic"] = t.get("k_decode_bytes_per_launch")
+                result["roofline"]["traffic_source"] = "profiles/pmc_traffic.json (same lib_sha16, n, B)"
                 if t.get("k_lf_bytes_per_launch") is not None:
                     result["standalone_kernels"]["k_lf"]["pmc_bytes_per_launch"] = t["k_lf_bytes_per_launch"]
+            else:
+                result["roofline"]["traffic_source"] = (f"none: profiles/pmc_traffic.json was counted on lib "
+                                                        f"{t.get('lib_sha16')} / n={t.get('corpus_tokens')}, "
+                                                        f"this run is lib {lib_hash} / n={n}")
         except Exception:
             pass
-    pr = os.path.join(REPO, "profiles", "r02_rank", "pmc", "pmc_rank.json")
+    pr = os.path.join(REPO, "profiles", "pmc_rank.json")
     if os.path.exists(pr) and n > 4e9:
         try:   # tools/pmc_rank.sh: the 2^19-row grouped launches of tools/probe_rank.py on a C3 index
             with open(pr) as f:
                 t = json.load(f)
             big = [(a, b) for a, b in zip(t["fetch_bytes"], t["write_bytes"]) if b >= 8e6]
+            if t.get("lib_sha16") != lib_hash:
+                big = []
             if big:
                 result["standalone_kernels"]["k_lf"]["at_scale"]["pmc_bytes_per_launch"] = float(
                     np.median([a + b for a, b in big]))
@@ -719,10 +974,10 @@ def main():
     if cpu_leg:
         try:
             result["cpu_baseline"] = cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, W,
-                                                  args.cpu_seconds, dev)
+                                                  args.cpu_window, args.cpu_reps, dev)
         except Exception as e:  # the GPU line must still print
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
-    if (world > 1 and not args.no_sharded) or args.sharded_at_1:
+    if want_sharded:
         if world == 1:
             import torch.distributed as dist
 
@@ -733,11 +988,25 @@ def main():
         del bwt, fm
         torch.cuda.empty_cache()
         try:
-            result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, B, K, W, world, rank, dev)
+            result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, B, K, W, world, rank, dev, sh)
             log(f"sharded: {result['sharded']['value'] / 1e6:.2f} M masks/s, "
                 f"{result['sharded']['ms_per_step'] * 1e3:.1f} us/step, exact {result['sharded']['masks_equal_unsharded']}")
         except Exception as e:  # the replica line must still print
             result["sharded"] = {"value": None, "error": repr(e)}
+    elif want_c4:
+        holder = [bwt, fm]
+        del bwt, fm
+        torch.cuda.empty_cache()
+        try:
+            main_trace = (tokens[W:S], state_lo, state_hi, lo_hist[S - 1], hi_hist[S - 1])
+            result["compact_profile"], result["c4_one_gpu"] = after_replica_legs(
+                holder, args.seed, n_tokens, V, B, K, W, dev, main_trace, sh)
+            c4 = result["c4_one_gpu"]
+            log(f"c4 on one GPU: slowest shard {c4['slowest_shard_cold_us']:.1f}us cold, OR {c4['or_pass_cold_us']:.1f}us, "
+                f"exact {c4['masks_equal_unsharded']}, predicted 8-GPU step {c4['predicted_step_us']['direct']:.0f}"
+                f"-{c4['predicted_step_us']['ring']:.0f}us")
+        except Exception as e:  # the replica line must still print
+            result["c4_one_gpu"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

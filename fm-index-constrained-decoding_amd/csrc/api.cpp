@@ -5,6 +5,7 @@
 // of host arguments for the synchronous SWIG-equivalent calls.  Every query
 // computes on the GPU through the launchers in query.hip.
 #include "fmidx_internal.h"
+#include "fileformat.h"
 #include "sais.h"
 #include "../../include/fmidx.h"
 
@@ -413,23 +414,46 @@ int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint
   return 0;
 }
 
-constexpr char kMagic[8] = {'F', 'M', 'I', 'D', 'X', 'A', 'M', 'D'};
-
 }  // namespace
+
+// Every extern "C" entry catches what the host code may throw (std::bad_alloc
+// from a vector sized by a huge request, anything from the standard library)
+// and reports it as a status + fm_last_error(): no C++ exception crosses the
+// C-ABI into ctypes / cgo / JNI callers.
+#define FM_API_BEGIN try {
+#define FM_API_CATCH(RET)                          \
+  }                                                \
+  catch (const std::bad_alloc&) {                  \
+    set_error("out of host memory");               \
+    RET;                                           \
+  }                                                \
+  catch (const std::exception& e) {                \
+    set_error("C++ exception: %s", e.what());      \
+    RET;                                           \
+  }                                                \
+  catch (...) {                                    \
+    set_error("unknown C++ exception");            \
+    RET;                                           \
+  }
+#define FM_API_END FM_API_CATCH(return -1)
+#define FM_API_END_VOID FM_API_CATCH(return)
 
 extern "C" {
 
 const char* fm_last_error(void) { return fmidx::g_err.c_str(); }
 
 int fm_device_info(int device, char* buf, size_t cap) {
+  FM_API_BEGIN
   hipDeviceProp_t p;
   FM_HIP(hipGetDeviceProperties(&p, device));
   std::snprintf(buf, cap, "%s cu=%d hbm=%zuMB", p.gcnArchName, p.multiProcessorCount,
                 (size_t)(p.totalGlobalMem >> 20));
   return 0;
+  FM_API_END
 }
 
 int fm_create(fm_index** out, int device) {
+  FM_API_BEGIN
   if (!out) {
     set_error("null out");
     return -1;
@@ -455,9 +479,11 @@ int fm_create(fm_index** out, int device) {
   }
   *out = h;
   return 0;
+  FM_API_END
 }
 
 void fm_destroy(fm_index* h) {
+  FM_API_BEGIN
   if (!h) return;
   {
     DeviceGuard g(h->idx.device);
@@ -471,9 +497,11 @@ void fm_destroy(fm_index* h) {
     if (h->idx.stream) (void)hipStreamDestroy(h->idx.stream);
   }
   delete h;
+  FM_API_END_VOID
 }
 
 int fm_initialize(fm_index* h, const uint64_t* data, uint64_t n) {
+  FM_API_BEGIN
   FM_CHECK_HANDLE(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -482,9 +510,11 @@ int fm_initialize(fm_index* h, const uint64_t* data, uint64_t n) {
     return -1;
   }
   return initialize_symbols(h, data, n);
+  FM_API_END
 }
 
 int fm_initialize_from_file(fm_index* h, const char* path, int width) {
+  FM_API_BEGIN
   FM_CHECK_HANDLE(h);
   if (width != 1 && width != 2 && width != 4 && width != 8) {
     set_error("unsupported width %d", width);
@@ -506,10 +536,12 @@ int fm_initialize_from_file(fm_index* h, const char* path, int width) {
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   return initialize_symbols(h, data.data(), n);
+  FM_API_END
 }
 
 int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n,
                                   const uint64_t* d_sa, const uint32_t* d_text, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_HANDLE(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -529,10 +561,12 @@ int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n
   }
   FM_HIP(hipStreamSynchronize(x.stream));
   return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
+  FM_API_END
 }
 
 int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t n, int keep_sa_text,
                                    void* stream) {
+  FM_API_BEGIN
   FM_CHECK_HANDLE(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -557,38 +591,62 @@ int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t
     if (rc) return -1;
   }
   return fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream);
+  FM_API_END
+}
+
+int fm_attach_isa_samples_device(fm_index* h, const uint64_t* d_isa, uint64_t nisa, void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (!d_isa) {
+    set_error("null ISA samples");
+    return -1;
+  }
+  FM_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  return fmidx::device_samples_from_isa(&h->idx, d_isa, nisa, h->idx.stream);
+  FM_API_END
 }
 
 int fm_suffix_sort_device(const uint32_t* d_text, uint64_t n, uint32_t* d_bwt, uint64_t* d_sa, void* stream) {
+  FM_API_BEGIN
   if (!d_text) {
     set_error("null text");
     return -1;
   }
   return fmidx::gpu_suffix_sort(d_text, n, d_bwt, d_sa, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_wt_int_levels_device(const uint32_t* d_bwt, uint64_t n, uint32_t L, uint64_t* d_words, void* stream) {
+  FM_API_BEGIN
   if (!d_bwt || !d_words || n == 0) {
     set_error("null or empty input");
     return -1;
   }
   return fmidx::gpu_wt_int_levels(d_bwt, n, L, d_words, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_size(const fm_index* h, uint64_t* out) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   *out = h->idx.n;
   return 0;
+  FM_API_END
 }
 
 int fm_sigma(const fm_index* h, uint64_t* out) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   *out = h->idx.sigma;
   return 0;
+  FM_API_END
 }
 
 int fm_backward_search_step(fm_index* h, uint64_t symbol, uint64_t low, uint64_t high,
                             uint64_t out[2]) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -601,9 +659,11 @@ int fm_backward_search_step(fm_index* h, uint64_t symbol, uint64_t low, uint64_t
   FM_HIP(hipStreamSynchronize(x.stream));
   std::memcpy(out, hstage_at<uint64_t>(h, o_out), 16);
   return 0;
+  FM_API_END
 }
 
 int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, uint64_t out[2]) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -623,10 +683,12 @@ int fm_backward_search_multi(fm_index* h, const uint64_t* query, uint64_t len, u
   std::memcpy(out, hstage_at<uint64_t>(h, o_out), 16);
   stage_trim(h);
   return 0;
+  FM_API_END
 }
 
 int fm_distinct_count_multi(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint64_t m,
                             uint64_t* out, uint64_t cap, uint64_t* offsets) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -641,10 +703,12 @@ int fm_distinct_count_multi(fm_index* h, const uint64_t* lows, const uint64_t* h
   }
   if (!pairs.empty()) std::memcpy(out, pairs.data(), pairs.size() * 8);
   return 0;
+  FM_API_END
 }
 
 int fm_distinct_count(fm_index* h, uint64_t low, uint64_t high, uint64_t* out, uint64_t cap,
                       uint64_t* k) {
+  FM_API_BEGIN
   uint64_t off[2];
   FM_CHECK_BUILT(h);
   // two-call protocol: with too small a buffer report the size and fail
@@ -661,9 +725,11 @@ int fm_distinct_count(fm_index* h, uint64_t low, uint64_t high, uint64_t* out, u
   }
   std::memcpy(out, tmp.data(), 2 * off[1] * 8);
   return 0;
+  FM_API_END
 }
 
 int fm_distinct(fm_index* h, uint64_t low, uint64_t high, uint64_t* syms, uint64_t cap, uint64_t* k) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const uint64_t need = 2 * std::min<uint64_t>(distinct_width(low, high, h->idx.n), h->idx.sigma);
   std::vector<uint64_t> tmp(std::max<uint64_t>(need, 1));
@@ -677,11 +743,13 @@ int fm_distinct(fm_index* h, uint64_t low, uint64_t high, uint64_t* syms, uint64
   }
   for (uint64_t i = 0; i < kk; ++i) syms[i] = tmp[2 * i];
   return 0;
+  FM_API_END
 }
 
 int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offsets, uint64_t m,
                        int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in,
                        uint64_t* lo_out, uint64_t* hi_out) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -711,9 +779,11 @@ int fm_get_range_batch(fm_index* h, const int64_t* tokens, const int64_t* offset
   std::memcpy(hi_out, hstage_at<uint64_t>(h, o_hi2), m * 8);
   stage_trim(h);
   return 0;
+  FM_API_END
 }
 
 int fm_locate(fm_index* h, uint64_t row, uint64_t* out) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   auto& x = h->idx;
   if (row >= x.n) {  // fm_index.cpp:170
@@ -743,10 +813,12 @@ int fm_locate(fm_index* h, uint64_t row, uint64_t* out) {
   FM_HIP(hipMemcpyAsync(out, x.sa + row, 8, hipMemcpyDeviceToHost, x.stream));
   FM_HIP(hipStreamSynchronize(x.stream));
   return 0;
+  FM_API_END
 }
 
 int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, uint64_t cap,
                     uint64_t* len) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   auto& x = h->idx;
   *len = 0;
@@ -803,104 +875,59 @@ int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, ui
     pos = n - 1;
   }
   return 0;
+  FM_API_END
 }
 
-// File layout (little endian): magic "FMIDXAMD", u32 version (2), u32 flags,
-// u64 n, BWT (n x u32); flags & 4: SA samples = mark bits (ceil(n/64) x u64),
-// sa_samp (ceil(n/32) x u32), isa_samp ((n-1)/64 + 1 x u64); flags & 2: T'
-// (n x u32, indexes built without a suffix array).  Version 1 files (flags & 1:
-// the full SA) are read too; their SA is reduced to samples on load.
+// The file layout and its checks: fileformat.h.
+static_assert(fmidx::kFileSaRate == fmidx::kSaRate && fmidx::kFileIsaRate == fmidx::kIsaRate &&
+                  fmidx::kFileSymBits == fmidx::kMaxSymBits,
+              "fileformat.h sampling / symbol constants");
+
 int fm_save(fm_index* h, const char* path) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   auto& x = h->idx;
   const uint64_t n = x.n;
-  const uint64_t nwords = (n + 63) / 64, nsamp = (n + fmidx::kSaRate - 1) / fmidx::kSaRate,
-                 nisa = (n - 1) / fmidx::kIsaRate + 1;
-  std::vector<uint32_t> bwt(n), text, samp;
-  std::vector<uint64_t> mark, isa;
-  FM_HIP(hipMemcpy(bwt.data(), x.bwt, n * 4, hipMemcpyDeviceToHost));
-  uint32_t flags = 0;
+  fmidx::IndexFile f;
+  f.n = n;
+  f.bwt.resize(n);
+  FM_HIP(hipMemcpy(f.bwt.data(), x.bwt, n * 4, hipMemcpyDeviceToHost));
   if (x.mark) {
-    mark.resize(nwords);
-    samp.resize(nsamp);
-    isa.resize(nisa);
-    FM_HIP(hipMemcpy(mark.data(), x.mark, nwords * 8, hipMemcpyDeviceToHost));
-    FM_HIP(hipMemcpy(samp.data(), x.sa_samp, nsamp * 4, hipMemcpyDeviceToHost));
-    FM_HIP(hipMemcpy(isa.data(), x.isa_samp, nisa * 8, hipMemcpyDeviceToHost));
-    flags |= 4;
+    f.mark.resize(fmidx::file_mark_words(n));
+    f.samp.resize(fmidx::file_samp_count(n));
+    f.isa.resize(fmidx::file_isa_count(n));
+    FM_HIP(hipMemcpy(f.mark.data(), x.mark, f.mark.size() * 8, hipMemcpyDeviceToHost));
+    FM_HIP(hipMemcpy(f.samp.data(), x.sa_samp, f.samp.size() * 4, hipMemcpyDeviceToHost));
+    FM_HIP(hipMemcpy(f.isa.data(), x.isa_samp, f.isa.size() * 8, hipMemcpyDeviceToHost));
   } else if (x.text) {
-    text.resize(n);
-    FM_HIP(hipMemcpy(text.data(), x.text, n * 4, hipMemcpyDeviceToHost));
-    flags |= 2;
+    f.text.resize(n);
+    FM_HIP(hipMemcpy(f.text.data(), x.text, n * 4, hipMemcpyDeviceToHost));
   }
-  std::ofstream f(path, std::ios::binary | std::ios::trunc);
-  if (!f) {
-    set_error("cannot write %s", path);
-    return -1;
-  }
-  const uint32_t version = 2;
-  f.write(kMagic, 8);
-  f.write(reinterpret_cast<const char*>(&version), 4);
-  f.write(reinterpret_cast<const char*>(&flags), 4);
-  f.write(reinterpret_cast<const char*>(&n), 8);
-  f.write(reinterpret_cast<const char*>(bwt.data()), n * 4);
-  if (flags & 4) {
-    f.write(reinterpret_cast<const char*>(mark.data()), nwords * 8);
-    f.write(reinterpret_cast<const char*>(samp.data()), nsamp * 4);
-    f.write(reinterpret_cast<const char*>(isa.data()), nisa * 8);
-  }
-  if (flags & 2) f.write(reinterpret_cast<const char*>(text.data()), n * 4);
-  if (!f) {
-    set_error("write failed: %s", path);
+  std::string err;
+  if (!fmidx::write_index_file(path, std::move(f), err)) {
+    set_error("%s", err.c_str());
     return -1;
   }
   return 0;
+  FM_API_END
 }
 
 int fm_load(fm_index** out, const char* path, int device) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) {
-    set_error("cannot open %s", path ? path : "(null)");
+  FM_API_BEGIN
+  if (!out) {
+    set_error("null out");
     return -1;
   }
-  char magic[8];
-  uint32_t version = 0, flags = 0;
-  uint64_t n = 0;
-  f.read(magic, 8);
-  f.read(reinterpret_cast<char*>(&version), 4);
-  f.read(reinterpret_cast<char*>(&flags), 4);
-  f.read(reinterpret_cast<char*>(&n), 8);
-  if (!f || std::memcmp(magic, kMagic, 8) != 0 || (version != 1 && version != 2) || n == 0) {
-    set_error("%s is not an fmidx index file", path);
+  *out = nullptr;
+  fmidx::IndexFile f;
+  std::string err;
+  if (!fmidx::read_index_file(path, f, err)) {   // sizes, samples and symbols checked here
+    set_error("%s", err.c_str());
     return -1;
   }
-  const uint64_t nwords = (n + 63) / 64, nsamp = (n + fmidx::kSaRate - 1) / fmidx::kSaRate,
-                 nisa = (n - 1) / fmidx::kIsaRate + 1;
-  std::vector<uint32_t> bwt(n), text, samp;
-  std::vector<uint64_t> sa, mark, isa;
-  f.read(reinterpret_cast<char*>(bwt.data()), n * 4);
-  if (version == 1 && (flags & 1)) {
-    sa.resize(n);
-    f.read(reinterpret_cast<char*>(sa.data()), n * 8);
-  }
-  if (version == 2 && (flags & 4)) {
-    mark.resize(nwords);
-    samp.resize(nsamp);
-    isa.resize(nisa);
-    f.read(reinterpret_cast<char*>(mark.data()), nwords * 8);
-    f.read(reinterpret_cast<char*>(samp.data()), nsamp * 4);
-    f.read(reinterpret_cast<char*>(isa.data()), nisa * 8);
-  }
-  if (flags & 2) {
-    text.resize(n);
-    f.read(reinterpret_cast<char*>(text.data()), n * 4);
-  }
-  if (!f) {
-    set_error("truncated index file %s", path);
-    return -1;
-  }
+  const uint64_t n = f.n;
   fm_index* h = nullptr;
   if (fm_create(&h, device)) return -1;
   {
@@ -911,33 +938,35 @@ int fm_load(fm_index** out, const char* path, int device) {
       return -1;
     };
     if (hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4) != hipSuccess) return fail();
-    if (hipMemcpy(x.bwt, bwt.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
-    if (!sa.empty()) {
+    if (hipMemcpy(x.bwt, f.bwt.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
+    if (!f.sa.empty()) {
       uint64_t* d_sa = nullptr;
       if (hipMalloc(reinterpret_cast<void**>(&d_sa), n * 8) != hipSuccess) return fail();
-      const bool ok = hipMemcpy(d_sa, sa.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
+      const bool ok = hipMemcpy(d_sa, f.sa.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess &&
                       fmidx::device_build_samples(&x, d_sa, n, x.stream) == 0;
       (void)hipFree(d_sa);
       if (!ok) return fail();
-    } else if (!mark.empty()) {
+    } else if (!f.mark.empty()) {
+      const uint64_t nwords = f.mark.size(), nsamp = f.samp.size(), nisa = f.isa.size();
       if (hipMalloc(reinterpret_cast<void**>(&x.mark), nwords * 8) != hipSuccess ||
           hipMalloc(reinterpret_cast<void**>(&x.sa_samp), nsamp * 4) != hipSuccess ||
           hipMalloc(reinterpret_cast<void**>(&x.isa_samp), nisa * 8) != hipSuccess)
         return fail();
-      if (hipMemcpy(x.mark, mark.data(), nwords * 8, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(x.sa_samp, samp.data(), nsamp * 4, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(x.isa_samp, isa.data(), nisa * 8, hipMemcpyHostToDevice) != hipSuccess)
+      if (hipMemcpy(x.mark, f.mark.data(), nwords * 8, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(x.sa_samp, f.samp.data(), nsamp * 4, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(x.isa_samp, f.isa.data(), nisa * 8, hipMemcpyHostToDevice) != hipSuccess)
         return fail();
       if (fmidx::device_finish_samples(&x, n, x.stream)) return fail();
     }
-    if (!text.empty() && !x.isa_samp) {
+    if (!f.text.empty() && !x.isa_samp) {
       if (hipMalloc(reinterpret_cast<void**>(&x.text), n * 4) != hipSuccess) return fail();
-      if (hipMemcpy(x.text, text.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
+      if (hipMemcpy(x.text, f.text.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return fail();
     }
     if (fmidx::device_build_from_bwt(&x, x.bwt, n, x.stream)) return fail();
   }
   *out = h;
   return 0;
+  FM_API_END
 }
 
 // ---- batched device entry points ------------------------------------------
@@ -945,44 +974,53 @@ int fm_load(fm_index** out, const char* path, int device) {
 int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
                      const uint64_t* d_lo, const uint64_t* d_hi, uint64_t* d_lo_out,
                      uint64_t* d_hi_out, uint64_t m, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out,
                                d_hi_out, m, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_backward_search_batch(fm_index* h, const int64_t* d_tokens, const int64_t* d_offsets,
                              uint64_t m, int64_t shift, const uint64_t* d_lo_in,
                              const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
                              void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_search(h->idx.view, d_tokens, d_offsets, m, shift, d_lo_in, d_hi_in,
                               d_lo_out, d_hi_out, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_allowed_mask_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
                           uint8_t* d_mask, uint64_t ld, uint64_t vocab, int64_t shift, int packed,
                           void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_mask(h->idx.view, d_lo, d_hi, m, d_mask, ld, vocab, shift, packed,
                             reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
                          const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out,
                          uint64_t* d_hi_out, uint64_t m, uint8_t* d_mask, uint64_t ld,
                          uint64_t vocab, int packed, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_decode(h->idx.view, d_tokens, shift, reset_below, d_lo_in, d_hi_in, d_lo_out,
                               d_hi_out, m, d_mask, ld, vocab, packed, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
                             const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
                             uint64_t* d_counts, uint64_t* d_k, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
@@ -991,32 +1029,40 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
   if (fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k, h->idx.ws, total_cap, s))
     return -1;
   return ws_release(h, s);
+  FM_API_END
 }
 
 int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, uint64_t V,
                     uint64_t ld_scores, uint64_t ld_out, const uint32_t* d_bits, uint64_t ld_bits,
                     const uint32_t* d_unigram_bits, const fm_row_params* d_rows, int64_t eos,
                     void* stream) {
+  FM_API_BEGIN
   static_assert(sizeof(fm_row_params) == 32, "fm_row_params layout");
   return fmidx::launch_epilogue(dtype, d_scores, d_out, B, V, ld_scores, ld_out, d_bits, ld_bits,
                                 d_unigram_bits, d_rows, eos, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_locate_batch(fm_index* h, const uint64_t* d_rows, uint64_t m, uint64_t* d_out, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_locate(h->idx.view, h->idx.samples(), d_rows, m, d_out, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_extract_batch(fm_index* h, const uint64_t* d_begin, const uint64_t* d_end, const uint64_t* d_off, uint64_t m,
                      uint64_t* d_out, void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_extract(h->idx.view, h->idx.samples(), d_begin, d_end, d_off, m, d_out,
                                reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, uint64_t* total_bytes) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
   const uint64_t e = (x.E ? x.n * 8 : 0) + (x.E2 ? x.n * 4 : 0);
@@ -1028,10 +1074,12 @@ int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, u
                    x.w2_bytes + e + x.cache_bytes + x.trans_bytes + x.samp_bytes + (x.sa ? x.n * 8 : 0) +
                    (x.text ? x.n * 4 : 0) + 3 * K * 8;
   return 0;
+  FM_API_END
 }
 
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
              uint64_t* bitmap_bytes, uint64_t* bitmap_block) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
   if (levels) *levels = x.NL;
@@ -1040,10 +1088,12 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
   if (bitmap_bytes) *bitmap_bytes = x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0);
   if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;
   return 0;
+  FM_API_END
 }
 
 int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint64_t* cache_nodes,
                 uint64_t* cache_bytes, uint64_t* cache_min) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
   if (w2_levels) *w2_levels = x.view.NL2;
@@ -1052,22 +1102,27 @@ int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint
   if (cache_bytes) *cache_bytes = x.cache_bytes;
   if (cache_min) *cache_min = x.view.cache_mask ? x.view.cache_min : 0;
   return 0;
+  FM_API_END
 }
 
 int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
   if (entries) *entries = x.trans_entries;
   if (dropped) *dropped = x.trans_dropped;
   if (bytes) *bytes = x.trans_bytes;
   return 0;
+  FM_API_END
 }
 
 int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
                           void* stream) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_cache_probe(h->idx.view, d_lo, d_hi, m, d_out, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_ids, uint64_t B, uint64_t L,
@@ -1075,6 +1130,7 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
                       const int64_t* d_prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* d_prev_state,
                       fm_row_params* d_rows, uint64_t* d_mask_lo, uint64_t* d_mask_hi, int64_t* d_state,
                       uint32_t* d_status, void* stream) {
+  FM_API_BEGIN
   static_assert(sizeof(fm_prep_config) == 192, "fm_prep_config layout");
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
@@ -1085,10 +1141,12 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
   return fmidx::launch_processor_step(h->idx.view, *cfg, d_ids, B, L, ld_ids, d_fdf, fdf_len, d_pow, pow_len,
                                       d_prev_ids, prev_ld, prev_B, d_prev_state, d_rows, d_mask_lo, d_mask_hi,
                                       d_state, d_status, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* a, void* stream) {
-  static_assert(sizeof(fm_processor_args) == 240, "fm_processor_args layout");
+  FM_API_BEGIN
+  static_assert(sizeof(fm_processor_args) == 248, "fm_processor_args layout");
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   if (!cfg || !a) {
@@ -1101,6 +1159,10 @@ int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor
                                    a->pow_len, a->prev_ids, a->prev_ld, a->prev_B, a->prev_state, a->rows, a->mask_lo,
                                    a->mask_hi, a->state, a->status, s))
     return -1;
+  // the status right behind the bookkeeping: the host waits on status_event (not on the whole
+  // call) to learn whether the device path holds, while the mask and the epilogue run
+  if (a->status_host) FM_HIP(hipMemcpyAsync(a->status_host, a->status, 16, hipMemcpyDeviceToHost, s));
+  if (a->status_event) FM_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(a->status_event), s));
   // 2. the allowed bits of the rows that need them (empty ranges give zero rows)
   if (a->B && fmidx::launch_mask(h->idx.view, a->mask_lo, a->mask_hi, a->B, reinterpret_cast<uint8_t*>(a->bits),
                                  a->bits_ld * 4, a->V, cfg->shift, 1, s))
@@ -1109,46 +1171,63 @@ int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor
   if (a->B && fmidx::launch_epilogue(a->dtype, a->scores, a->out, a->B, a->V, a->ld_scores, a->ld_out, a->bits,
                                      a->bits_ld, a->unigram_bits, a->rows, a->eos, s))
     return -1;
-  // 4. this call's ids for the next call's incremental ranges, and the status to the host
+  // 4. this call's ids for the next call's incremental ranges
   if (a->ids_copy && a->B && a->L)
     FM_HIP(hipMemcpy2DAsync(a->ids_copy, a->copy_ld * 8, a->ids, a->ld * 8, a->L * 8, a->B, hipMemcpyDeviceToDevice, s));
-  if (a->status_host) FM_HIP(hipMemcpyAsync(a->status_host, a->status, 16, hipMemcpyDeviceToHost, s));
   return 0;
+  FM_API_END
 }
 
 int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
                uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream) {
+  FM_API_BEGIN
   return fmidx::launch_or_bits(d_parts, nparts, part_stride, B, words_per_row, vocab, d_out, ld_out, unpack,
                                reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream) {
+  FM_API_BEGIN
   return fmidx::launch_probe_gather(d_buf, bytes, chase, loads, threads, d_sink,
                                     reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
 }
 
 int fm_device_bwt(const fm_index* h, const uint32_t** out) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   *out = h->idx.bwt;
   return 0;
+  FM_API_END
 }
 
 #ifdef FMIDX_STAMPS
 // Diagnostic build only (not part of include/fmidx.h): per-workgroup phase
 // stamps of the decode kernel go to d_buf (16 uint64 per workgroup: 8 stamps + the row served), or off.
 int fm_debug_set_stamps(fm_index* h, uint64_t* d_buf) {
+  FM_API_BEGIN
   FM_CHECK_BUILT(h);
   h->idx.view.stamps = d_buf;
   return 0;
+  FM_API_END
 }
 #endif
 
+int fm_reload_tuning(void) {
+  FM_API_BEGIN
+  fmidx::reload_lf_tuning();
+  return 0;
+  FM_API_END
+}
+
 int fm_synchronize(fm_index* h) {
+  FM_API_BEGIN
   FM_CHECK_HANDLE(h);
   FM_GUARD(h);
   FM_HIP(hipDeviceSynchronize());
   return 0;
+  FM_API_END
 }
 
 }  // extern "C"

@@ -678,12 +678,18 @@ int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStr
 // locate.hip: samples from a device suffix array (uint64[n]); from loaded samples
 int device_build_samples(Index* h, const uint64_t* d_sa, uint64_t n, hipStream_t s);
 int device_finish_samples(Index* h, uint64_t n, hipStream_t s);
+// locate.hip: samples of an index built from a BWT, from ISA samples (isa[k] = row of position 64 k)
+int device_samples_from_isa(Index* h, const uint64_t* d_isa, uint64_t nisa, hipStream_t s);
 int launch_locate(const DevView& v, const SampleView& sv, const uint64_t* rows, uint64_t m, uint64_t* out,
                   hipStream_t s);
 int launch_extract(const DevView& v, const SampleView& sv, const uint64_t* begin, const uint64_t* end,
                    const uint64_t* off, uint64_t m, uint64_t* out, hipStream_t s);
 
 // query.hip launchers
+// re-reads the LF / search launch variants from the environment (query.hip)
+void reload_lf_tuning();
+// locate.hip: rows of the positions that are multiples of kSaRate, from ISA samples
+int launch_isa_walk(const DevView& v, const uint64_t* isa, uint64_t nisa, uint64_t* rows_out, hipStream_t s);
 int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s);

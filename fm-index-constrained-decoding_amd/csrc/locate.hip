@@ -19,6 +19,11 @@
 // the index has it, else the 2-level wavelet-matrix descent of lf_step_decode.
 #include "fmidx_internal.h"
 
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
 namespace fmidx {
 
 namespace {
@@ -30,6 +35,11 @@ int dalloc(T** p, size_t count) {
   *p = nullptr;
   FM_HIP(hipMalloc(reinterpret_cast<void**>(p), (count ? count : 1) * sizeof(T)));
   return 0;
+}
+
+__global__ void __launch_bounds__(kThreads) k_iota_u32(uint32_t* __restrict__ out, uint64_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < m) out[i] = (uint32_t)i;
 }
 
 // one wave per 64-row word: the mark bits, and the ISA samples (scatter)
@@ -151,7 +161,187 @@ __global__ void __launch_bounds__(kThreads) k_extract(DevView v, SampleView sv, 
   }
 }
 
+// The text-order SA samples from ISA samples alone (an index read from a file
+// that holds the BWT and isa[k] = row of text position 64 k -- sdsl's
+// isa_sampling<> of a csa_wt_int<>, fmidx/sdsl_fmi.py): block k walks LF from
+// the row of position p_start = 64 (k + 1) (the last block: n - 1, whose row
+// is 0 -- the sentinel suffix) down to position 64 k, each step one position
+// back (LF(isa[p]) = isa[p - 1]), recording the row of every position that is
+// a multiple of 32 in rows_out[p / 32].  The walk must arrive at isa[k]: the
+// caller checks rows_out[2 k] == isa[k] for every block (a mismatch = an
+// inconsistent BWT / sample pair; no atomics here).
+// One lane per block when the index has the E array (LF | BWT in one load),
+// one wave per block through lf_row otherwise.
+template <bool LANE>
+__global__ void __launch_bounds__(kThreads) k_isa_walk(DevView v, const uint64_t* __restrict__ isa, uint64_t nisa,
+                                                       uint64_t* __restrict__ rows_out) {
+  const uint64_t gid = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint64_t k = LANE ? gid : gid >> 6;
+  if (k >= nisa) return;
+  const bool last = k + 1 >= nisa;
+  const uint64_t p_start = last ? v.n - 1 : kIsaRate * (k + 1);
+  uint64_t row = last ? 0 : isa[k + 1];
+  const uint64_t p_end = kIsaRate * k;
+  const bool writer = LANE || (threadIdx.x & 63u) == 0;
+  for (uint64_t p = p_start; p > p_end; --p) {
+    if (writer && (p & (kSaRate - 1)) == 0 && p < kIsaRate * (k + 1)) rows_out[p / kSaRate] = row;
+    if (row >= v.n) break;                                   // a corrupt sample: caught by the caller's check
+    uint64_t lf;
+    if (LANE) {
+      lf = v.E[row] & kELfMask;
+    } else {
+      uint32_t c;
+      lf_row(v, row, lf, c);
+    }
+    row = lf;
+  }
+  if (writer) rows_out[p_end / kSaRate] = row;
+}
+
+// mark words from the sorted marked rows, without atomics: the first row of
+// every 64-row word ORs the (<= 64) sorted rows of that word and writes it
+__global__ void __launch_bounds__(kThreads) k_mark_from_sorted(const uint64_t* __restrict__ rows, uint64_t m,
+                                                               uint64_t* __restrict__ mark) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t w = rows[i] >> 6;
+  if (i > 0 && (rows[i - 1] >> 6) == w) return;
+  uint64_t bits = 0;
+  for (uint64_t j = i; j < m && (rows[j] >> 6) == w; ++j) bits |= 1ull << (rows[j] & 63);
+  mark[w] = bits;
+}
+
+struct IsaOutOfRange {
+  const uint64_t* isa;
+  uint64_t n;
+  __host__ __device__ uint64_t operator()(uint64_t k) const { return isa[k] >= n ? 1ull : 0ull; }
+};
+
+// a block whose walk did not arrive at its own sample (rows[2 k] = the row reached for position 64 k)
+struct WalkMismatch {
+  const uint64_t* isa;
+  const uint64_t* rows;
+  __host__ __device__ uint64_t operator()(uint64_t k) const { return rows[2 * k] != isa[k] ? 1ull : 0ull; }
+};
+
+template <typename F>
+int count_where(F f, uint64_t m, uint64_t* d_out, uint64_t& out, hipStream_t s) {
+  rocprim::counting_iterator<uint64_t> iota(0);
+  auto it = rocprim::make_transform_iterator(iota, f);
+  size_t tb = 0;
+  FM_HIP(rocprim::reduce(nullptr, tb, it, d_out, (uint64_t)0, (size_t)m, rocprim::plus<uint64_t>(), s));
+  void* tmp = nullptr;
+  FM_HIP(hipMalloc(&tmp, tb ? tb : 1));
+  const hipError_t e = rocprim::reduce(tmp, tb, it, d_out, (uint64_t)0, (size_t)m, rocprim::plus<uint64_t>(), s);
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  FM_HIP(e);
+  FM_HIP(hipMemcpy(&out, d_out, 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 }  // namespace
+
+// The text-order SA samples of an index built from a BWT, from ISA samples
+// (isa[k] = row of text position 64 k, (n-1)/64 + 1 of them: sdsl
+// isa_sampling<> of a csa_wt_int<>): every sample is checked to be a row, the
+// LF walks (k_isa_walk) give the row of every position that is a multiple of
+// 32, every walk must end at its own block's sample, then the rows are sorted
+// (their order is sa_samp: SA / 32 by row) and the mark words written.
+int device_samples_from_isa(Index* h, const uint64_t* d_isa, uint64_t nisa, hipStream_t s) {
+  const uint64_t n = h->n;
+  if (nisa != (n - 1) / kIsaRate + 1) {
+    set_error("ISA samples: %llu given, (n - 1) / 64 + 1 = %llu expected", (unsigned long long)nisa,
+              (unsigned long long)((n - 1) / kIsaRate + 1));
+    return -1;
+  }
+  const uint64_t nwords = (n + 63) / 64, nblocks = (n + 511) / 512;
+  const uint64_t nsamp = (n + kSaRate - 1) / kSaRate;
+  uint64_t *isa = nullptr, *rows = nullptr, *rows2 = nullptr, *d_cnt = nullptr, *mark = nullptr, *cnt = nullptr,
+           *tmp = nullptr;
+  uint32_t *ord = nullptr, *samp = nullptr;
+  auto cleanup = [&]() {
+    for (void* p : {(void*)isa, (void*)rows, (void*)rows2, (void*)d_cnt, (void*)mark, (void*)cnt, (void*)tmp,
+                    (void*)ord, (void*)samp})
+      if (p) (void)hipFree(p);
+  };
+  if (dalloc(&isa, nisa) || dalloc(&rows, nsamp) || dalloc(&rows2, nsamp) || dalloc(&d_cnt, 1) ||
+      dalloc(&ord, nsamp) || dalloc(&samp, nsamp)) {
+    cleanup();
+    return -1;
+  }
+  FM_HIP(hipMemcpyAsync(isa, d_isa, nisa * 8, hipMemcpyDeviceToDevice, s));
+  uint64_t bad = 0;
+  if (count_where(IsaOutOfRange{isa, n}, nisa, d_cnt, bad, s) || bad) {
+    if (bad) set_error("ISA samples: %llu rows out of range (n = %llu)", (unsigned long long)bad, (unsigned long long)n);
+    cleanup();
+    return -1;
+  }
+  if (launch_isa_walk(h->view, isa, nisa, rows, s) || count_where(WalkMismatch{isa, rows}, nisa, d_cnt, bad, s) ||
+      bad) {
+    if (bad)
+      set_error("ISA samples disagree with the BWT: %llu of %llu LF walks missed their sample", (unsigned long long)bad,
+                (unsigned long long)nisa);
+    cleanup();
+    return -1;
+  }
+  // sort the marked rows; the permutation that sorts them is sa_samp (position / 32 in row order)
+  uint32_t* seq = ord;
+  {
+    size_t tb = 0;
+    int bits = 1;
+    while (bits < 64 && (n - 1) >> bits) ++bits;
+    FM_HIP(rocprim::radix_sort_pairs(nullptr, tb, rows, rows2, seq, samp, (size_t)nsamp, 0, bits, s));
+    void* t = nullptr;
+    FM_HIP(hipMalloc(&t, tb ? tb : 1));
+    hipError_t e = hipSuccess;
+    k_iota_u32<<<(unsigned)((nsamp + kThreads - 1) / kThreads), kThreads, 0, s>>>(seq, nsamp);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = rocprim::radix_sort_pairs(t, tb, rows, rows2, seq, samp, (size_t)nsamp, 0, bits, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(t);
+    if (e != hipSuccess) {
+      cleanup();
+      set_error("sorting the sampled rows: %s", hipGetErrorString(e));
+      return -1;
+    }
+  }
+  if (dalloc(&mark, nwords) || dalloc(&cnt, nblocks) || dalloc(&tmp, nblocks)) {
+    cleanup();
+    return -1;
+  }
+  FM_HIP(hipMemsetAsync(mark, 0, nwords * 8, s));
+  k_mark_from_sorted<<<(unsigned)((nsamp + kThreads - 1) / kThreads), kThreads, 0, s>>>(rows2, nsamp, mark);
+  k_mark_blocks<<<(unsigned)((nblocks + kThreads - 1) / kThreads), kThreads, 0, s>>>(mark, nwords, nblocks, tmp);
+  FM_HIP(hipGetLastError());
+  if (exclusive_scan_u64(tmp, cnt, nblocks, s, nullptr)) {
+    cleanup();
+    return -1;
+  }
+  FM_HIP(hipStreamSynchronize(s));
+  for (void* p : {(void*)h->mark, (void*)h->mark_cnt, (void*)h->sa_samp, (void*)h->isa_samp})
+    if (p) (void)hipFree(p);
+  h->mark = mark;
+  h->mark_cnt = cnt;
+  h->sa_samp = samp;
+  h->isa_samp = isa;
+  h->samp_bytes = nwords * 8 + nblocks * 8 + nsamp * 4 + nisa * 8;
+  mark = cnt = isa = nullptr;
+  samp = nullptr;
+  cleanup();
+  return 0;
+}
+
+int launch_isa_walk(const DevView& v, const uint64_t* isa, uint64_t nisa, uint64_t* rows_out, hipStream_t s) {
+  if (nisa == 0) return 0;
+  if (v.E) {
+    k_isa_walk<true><<<(unsigned)((nisa + kThreads - 1) / kThreads), kThreads, 0, s>>>(v, isa, nisa, rows_out);
+  } else {
+    k_isa_walk<false><<<(unsigned)((nisa * 64 + kThreads - 1) / kThreads), kThreads, 0, s>>>(v, isa, nisa, rows_out);
+  }
+  FM_HIP(hipGetLastError());
+  return 0;
+}
 
 int device_build_samples(Index* h, const uint64_t* d_sa, uint64_t n, hipStream_t s) {
   const uint64_t nwords = (n + 63) / 64, nblocks = (n + 511) / 512;

@@ -36,12 +36,13 @@ __global__ void __launch_bounds__(kLfThreads) k_lf(DevView v, const int64_t* __r
   if (i >= m) return;
   const int64_t t = (int64_t)row_load_u64(tok, m, i);
   uint64_t l = row_load_u64(lo_in, m, i), h = row_load_u64(hi_in, m, i);
-  // Every row takes the LF step, a reset row's result is replaced after it:
-  // with a branch on the token, the compiler sank the (lo, hi) loads into the
-  // non-reset side, behind the token's round trip.
+  // Every row runs lf_step_decode, a reset row with symbol -1 so it leaves at
+  // the dead check (its stale range costs no probe or descent), and its result
+  // is replaced after it: with a branch on the token, the compiler sank the
+  // (lo, hi) loads into the non-reset side, behind the token's round trip.
   const uint32_t* cbm;
   int64_t one;
-  lf_step_decode(v, t + shift, l, h, cbm, one);
+  lf_step_decode(v, t < reset_below ? -1 : t + shift, l, h, cbm, one);
   if (t < reset_below) {
     l = 0;
     h = v.n;
@@ -313,7 +314,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_
   const int64_t t = (int64_t)row_load_u64(tok, m, ii);
   const uint64_t l = row_load_u64(lo_in, m, ii), h = row_load_u64(hi_in, m, ii);
   uint64_t nl, nh;
-  group_step<G, GP, Q>(v, valid, t + shift, l, h, nl, nh);
+  // a reset row takes no step (never joins the wide-row ballots); it is replaced below
+  group_step<G, GP, Q>(v, valid && t >= reset_below, t + shift, l, h, nl, nh);
   if (t < reset_below) {
     nl = 0;
     nh = v.n;
@@ -644,14 +646,21 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
   const uint64_t cap = cap_off[row + 1] - base;
   const uint32_t W = v.bm_words;
   const uint32_t w0 = ch * kDcWords;
-  // output offset of this chunk: set bits before it (chunk 0: also the row's total)
-  uint32_t pre = 0;
-  const uint32_t lim = ch == 0 ? W : min(w0, W);
-  for (uint32_t w = threadIdx.x; w < lim; w += 256) pre += __popc(bm[w]);
-  uint32_t all;
-  (void)block_scan_u32(pre, wave_tot, all);
-  if (ch == 0 && threadIdx.x == 0) k_out[row] = all;
-  const uint32_t before = ch == 0 ? 0u : all;
+  // the row's total and this chunk's output offset (set bits before it); every
+  // chunk needs the total: a row over capacity reports k = ~0 and stores
+  // nothing (k_distinct's contract, fmidx.h fm_distinct_count_batch)
+  uint32_t pre = 0, mine = 0;
+  const uint32_t lim = min(w0, W);
+  for (uint32_t w = threadIdx.x; w < W; w += 256) {
+    const uint32_t c = __popc(bm[w]);
+    mine += c;
+    pre += w < lim ? c : 0u;
+  }
+  uint32_t all, before;
+  (void)block_scan_u32(mine, wave_tot, all);
+  (void)block_scan_u32(pre, wave_tot, before);
+  if (ch == 0 && threadIdx.x == 0) k_out[row] = all <= cap ? all : ~0ull;
+  if (all > cap) return;                     // workgroup-uniform
   const uint32_t wi = w0 + threadIdx.x;
   const uint32_t word = wi < W ? bm[wi] : 0u;
   uint32_t tot;
@@ -771,41 +780,54 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
   return (uint32_t)std::strtoul(s, nullptr, 10);
 }
 
-// Lanes per row of the LF / search launches: 64 (one wave per row) while the
-// rows fit the chip's wave slots (latency: no row waits behind another's wide
-// step), else FMIDX_LF_GROUP lanes (default 2; 64 = never group) above
-// FMIDX_LF_GROUP_MIN rows (default 8192 = 256 CUs x 32 waves).  Measured on
-// the C3 index (tools/probe_rank.py, 2^19 pairs, cold): one wave per row 308 us,
-// G = 16 / 8 / 4 / 2 / 1: 179 / 125 / 99 / 90 / 100 us; get_range of 2^18
-// patterns 2658 us -> 539 us at G = 2.
-uint32_t lf_group(uint64_t m) {
-  static const uint32_t G = [] {
-    const uint32_t g = env_u32("FMIDX_LF_GROUP", 2);
-    return (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 64u;
-  }();
-  static const uint64_t min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
-  return m > min_rows ? G : 64u;
+// LF / search launch variants, read from the environment once and again on
+// fm_reload_tuning() (tests select every variant in one process that way).
+//  * lanes per row: 64 (one wave per row) while the rows fit the chip's wave
+//    slots (latency: no row waits behind another's wide step), else
+//    FMIDX_LF_GROUP lanes (default 2; 64 = never group) above
+//    FMIDX_LF_GROUP_MIN rows (default 8192 = 256 CUs x 32 waves).  Measured on
+//    the C3 index (tools/probe_rank.py, 2^19 pairs, cold): one wave per row
+//    308 us, G = 16 / 8 / 4 / 2 / 1: 179 / 125 / 99 / 90 / 100 us; get_range of
+//    2^18 patterns 2658 us -> 539 us at G = 2.
+//  * FMIDX_LF_GPROBE (default 1): grouped launches with G >= 4 probe the
+//    transition table inside the group, so a cached range's hit needs no
+//    wave-wide step.
+//  * FMIDX_LF_QUAD (default 1): G = 2 LF launches settle wide rows four at a
+//    time (16 lanes each: a probe or a <= 128-row E scan) before the serial
+//    loop: 2^19 cold pairs 87 vs 93 us.  Not in k_search_group, where the extra
+//    registers (155 VGPRs: 3 waves per SIMD) cost more than it saves (565 vs
+//    548 us).
+struct LfTuning {
+  uint32_t G;
+  uint64_t min_rows;
+  bool gprobe;
+  bool quad;
+};
+
+LfTuning load_lf_tuning() {
+  LfTuning t;
+  const uint32_t g = env_u32("FMIDX_LF_GROUP", 2);
+  t.G = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 64u;
+  t.min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
+  t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
+  t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
+  return t;
 }
 
-// Grouped launches (G >= 4) probe the transition table inside the group
-// (FMIDX_LF_GPROBE, default 1): a cached range's hit then needs no wave-wide step.
-bool lf_gprobe() {
-  static const bool on = env_u32("FMIDX_LF_GPROBE", 1) != 0;
-  return on;
+LfTuning& lf_tuning() {
+  static LfTuning t = load_lf_tuning();
+  return t;
 }
 
-// G = 2 LF launches settle wide rows four at a time (16 lanes each: a probe or
-// a <= 128-row E scan) before the serial loop (FMIDX_LF_QUAD, default 1):
-// 2^19 cold pairs 87 vs 93 us.  Not in k_search_group, where the extra
-// registers (155 VGPRs: 3 waves per SIMD) cost more than it saves (565 vs 548 us).
-bool lf_quad() {
-  static const bool on = env_u32("FMIDX_LF_QUAD", 1) != 0;
-  return on;
-}
+uint32_t lf_group(uint64_t m) { return m > lf_tuning().min_rows ? lf_tuning().G : 64u; }
+bool lf_gprobe() { return lf_tuning().gprobe; }
+bool lf_quad() { return lf_tuning().quad; }
 
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
+void reload_lf_tuning() { lf_tuning() = load_lf_tuning(); }
+
 int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s) {

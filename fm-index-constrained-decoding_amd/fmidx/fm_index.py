@@ -346,15 +346,20 @@ class FMIndex:
             hi.copy_(hi_out)
         return mask
 
-    def distinct_count_batch(self, lo, hi):
-        """Device interval_symbols for m ranges -> (syms, counts, k, cap_off)."""
+    def distinct_count_batch(self, lo, hi, cap=None):
+        """Device interval_symbols for m ranges -> (syms, counts, k, cap_off).
+        ``cap`` (int64 device tensor [m]) overrides the per-row capacity
+        (default min(width, sigma), always enough); a row with more distinct
+        symbols than its capacity reports k = UINT64_MAX (-1 here) and writes
+        nothing."""
         import torch
 
         n = self.size()
         sigma = self.sigma()
-        hc = torch.clamp(hi, max=n)
-        width = torch.where((lo == hi) | (lo >= hc), torch.zeros_like(lo), hc - lo)
-        cap = torch.clamp(width, max=sigma)
+        if cap is None:
+            hc = torch.clamp(hi, max=n)
+            width = torch.where((lo == hi) | (lo >= hc), torch.zeros_like(lo), hc - lo)
+            cap = torch.clamp(width, max=sigma)
         cap_off = torch.zeros(lo.numel() + 1, dtype=torch.int64, device=lo.device)
         torch.cumsum(cap, 0, out=cap_off[1:])
         total = int(cap_off[-1].item())
@@ -440,7 +445,13 @@ class FMIndex:
 
 
 def load_FMIndex(path: str, device: Optional[int] = None) -> FMIndex:
-    """fm_index.cpp:201-209 (own binary format)."""
+    """fm_index.cpp:201-209: this engine's own file (csrc/fileformat.h), or a
+    reference ``.fmi`` (sdsl csa_wt_int<> serialisation, fmidx/sdsl_fmi.py --
+    parity unpinned: no sdsl file exists to test against)."""
+    from .sdsl_fmi import is_sdsl_file, load_sdsl_fmi
+
+    if os.path.isfile(path) and is_sdsl_file(path):
+        return load_sdsl_fmi(path, device)
     obj = FMIndex.__new__(FMIndex)
     obj._h = c_void_p()
     obj._device = _default_device() if device is None else int(device)

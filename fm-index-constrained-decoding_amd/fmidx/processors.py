@@ -26,6 +26,7 @@ from __future__ import annotations
 import ctypes
 import functools
 import math
+import os
 from ctypes import c_float, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 from typing import List, Optional, Sequence
 
@@ -88,10 +89,10 @@ class _ProcessorArgs(ctypes.Structure):
                 ("bits", c_void_p), ("bits_ld", c_uint64), ("dtype", c_int32), ("reserved", c_int32),
                 ("scores", c_void_p), ("out", c_void_p), ("V", c_uint64), ("ld_scores", c_uint64),
                 ("ld_out", c_uint64), ("unigram_bits", c_void_p), ("eos", c_int64), ("ids_copy", c_void_p),
-                ("copy_ld", c_uint64), ("status_host", c_void_p)]
+                ("copy_ld", c_uint64), ("status_host", c_void_p), ("status_event", c_void_p)]
 
 
-assert ctypes.sizeof(_ProcessorArgs) == 240
+assert ctypes.sizeof(_ProcessorArgs) == 248
 
 
 class _DeviceStep:
@@ -125,6 +126,14 @@ class _DeviceStep:
         self._state = [None, None]
         self._cur = 0                 # the set the next call writes
         self._prev_ok = False         # the other set holds a valid previous call
+        # The call's status is read after an event recorded right behind the row
+        # bookkeeping (k_prep + the status copy), not after the whole call: the
+        # mask and the epilogue are still running when the output is returned
+        # (torch's stream order covers its consumers).  FMIDX_PROC_WAIT=stream
+        # restores the full synchronize (measurement only).
+        self._ev = torch.cuda.Event()
+        self._ev_ready = False
+        self._wait_stream = os.environ.get("FMIDX_PROC_WAIT", "event") == "stream"
 
     @property
     def prev_ids(self):
@@ -196,9 +205,16 @@ class _DeviceStep:
         a.ids_copy, a.copy_ld = keep.data_ptr(), keep.stride(0)
         a.status_host = self.status_h.data_ptr()
         stream = torch.cuda.current_stream(dev)
+        if not self._ev_ready:          # torch creates the event at its first record
+            self._ev.record(stream)
+            self._ev_ready = True
+        a.status_event = self._ev.cuda_event
         check(lib().fm_processor_call(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
                                       c_void_p(stream.cuda_stream)), "processor_call")
-        stream.synchronize()
+        if self._wait_stream:
+            stream.synchronize()
+        else:
+            self._ev.synchronize()
         st = self._status_np
         if st[0] != 0 or st[1] != st[2]:
             self._prev_ok = False
@@ -669,6 +685,9 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
         self.BOOST = 0.0
         self._core = _BatchedCore(index)
         self._dev = _device_step(self._core, self.BOOST, 1.0, force_decoding_from)
+        self._ids_dev = None        # the sequence's ids on the device (see _device_ids)
+        self._ids_pin = None
+        self._ids_prev = ()
 
     def clone(self):
         return VllmIndexBasedLogitsProcessor(num_beams=self._num_beams, index=self.index,
@@ -678,13 +697,36 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
                                              always_allow_eos=self.always_allow_eos,
                                              forced_bos_token_id=self.forced_bos_token_id)
 
+    def _device_ids(self, toks):
+        """The sequence's output ids as a device int64 [1, L] view.  vLLM hands
+        each sequence's clone its whole output tuple every step, one token
+        longer than last time: only the tokens beyond the part already on the
+        device are staged (pinned) and copied -- one 8-byte copy per step
+        instead of the whole tuple (the prefix is compared on the host first, so
+        a tuple that does not extend the previous one is uploaded whole)."""
+        L = len(toks)
+        buf = self._ids_dev
+        if buf is None or buf.shape[1] < max(L, 1):
+            cap = max(64, 2 * L)
+            self._ids_dev = buf = torch.empty((1, cap), dtype=torch.int64, device=self._dev.dev)
+            self._ids_pin = torch.empty(cap, dtype=torch.int64).pin_memory()
+            self._ids_pin_np = self._ids_pin.numpy()
+            self._ids_prev = ()
+        prev = self._ids_prev
+        k = len(prev) if len(prev) <= L and toks[:len(prev)] == prev else 0
+        if L > k:
+            self._ids_pin_np[k:L] = toks[k:L]
+            buf[0, k:L].copy_(self._ids_pin[k:L], non_blocking=True)
+        self._ids_prev = toks
+        return buf[:, :L]
+
     def __call__(self, input_ids, scores):
-        input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
         scores = scores.unsqueeze(0)
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            out = self._dev(self._device_ids(tuple(input_ids)), scores, self._prep_config(scores.dtype))
             if out is not None:
                 return out
+        input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
         B, V = scores.shape
         dt = scores.dtype
         boost = _round(self.BOOST, dt)

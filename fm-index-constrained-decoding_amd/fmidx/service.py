@@ -19,6 +19,7 @@ The index is any object with the reference FMIndex's query methods plus
 Run: FM_INDEX_PATH=<path> python -m fmidx.service [--port 8000]
 """
 import asyncio
+import itertools
 import logging
 import os
 import time
@@ -256,9 +257,16 @@ def create_app(index=None, index_path: Optional[str] = None, window_s: float = 2
             docs = []
             if count > 0:
                 lim = request.limit
-                docs = await on_worker(lambda: list(index.get_doc_indices(request.sequence)))
-                if lim and len(docs) > lim:
-                    docs = docs[:lim]
+                # get_doc_indices yields in row order, located chunk by chunk on the device:
+                # with a limit only the chunks that reach it are located (the reference
+                # slices the full list, fm_index_api_service.py:121-124 -- same output)
+                if lim and lim > 0:
+                    docs = await on_worker(lambda: list(itertools.islice(index.get_doc_indices(request.sequence),
+                                                                         lim)))
+                else:
+                    docs = await on_worker(lambda: list(index.get_doc_indices(request.sequence)))
+                    if lim and len(docs) > lim:      # a negative limit slices from the end, as there
+                        docs = docs[:lim]
             return SearchResponse(count=count, doc_indices=docs, took_ms=(time.time() - t0) * 1000)
         except HTTPException:
             raise

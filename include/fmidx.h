@@ -81,6 +81,16 @@ int fm_initialize_from_bwt_device(fm_index* h, const uint32_t* d_bwt, uint64_t n
 int fm_initialize_from_text_device(fm_index* h, const uint32_t* d_text, uint64_t n, int keep_sa_text,
                                    void* stream);
 
+/* Adds locate / extract_text to an index built from a BWT alone
+ * (fm_initialize_from_bwt_device) from ISA samples: d_isa[k] = the row of
+ * text position 64 k, nisa = (n - 1) / 64 + 1 (sdsl's isa_sampling<> of a
+ * csa_wt_int<>, i.e. what a reference .fmi holds next to its wavelet tree;
+ * fm_index.cpp:196-209).  The SA samples are rebuilt by LF walks from them.
+ * Every sample is checked (a row < n, and every 64-position walk must arrive at
+ * its own block's sample), else -1 and nothing changes.  No reference
+ * counterpart (the reference loads its .fmi through sdsl load_from_file). */
+int fm_attach_isa_samples_device(fm_index* h, const uint64_t* d_isa, uint64_t nisa, void* stream);
+
 /* The GPU suffix sorter on its own (current device, ``stream``): writes
  * BWT[j] = T'[SA[j] - 1 mod n] to ``d_bwt`` (n uint32, may be NULL) and the
  * suffix array to ``d_sa`` (n uint64, may be NULL). */
@@ -310,9 +320,11 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
  * the hand-offs), so the host makes one call per decode step:
  *   fm_processor_step -> fm_allowed_mask_batch(packed) of (mask_lo, mask_hi)
  *   into bits -> fm_apply_boosts(scores -> out) -> ids copied to ids_copy (the
- *   next call's prev_ids, optional) -> status copied to status_host (pinned,
- *   optional).  Stream-ordered; the caller synchronizes before reading
- *   status_host.  Replaces the per-call work of
+ *   next call's prev_ids, optional).  The status is copied to status_host
+ *   (pinned, optional) right after fm_processor_step, and status_event (a
+ *   hipEvent_t, optional) is recorded behind that copy: the caller waits on the
+ *   event -- the row bookkeeping only -- before reading status_host, while the
+ *   mask and the epilogue still run.  Stream-ordered.  Replaces the per-call work of
  *   document_constrained_generation_causal_qwen.py:101-214 / causal.py:62-180. */
 typedef struct fm_processor_args {
   const int64_t* ids;          /* [B][ld] input_ids */
@@ -341,6 +353,7 @@ typedef struct fm_processor_args {
   int64_t* ids_copy;           /* [B][copy_ld] or null */
   uint64_t copy_ld;
   uint32_t* status_host;       /* pinned [4] or null */
+  void* status_event;          /* hipEvent_t recorded after the status copy, or null */
 } fm_processor_args;
 
 int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* args, void* stream);
@@ -373,11 +386,16 @@ int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
                           void* stream);
 
 /* HBM gather probe (bench roofline of the rank/LF path); no
- * index needed, current device.  chase == 0: ``threads`` threads each load
- * ``loads`` independent random 64-B lines of d_buf[0, bytes) (the random-line
- * throughput ceiling); chase != 0: ``threads`` chains each follow ``loads``
- * dependent hops (next line = the uint64 at the start of the current line
- * mod the line count).  d_sink: >= 1024 uint64 (practically never written). */
+ * index needed, current device.  ``chase`` selects the access pattern over
+ * d_buf[0, bytes), ``threads`` threads each issuing ``loads`` loads:
+ *   0: every thread its own random 64-B line (4 x 16 B) -- per-lane lines;
+ *   1: ``threads`` chains each follow ``loads`` dependent hops (next line =
+ *      the uint64 at the start of the current line mod the line count);
+ *   2: 4 lanes share a random 64-B line, 16 B each (lane-cooperative);
+ *   3: 8 lanes share a random 128-B line, 16 B each;
+ *   4: every thread its own random 8-B word.
+ * Line counts are powers of two (the largest that fits).  d_sink: >= 1024
+ * uint64 (practically never written). */
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream);
 
@@ -386,6 +404,12 @@ int fm_device_bwt(const fm_index* h, const uint32_t** out);
 
 /* Synchronise the handle's device (hipDeviceSynchronize on its device). */
 int fm_synchronize(fm_index* h);
+
+/* Re-reads the launch-variant environment variables of the LF / get_range
+ * launches (FMIDX_LF_GROUP, FMIDX_LF_GROUP_MIN, FMIDX_LF_GPROBE,
+ * FMIDX_LF_QUAD), which are otherwise read once per process.  Call it while
+ * no launch is being issued (tuning and tests).  No reference counterpart. */
+int fm_reload_tuning(void);
 
 #ifdef __cplusplus
 }

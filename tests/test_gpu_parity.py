@@ -224,15 +224,14 @@ def test_incremental_lf_equals_full_research(dev):
         assert got == want, s
 
 
-@pytest.mark.parametrize("cache_min", [None, 4])
-def test_grouped_lf_and_search_vs_oracle(dev, cache_min):
-    """Launches above FMIDX_LF_GROUP_MIN (8192) rows take the grouped kernels
-    (G lanes per row, wide rows by the whole wave): get_range of 20000
-    patterns (index.py:103-114 with its early exit) and one LF step of 20000
-    (state, token) pairs, against the oracle -- dead, empty, full-range,
-    narrow, wide and cached rows, unknown ids, hi past n, reset rows."""
-    import torch
+_GROUPED_CASES = {}
 
+
+def _grouped_case(cache_min):
+    """Index, oracle answers and inputs of the grouped-LF test (built once per
+    cache_min and shared by every launch variant)."""
+    if cache_min in _GROUPED_CASES:
+        return _GROUPED_CASES[cache_min]
     docs = markov_docs(17, 400, 60, 100)
     ours = ours_index(docs, bm_log2=6, cache_min=cache_min)
     ora = OracleIndex()
@@ -253,34 +252,73 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min):
             elif r < 0.12:
                 p[j] = 1000 + int(rng.integers(0, 5))     # beyond the largest symbol
         pats.append(p)
-    toks = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=dev)
-    offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), dtype=torch.int64, device=dev)
-    lo = torch.zeros(m, dtype=torch.int64, device=dev)
-    hi = torch.zeros(m, dtype=torch.int64, device=dev)
-    ours.backward_search_batch(toks, offs, 10, lo, hi)
-    got = list(zip(lo.cpu().tolist(), hi.cpu().tolist()))
     want = [ora.get_range(p) if p else (0, n) for p in pats]
-    bad = [i for i in range(m) if got[i] != want[i]]
-    assert not bad, [(pats[i], got[i], want[i]) for i in bad[:5]]
     # one LF step from every pattern's range (some states past n, some reset)
     nxt = np.where(rng.random(m) < 0.8, [F[int(rng.integers(0, len(F)))] for _ in range(m)],
                    rng.integers(-3, 80, m)).astype(np.int64)
-    lo_in = lo.clone()
-    hi_in = hi.clone()
-    hi_in[::97] = n + 5
-    lo_out, hi_out = torch.empty_like(lo), torch.empty_like(hi)
-    ours.lf_step_batch(torch.tensor(nxt, device=dev), lo_in, hi_in, 10, lo_out=lo_out, hi_out=hi_out,
-                       reset_below=-2)
-    got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
-    li, hv = lo_in.cpu().tolist(), hi_in.cpu().tolist()
+    li = [w[0] for w in want]
+    hv = [w[1] for w in want]
+    hv[::97] = [n + 5] * len(hv[::97])
+    want_lf = []
     for i in range(m):
         t = int(nxt[i])
         if t < -2:
-            w = (0, n)
+            want_lf.append((0, n))
         else:
-            a, b = li[i], min(hv[i], n)
-            w = (0, 0) if a >= b else ora.backward_search_step(t + 10, a, b - 1)
-        assert got[i] == w, (i, t, li[i], hv[i], got[i], w)
+            a_, b_ = li[i], min(hv[i], n)
+            want_lf.append((0, 0) if a_ >= b_ else ora.backward_search_step(t + 10, a_, b_ - 1))
+    _GROUPED_CASES[cache_min] = (ours, pats, want, nxt, li, hv, want_lf)
+    return _GROUPED_CASES[cache_min]
+
+
+# every launch variant of the grouped kernels (csrc/query.hip lf_tuning): lanes per
+# row, the in-group transition probe (G >= 4) and the four-at-a-time wide stage (G = 2)
+_LF_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"},
+                {"FMIDX_LF_GROUP": "4", "FMIDX_LF_GPROBE": "0"}, {"FMIDX_LF_GROUP": "4", "FMIDX_LF_GPROBE": "1"},
+                {"FMIDX_LF_GROUP": "8", "FMIDX_LF_GPROBE": "0"}, {"FMIDX_LF_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
+                {"FMIDX_LF_GROUP": "16"}, {"FMIDX_LF_GROUP": "64"}]
+
+
+@pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k[6:]}{x}" for k, x in v.items()) or "default")
+@pytest.mark.parametrize("cache_min", [None, 4])
+def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
+    """Launches above FMIDX_LF_GROUP_MIN (8192) rows take the grouped kernels
+    (G lanes per row, wide rows by the whole wave): get_range of 20011
+    patterns (index.py:103-114 with its early exit) and one LF step of 20011
+    (state, token) pairs, against the oracle -- dead, empty, full-range,
+    narrow, wide and cached rows, unknown ids, hi past n, reset rows -- for
+    every launch variant (selected through fm_reload_tuning in this process)."""
+    import torch
+
+    from fmidx._lib import lib
+
+    ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
+    m = len(pats)
+    for k in ("FMIDX_LF_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD"):
+        monkeypatch.delenv(k, raising=False)
+    for k, x in variant.items():
+        monkeypatch.setenv(k, x)
+    lib().fm_reload_tuning()
+    try:
+        toks = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=dev)
+        offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), dtype=torch.int64, device=dev)
+        lo = torch.zeros(m, dtype=torch.int64, device=dev)
+        hi = torch.zeros(m, dtype=torch.int64, device=dev)
+        ours.backward_search_batch(toks, offs, 10, lo, hi)
+        got = list(zip(lo.cpu().tolist(), hi.cpu().tolist()))
+        bad = [i for i in range(m) if got[i] != want[i]]
+        assert not bad, [(pats[i], got[i], want[i]) for i in bad[:5]]
+        lo_in = torch.tensor(li, dtype=torch.int64, device=dev)
+        hi_in = torch.tensor(hv, dtype=torch.int64, device=dev)
+        lo_out, hi_out = torch.empty_like(lo), torch.empty_like(hi)
+        ours.lf_step_batch(torch.tensor(nxt, device=dev), lo_in, hi_in, 10, lo_out=lo_out, hi_out=hi_out,
+                           reset_below=-2)
+        got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
+        bad = [i for i in range(m) if got[i] != want_lf[i]]
+        assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
+    finally:
+        monkeypatch.undo()
+        lib().fm_reload_tuning()
 
 
 @pytest.mark.parametrize("cache_min,e2", [(None, "0"), (4, "0"), (None, "1"), (4, "1")])
@@ -742,3 +780,40 @@ def test_sharded_decode_at_scale_one_gpu(dev):
         assert torch.equal(ms[0] | ms[1] | ms[2], want), s
     packed_or = or_bits(parts, V, unpack=False)
     assert torch.equal(packed_or, parts[0] | parts[1] | parts[2])
+
+
+def test_distinct_count_batch_capacity_overflow(dev):
+    """fm_distinct_count_batch's contract (include/fmidx.h): a row whose distinct
+    symbols exceed its capacity reports k = UINT64_MAX and writes nothing --
+    for a BFS row, a cached row (k_distinct_cached) and the full range; the rows
+    around it, with enough capacity, are exact."""
+    import torch
+
+    docs = markov_docs(71, 300, 40, 120)
+    ours = ours_index(docs, bm_log2=5, cache_min=4)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    n = ora.size()
+    assert ours.stats()["trans_entries"] > 0
+    F = [t for d in reversed(docs) for t in d]
+    cand = [ora.get_range(F[s:s + 1]) for s in range(0, 400, 7)]
+    cached = [r for r in cand if r[1] - r[0] >= 8 and
+              bool(ours.cache_contains(torch.tensor([r[0]], device=dev), torch.tensor([r[1]], device=dev))[0])]
+    uncached = [(a, a + 40) for a in range(3, n - 50, 997)]
+    assert cached, "no cached range among the unigram ranges"
+    rows = [cached[0], (0, n), uncached[0], cached[-1], (0, n), uncached[-1]]
+    lo = torch.tensor([r[0] for r in rows], dtype=torch.int64, device=dev)
+    hi = torch.tensor([r[1] for r in rows], dtype=torch.int64, device=dev)
+    ks = [len(ora.distinct_count(a, b)) // 2 for a, b in rows]
+    assert all(k >= 2 for k in ks[:3])
+    cap = torch.tensor([1, 1, 1, ks[3], ks[4], ks[5]], dtype=torch.int64, device=dev)   # first three too small
+    syms, counts, k, cap_off = ours.distinct_count_batch(lo, hi, cap=cap)
+    syms, counts, k, cap_off = [x.cpu().numpy() for x in (syms, counts, k, cap_off)]
+    assert k[:3].tolist() == [-1, -1, -1]
+    for i in range(3, 6):
+        a, b = rows[i]
+        s0 = int(cap_off[i])
+        got = []
+        for j in range(int(k[i])):
+            got += [int(syms[s0 + j]), int(counts[s0 + j])]
+        assert tuple(got) == ora.distinct_count(a, b), i

@@ -351,3 +351,134 @@ def test_c3_locate_extract_from_samples(dev, c3):
         assert list(out) == text[idx].tolist(), d
     assert fm.extract_text(b[0], e[0]) == got[0]
     assert fm.locate(int(rows[0])) == int(pos[0])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("variant,B,Vs,beams", [("qwen", 256, 151936, 4), ("seq", 256, 128256, 4),
+                                                ("causal", 2048, 128256, 4)])
+def test_c3_processors_device_vs_host_vs_cpu_ref(dev, c3, variant, B, Vs, beams):
+    """The processors on the C3 index (n > 2^32, where the range-bitmap cache,
+    the transition table and the hierarchy serve k_prep's LF steps and the
+    packed mask): 12 generation steps with beam reordering, the device path
+    (fm_processor_call) == the host path of the same class, bit for bit; and
+    every row the device path gave allowed bits has bits == the mask cpu_ref
+    computes from that row's pattern, and its range == cpu_ref's get_range.
+    Reference: document_constrained_generation_causal_qwen.py:101-214 (B = 256,
+    Qwen3 vocabulary), document_constrained_generation_seq.py:35-123 (B = 256),
+    document_constrained_generation_causal.py:74-180 (B = 2048, C5's rows)."""
+    import torch
+
+    import fmidx.processors as P
+
+    ix, text, ref = c3["fm"], c3["text"], c3["ref"]
+    n = text.numel()
+    if not hasattr(ix, "occurring_distinct"):
+        # the all-unigrams set of index.py:67 (A7: the full range minus BWT row n - 1, sentinel dropped)
+        raw = ix.distinct_count(0, n - 1)
+        ix.occurring_distinct = [s - SHIFT for s in raw[0::2] if s > 0]
+    g = torch.Generator(device=dev)
+    g.manual_seed({"qwen": 61, "seq": 62, "causal": 63}[variant])
+    q = torch.randint(0, n - 200, (B,), generator=g, device=dev).cpu().numpy()
+
+    def F(j):   # F = reverse(T') (index.py:47-53) token j, as a corpus token id
+        return int(text[n - 2 - j]) - SHIFT
+
+    rng = np.random.default_rng(7)
+    sents = [[F(int(q[b]))] for b in range(B)]
+    kw = dict(num_beams=beams, pad_token_id=0, eos_token_id=2)
+    if variant == "qwen":
+        mk = lambda: P.QwenIndexBasedLogitsProcessor(index=ix, min_new_tokens=3, **kw)   # noqa: E731
+        head = [11, 12, 151645, 198, 151644, 77091, 198, 151667, 271, 151668, 271]
+    elif variant == "causal":
+        mk = lambda: P.CausalIndexBasedLogitsProcessor(index=ix, model_name="llama-3", **kw)   # noqa: E731
+        head = [11, 12, 78191, 128007, 271]
+    else:
+        mk = lambda: P.SeqIndexBasedLogitsProcessor(index=ix, **kw)   # noqa: E731
+        head = [1]                                                     # the decoder start token
+    dev_p, host_p = mk(), mk()
+    host_p._dev = None
+    groups = B // beams
+    flagged_total = 0
+    for step in range(12):
+        perm = np.concatenate([gr * beams + rng.permutation(beams) for gr in range(groups)])
+        sents = [list(sents[i]) for i in perm]
+        q = q[perm]
+        if step:
+            for b in range(B):
+                r = rng.random()
+                sents[b].append(F(int(q[b]) + len(sents[b])) if r < 0.85 else int(rng.integers(3, 128000)))
+        ids = torch.tensor([head + s for s in sents], dtype=torch.int64, device=dev)
+        scores = torch.randn((B, Vs), generator=g, device=dev).to(torch.bfloat16)
+        want = host_p(ids, scores.clone())
+        got = dev_p(ids, scores.clone())
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (variant, step)
+        bufs = dev_p._dev._bufs
+        rows = np.frombuffer(bufs["rows"].cpu().numpy().tobytes(), dtype=P.ROW_DTYPE)
+        fl = np.nonzero(rows["flags"] & P.FLAG_BITS)[0]
+        if fl.size == 0:
+            continue
+        flagged_total += fl.size
+        pats = [sents[i] for i in fl]
+        toks = np.asarray([t for p in pats for t in p], dtype=np.int64)
+        offs = np.concatenate([[0], np.cumsum([len(p) for p in pats])]).astype(np.int64)
+        clo = np.zeros(fl.size, dtype=np.uint64)
+        chi = np.zeros(fl.size, dtype=np.uint64)
+        cm = np.zeros((fl.size, Vs), dtype=np.uint8)
+        ref.full_step(toks, offs, SHIFT, clo, chi, cm, 16)
+        mlo = bufs["mlo"].cpu().numpy().astype(np.uint64)[fl]
+        mhi = bufs["mhi"].cpu().numpy().astype(np.uint64)[fl]
+        assert np.array_equal(mlo, clo) and np.array_equal(mhi, chi), (variant, step)
+        bits = bufs["bits"][torch.tensor(fl, device=dev)].cpu().numpy()
+        unpacked = np.unpackbits(bits.view(np.uint8), axis=1, bitorder="little")[:, :Vs]
+        bad = np.nonzero((unpacked != cm).any(1))[0]
+        assert bad.size == 0, (variant, step, fl[bad[:8]].tolist())
+    assert flagged_total > B          # most rows took the allowed-bits path
+    assert dev_p._dev.prev_ids is not None
+
+
+@pytest.mark.timeout(900)
+def test_c2_bwt_equals_host_sais(dev, c2, monkeypatch):
+    """The whole BWT of the C2-scale corpus (n = 3e8) from the GPU suffix
+    sorter (prefix doubling, csrc/sa.hip -- the index of the c2 fixture) ==
+    the BWT from the host SA-IS sorter (csrc/sais.h, induced sorting: no code
+    shared with the GPU path), taken through the reference's own construction
+    entry point FMIndex.initialize (fm_index.cpp:33-41) with the GPU sort
+    switched off (FMIDX_GPU_SORT_MIN above n).  The host build's SA samples
+    come from the host suffix array, so locate of 2^20 random rows must agree
+    as well.  A heartbeat line every 30 s keeps the run visibly alive."""
+    import threading
+    import time
+
+    import torch
+
+    from fmidx.fm_index import FMIndex
+
+    text, bwt_gpu = c2["text"], c2["bwt"]
+    n = text.numel()
+    body = text[:-1].to(torch.int64).cpu().numpy().astype(np.uint64)
+    monkeypatch.setenv("FMIDX_GPU_SORT_MIN", str(1 << 40))
+    host = FMIndex(device=0)
+    err = []
+
+    def run():
+        try:
+            host.initialize(body)
+        except Exception as e:     # surfaced below
+            err.append(e)
+
+    th = threading.Thread(target=run)
+    t0 = time.time()
+    th.start()
+    while th.is_alive():
+        th.join(30)
+        if th.is_alive():
+            print(f"[host SA-IS build of n={n}: {time.time() - t0:.0f}s]", flush=True)
+    assert not err, err
+    print(f"host SA-IS build {time.time() - t0:.1f}s", flush=True)
+    del body
+    assert host.size() == n
+    assert torch.equal(host.device_bwt(), bwt_gpu)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    rows = torch.randint(0, n, (1 << 20,), generator=g, device=dev)
+    assert torch.equal(host.locate_batch(rows), c2["fm"].locate_batch(rows))

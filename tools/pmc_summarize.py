@@ -2,9 +2,20 @@
 per-launch HBM bytes of the fused decode kernel (the last K eager
 k_decode<false, true> dispatches = the timed steps replayed eagerly)."""
 import csv
+import hashlib
 import json
 import os
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fm-index-constrained-decoding_amd", "fmidx",
+                   "libfmidx.so")
+
+
+def lib_sha16(path=LIB):
+    """The first 16 hex digits of the SHA-256 of the library the counters were
+    collected with: bench.py uses the committed figure only for the same build."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def per_dispatch(path, counter, kernel="k_decode<false, true,"):
@@ -34,6 +45,7 @@ def main():
     lfb = (2 * 1024 * sum(lf_fetch) / len(lf_fetch) + 1024 * sum(lf_write) / len(lf_write)) if lf_fetch else None
     res = {
         "kernel": "k_decode<false, true> (fused LF step + uint8 mask)",
+        "lib_sha16": lib_sha16(),
         "corpus_tokens": bench["config"]["corpus_tokens"],
         "batch": bench["config"]["batch_per_gpu"],
         "dispatches": [len(fetch), len(write)],

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=9, help="trace steps (pairs = rows x (steps - 1))")
     ap.add_argument("--patterns", type=int, default=1 << 18)
     ap.add_argument("--out", default="")
+    ap.add_argument("--by-path", action="store_true", help="also one launch per LF path class (PMC breakdown)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     fm, text, bwt, _ = bench.build_index(int(args.tokens), args.vocab, 20250905, dev)
@@ -67,17 +68,23 @@ def main():
         return best
 
     # ---- gather ceilings
-    def gather(ptr, nbytes, cold):
+    def gather(ptr, nbytes, cold, mode=0):
         threads, loads = 256 * 4096, 64
-        ms = timed(lambda: check(lib().fm_probe_gather(ptr, nbytes, 0, loads, threads, sink.data_ptr(), stream),
+        _, lpl, line = bench.GATHER_MODES[mode]
+        ms = timed(lambda: check(lib().fm_probe_gather(ptr, nbytes, mode, loads, threads, sink.data_ptr(), stream),
                                  "probe"), cold)
-        return threads * loads * 64 / (ms * 1e-3) / 1e9
+        return threads // lpl * loads * line / (ms * 1e-3) / 1e9
 
     buf = torch.randint(0, 1 << 62, (1 << 30,), dtype=torch.int64, device=dev)
     res["gather_8GiB_GBps"] = gather(buf.data_ptr(), 8 << 30, True)
+    res["gather_8GiB_by_shape_GBps"] = {bench.GATHER_MODES[m][0]: gather(buf.data_ptr(), 8 << 30, True, m)
+                                        for m in bench.GATHER_MODES}
     del buf
     torch.cuda.empty_cache()
-    res["gather_bwt_GBps"] = gather(bwt.data_ptr(), bwt.numel() * 4, True)
+    res["gather_bwt_by_shape_GBps"] = {bench.GATHER_MODES[m][0]: gather(bwt.data_ptr(), bwt.numel() * 4, True, m)
+                                       for m in bench.GATHER_MODES}
+    res["gather_bwt_GBps"] = max(res["gather_bwt_by_shape_GBps"]["lane_64B"],
+                                 res["gather_bwt_by_shape_GBps"]["coop4_64B"])
     print(f"gather ceiling: 8 GiB {res['gather_8GiB_GBps']:.0f} GB/s, index BWT "
           f"({bwt.numel() * 4 / 2**30:.1f} GiB) {res['gather_bwt_GBps']:.0f} GB/s", flush=True)
 
@@ -116,6 +123,58 @@ def main():
               flush=True)
         del tokens, lo_h, hi_h, tok, plo, phi, olo, ohi
         torch.cuda.empty_cache()
+
+    # ---- the last (largest) launch split by LF path: one grouped launch per class
+    # (FMIDX_LF_GROUP_MIN=0 through fm_reload_tuning, so even a small class takes the
+    # grouped kernel), each cold, bytes by the LF plan.  With tools/pmc_rank.sh the
+    # LAST len(by_path) k_lf_group dispatches are these, in this order.
+    if args.by_path:
+        os.environ["FMIDX_LF_GROUP_MIN"] = "0"
+        lib().fm_reload_tuning()
+        R = 1 << max(int(x) for x in args.rows_log2.split(",") if x)
+        S = args.steps
+        tokens, _, lo_h, hi_h, _ = decode_trace(fm, text, bwt, max(1, R // (S - 1)), args.vocab, S, 777, dev)
+        tok = tokens[1:S].reshape(-1).contiguous()
+        plo = lo_h[0:S - 1].reshape(-1).contiguous()
+        phi = hi_h[0:S - 1].reshape(-1).contiguous()
+        pc = fm.cache_contains(plo, phi).cpu().numpy().astype(bool)
+        t_np, l_np, h_np = tok.cpu().numpy(), plo.cpu().numpy(), np.minimum(phi.cpu().numpy(), n)
+        w = h_np - l_np
+        live = (t_np >= 0) & (w > 0)
+        full = live & (l_np == 0) & (h_np == n)
+        cmin = st["cache_min"] or (1 << 62)
+        cls = {"full_range": full,
+               "group_e_scan_le16": live & ~full & (w <= 16),
+               "quad_e_scan_17_128": live & ~full & (w > 16) & (w <= 128),
+               "probe_cached_parent": live & ~full & (w >= cmin) & pc,
+               "wave_e_scan_129_512": live & ~full & (w > 128) & (w <= 512),
+               "descent_or_other": live & ~full & (w > 512) & ~((w >= cmin) & pc),
+               "dead_or_restart": ~live}
+        res["by_path"] = []
+        for name, sel in cls.items():
+            idx = torch.tensor(np.flatnonzero(sel), dtype=torch.int64, device=dev)
+            if idx.numel() == 0:
+                continue
+            t_, l_, h_ = tok[idx].contiguous(), plo[idx].contiguous(), phi[idx].contiguous()
+            ol, oh = torch.empty_like(l_), torch.empty_like(h_)
+            by = bench.lf_plan_bytes(l_.cpu().numpy(), h_.cpu().numpy(), t_.cpu().numpy(), n, pc[sel], st, "lf")
+            flush.add_(1)
+            torch.cuda.synchronize()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            fm.lf_step_batch(t_, l_, h_, SHIFT, lo_out=ol, hi_out=oh, reset_below=0)
+            b.record()
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) * 1e3
+            ok = bool(torch.equal(ol, lo_h[1:S].reshape(-1)[idx]) and torch.equal(oh, hi_h[1:S].reshape(-1)[idx]))
+            e = {"path": name, "rows": int(idx.numel()), "alg_bytes": int(by.sum()), "cold_us": us,
+                 "GBps": by.sum() / (us * 1e-6) / 1e9, "exact": ok}
+            res["by_path"].append(e)
+            print(f"by path {name:22s} {e['rows']:7d} rows {us:8.1f} us {e['GBps']:7.0f} GB/s "
+                  f"({by.sum() / max(1, e['rows']):.0f} B/row), exact {ok}", flush=True)
+        del os.environ["FMIDX_LF_GROUP_MIN"]
+        lib().fm_reload_tuning()
 
     # ---- get_range (k_search) over P true patterns of U{1..32} tokens
     P = args.patterns
