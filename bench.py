@@ -23,10 +23,12 @@ collective); value = N*B*K / max-over-ranks time.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
 import time
+import traceback
 
 import numpy as np
 import torch
@@ -39,7 +41,7 @@ for _p in (REPO, PKG):
 
 from fmidx._lib import check, lib  # noqa: E402
 from fmidx.fm_index import FMIndex  # noqa: E402
-from fmidx.synth import decode_trace, markov_corpus_gpu, trace_patterns  # noqa: E402
+from fmidx.synth import decode_trace, markov_corpus_gpu, paq_corpus_gpu, paq_trace, trace_patterns  # noqa: E402
 
 SHIFT = 10
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 measured stream)
@@ -60,9 +62,12 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------
-def build_index(n_tokens: int, vocab: int, seed: int, dev):
+def build_index(n_tokens: int, vocab: int, seed: int, dev, corpus: str = "markov"):
     t0 = time.time()
-    text, beg = markov_corpus_gpu(n_tokens, vocab, seed, dev)
+    if corpus == "paq":
+        text, beg = paq_corpus_gpu(n_tokens, vocab, seed, dev)
+    else:
+        text, beg = markov_corpus_gpu(n_tokens, vocab, seed, dev)
     torch.cuda.synchronize()
     t1 = time.time()
     log(f"corpus n={text.numel()} docs={beg.numel() - 1} in {t1 - t0:.1f}s; GPU construction ...")
@@ -74,7 +79,7 @@ def build_index(n_tokens: int, vocab: int, seed: int, dev):
     t2 = time.time()
     bwt = fm.device_bwt()                  # zero-copy view of the index's BWT
     log(f"corpus {t1 - t0:.1f}s  suffix array + index {t2 - t1:.1f}s  n={bwt.numel()}")
-    return fm, text, bwt, {"corpus_s": t1 - t0, "sa_and_index_s": t2 - t1}
+    return fm, text, bwt, {"corpus_s": t1 - t0, "sa_and_index_s": t2 - t1, "beginnings": beg}
 
 
 def plan_bytes(lo: np.ndarray, hi: np.ndarray, n: int, b0_log2: int, bm_levels: int, bm_bytes_each: int,
@@ -308,8 +313,7 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
     dts = []
     for _ in range(3):
         a = time.perf_counter()
-        for l_, h_ in zip(lo_all[last].tolist(), hi_all[last].tolist()):
-            ref.distinct_count(int(l_), int(h_))
+        ref.distinct_only(lo_all[last], hi_all[last], 1)
         dts.append(time.perf_counter() - a)
     per_step = {"distinct_count_only": float(np.median(dts)),
                 "incremental": B / legs["incremental_1"]["value"],
@@ -463,9 +467,10 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
     S = W + K
     tokens, pats0, ref = sh                   # shard_trace, taken while the replica was resident
     del bwt, fm
+    gc.collect()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    mem_log("replica freed", dev)
+    mem_log(f"replica freed (torch reserves {torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB)", dev)
     text, beg = markov_corpus_gpu(n_tokens, V, text_seed, dev)
     flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
 
@@ -526,7 +531,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         del g, cx, bufs, lo, hi, mask
         torch.cuda.empty_cache()
     except Exception as e:      # the C4 leg and the line still run
-        compact = {"error": repr(e)}
+        compact = {"error": repr(e), "where": traceback.format_exc()[-1200:]}
 
     def c4_part():
         lens = [len(p) for p in pats0]
@@ -602,7 +607,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
     try:
         return compact, c4_part()
     except Exception as e:      # the compact result still reaches the line
-        return compact, {"error": repr(e)}
+        return compact, {"error": repr(e), "where": traceback.format_exc()[-1200:]}
 
 
 # ---------------------------------------------------------------------------
@@ -614,6 +619,8 @@ def main():
     ap.add_argument("--tokens", type=float, default=float(os.environ.get("FMIDX_BENCH_TOKENS", 4.5e9)))
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--vocab", type=int, default=128256)
+    ap.add_argument("--corpus", choices=("markov", "paq"), default="markov",
+                    help="paq: PAQ-shaped docs (prefix + question + eos, C5) with the paq trace")
     ap.add_argument("--seed", type=int, default=20250905)
     ap.add_argument("--cpu-window", type=int, default=3,
                     help="CPU baseline: trace steps every leg times (after one untimed warm-up step)")
@@ -647,7 +654,9 @@ def main():
     n_tokens = int(args.tokens)
     B, V, K, W = args.batch, args.vocab, args.steps, max(1, args.warmup)
 
-    fm, text, bwt, build_t = build_index(n_tokens, V, args.seed, dev)
+    fm, text, bwt, build_t = build_index(n_tokens, V, args.seed, dev, args.corpus)
+    beg = build_t.pop("beginnings")
+    mem_log("index built", dev)
     n = bwt.numel()
     st = fm.stats()
     st["lf_e"] = os.environ.get("FMIDX_LF_E", "1") != "0" and n < (1 << 36)
@@ -655,12 +664,15 @@ def main():
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu and args.cpu_window > 0 and args.cpu_reps > 0
     # the CPU legs replay steps W .. W + cpu_window of the same trace
     S_trace = max(S, W + args.cpu_window + 1) if cpu_leg else S
-    tokens, init, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
+    if args.corpus == "paq":
+        tokens, init, lo_hist, hi_hist, pats0 = paq_trace(fm, text, bwt, beg, B, V, S_trace, args.seed + rank, dev)
+    else:
+        tokens, init, lo_hist, hi_hist, pats0 = decode_trace(fm, text, bwt, B, V, S_trace, args.seed + rank, dev)
     # rank throughput at scale: RS_ROWS x (RS_STEPS - 1) independent (state,
     # token) pairs of a wider trace, for one k_lf launch (the grouped kernel)
     rs_tok, rs_lo, rs_hi, rs_ref = rank_pairs(fm, text, bwt, V, args.seed + 17 + rank, dev)
     want_sharded = (world > 1 and not args.no_sharded) or args.sharded_at_1
-    want_c4 = world == 1 and not args.no_c4 and not args.sharded_at_1 and n > 2e9
+    want_c4 = world == 1 and not args.no_c4 and not args.sharded_at_1 and n > 2e9 and args.corpus == "markov"
     sh = shard_trace(fm, text, bwt, B, V, S, dev) if (want_sharded or want_c4) else None
     del text
     torch.cuda.empty_cache()
@@ -872,9 +884,14 @@ def main():
         "dtype": "uint64",
         "data": "synthetic",
         "config": {
-            "workload": f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
-                        f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else ('C5 PAQ' if n > 1e9 else 'C2 simplewiki')} "
-                        f"scale), B={B} rows, V={V}, incremental ranges; timed replay cold (caches evicted)",
+            "workload": (f"decode step (LF + allowed-token mask) over a synthetic PAQ-shaped corpus (~24-token docs, "
+                         f"shared 3-token prefix + question + eos) of n={n} tokens (C5), B={B} rows whose patterns "
+                         f"start from the prefix (force_decoding_from), V={V}, incremental ranges; timed replay "
+                         f"cold (caches evicted)" if args.corpus == "paq" else
+                         f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
+                         f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else ('C5 PAQ' if n > 1e9 else 'C2 simplewiki')} "
+                         f"scale), B={B} rows, V={V}, incremental ranges; timed replay cold (caches evicted)"),
+            "corpus": args.corpus,
             "corpus_tokens": n,
             "global_batch": world * B,
             "batch_per_gpu": B,
@@ -996,15 +1013,20 @@ def main():
     elif want_c4:
         holder = [bwt, fm]
         del bwt, fm
+        gc.collect()
         torch.cuda.empty_cache()
+        mem_log("before the after-replica legs (replica still held)", dev)
         try:
             main_trace = (tokens[W:S], state_lo, state_hi, lo_hist[S - 1], hi_hist[S - 1])
             result["compact_profile"], result["c4_one_gpu"] = after_replica_legs(
                 holder, args.seed, n_tokens, V, B, K, W, dev, main_trace, sh)
             c4 = result["c4_one_gpu"]
-            log(f"c4 on one GPU: slowest shard {c4['slowest_shard_cold_us']:.1f}us cold, OR {c4['or_pass_cold_us']:.1f}us, "
-                f"exact {c4['masks_equal_unsharded']}, predicted 8-GPU step {c4['predicted_step_us']['direct']:.0f}"
-                f"-{c4['predicted_step_us']['ring']:.0f}us")
+            if "error" in c4:
+                log(f"c4 on one GPU failed: {c4['error']}")
+            else:
+                log(f"c4 on one GPU: slowest shard {c4['slowest_shard_cold_us']:.1f}us cold, OR "
+                    f"{c4['or_pass_cold_us']:.1f}us, exact {c4['masks_equal_unsharded']}, predicted 8-GPU step "
+                    f"{c4['predicted_step_us']['direct']:.0f}-{c4['predicted_step_us']['ring']:.0f}us")
         except Exception as e:  # the replica line must still print
             result["c4_one_gpu"] = {"error": repr(e)}
     if rank == 0:

@@ -95,7 +95,7 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
                           uint64_t ld, const int64_t* fdf, uint64_t fdf_len, const float* pow_tab, uint64_t pow_len,
                           const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
                           fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
-                          hipStream_t s);
+                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s);
 }  // namespace fmidx
 
 using fmidx::set_error;
@@ -1140,7 +1140,7 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
   }
   return fmidx::launch_processor_step(h->idx.view, *cfg, d_ids, B, L, ld_ids, d_fdf, fdf_len, d_pow, pow_len,
                                       d_prev_ids, prev_ld, prev_B, d_prev_state, d_rows, d_mask_lo, d_mask_hi,
-                                      d_state, d_status, reinterpret_cast<hipStream_t>(stream));
+                                      d_state, d_status, nullptr, 0, true, reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 
@@ -1157,7 +1157,8 @@ int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor
   // 1. row bookkeeping + pattern ranges
   if (fmidx::launch_processor_step(h->idx.view, *cfg, a->ids, a->B, a->L, a->ld, a->fdf, a->fdf_len, a->pow_tab,
                                    a->pow_len, a->prev_ids, a->prev_ld, a->prev_B, a->prev_state, a->rows, a->mask_lo,
-                                   a->mask_hi, a->state, a->status, s))
+                                   a->mask_hi, a->state, a->status, a->ids_copy, a->copy_ld,
+                                   a->status_host || a->status_event, s))
     return -1;
   // the status right behind the bookkeeping: the host waits on status_event (not on the whole
   // call) to learn whether the device path holds, while the mask and the epilogue run
@@ -1171,9 +1172,6 @@ int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor
   if (a->B && fmidx::launch_epilogue(a->dtype, a->scores, a->out, a->B, a->V, a->ld_scores, a->ld_out, a->bits,
                                      a->bits_ld, a->unigram_bits, a->rows, a->eos, s))
     return -1;
-  // 4. this call's ids for the next call's incremental ranges
-  if (a->ids_copy && a->B && a->L)
-    FM_HIP(hipMemcpy2DAsync(a->ids_copy, a->copy_ld * 8, a->ids, a->ld * 8, a->L * 8, a->B, hipMemcpyDeviceToDevice, s));
   return 0;
   FM_API_END
 }

@@ -67,7 +67,8 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
                                              uint64_t prev_B, const int64_t* __restrict__ prev_state,
                                              fm_row_params* __restrict__ rows, uint64_t* __restrict__ mlo,
                                              uint64_t* __restrict__ mhi, int64_t* __restrict__ state,
-                                             uint32_t* __restrict__ status) {
+                                             uint32_t* __restrict__ status, int64_t* __restrict__ ids_copy,
+                                             uint64_t copy_ld) {
   extern __shared__ int64_t srow[];   // STAGED: [npad] the row, then [4] its previous state
   const uint64_t row = blockIdx.x;
   const uint32_t lane = threadIdx.x;
@@ -98,6 +99,9 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
     for (int k = 0; k < 4; ++k) ps[k] = prev_state[k * prev_B + row];
   }
   const int64_t* r = STAGED ? srow : g;
+  // this call's row, kept for the next call's incremental ranges (prev_ids then)
+  if (ids_copy)
+    for (int64_t i = lane; i < n; i += 64) ids_copy[row * copy_ld + i] = r[i];
   uint32_t bad = 0;
   // remove_end_marker (causal_qwen.py:44-56): the tokens after the marker
   const bool hard = (cfg.flags & FM_PREP_HARD) != 0;
@@ -316,7 +320,7 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
                           uint64_t ld, const int64_t* fdf, uint64_t fdf_len, const float* pow_tab, uint64_t pow_len,
                           const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
                           fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
-                          hipStream_t s) {
+                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s) {
   if (!(cfg.flags & FM_PREP_HARD) && (cfg.marker_len < 1 || cfg.marker_len > 8)) {
     set_error("processor step: marker length %d not in 1..8", cfg.marker_len);
     return -1;
@@ -325,16 +329,24 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
     set_error("processor step: bad arguments");
     return -1;
   }
-  FM_HIP(hipMemsetAsync(status, 0, 16, s));
-  FM_HIP(hipMemsetAsync(status + 1, 0xFF, 4, s));
+  if (ids_copy && copy_ld < L) {
+    set_error("processor step: ids copy row of %llu < %llu", (unsigned long long)copy_ld, (unsigned long long)L);
+    return -1;
+  }
+  if (init_status) {   // a caller that never reads the status (fm_processor_call without a host copy) skips this
+    FM_HIP(hipMemsetAsync(status, 0, 16, s));
+    FM_HIP(hipMemsetAsync(status + 1, 0xFF, 4, s));
+  }
   if (B == 0) return 0;
   if (L <= (uint64_t)kMaxStaged) {
     const size_t lds = ((L + kStageBatch - 1) / kStageBatch * kStageBatch + 4) * sizeof(int64_t);
     k_prep<true><<<(unsigned)B, 64, lds, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
-                                              prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status);
+                                              prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status, ids_copy,
+                                              copy_ld);
   } else {
     k_prep<false><<<(unsigned)B, 64, 0, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
-                                             prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status);
+                                             prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status, ids_copy,
+                                             copy_ld);
   }
   FM_HIP(hipGetLastError());
   return 0;

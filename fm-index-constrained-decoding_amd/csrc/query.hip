@@ -81,30 +81,52 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
 // has wave slots (256 CUs x 32 waves): a wave is latency-bound on its dependent
 // round trips, so at one row per wave the rows in flight per CU cap the rate
 // (Little's law: 32 rows x ~3 cold hops).  Here a group of G lanes owns a row,
-// 64 / G rows per wave: a full range takes its C lookup, a range of <= 8 G rows
-// its E scan inside the group (8 entries per lane, one round trip), and the
+// 64 / G rows per wave: a full range takes its C lookup, a range of <= 128
+// rows its E scan in a scan packed over the whole wave (group_step), and the
 // rest -- wider ranges (transition probe / wavelet descent / wave-wide E
 // scan) -- are taken one at a time by the whole wave through lf_step_decode.
 
+// Rows of at most this many entries take their LF step from E inside the
+// wave-packed scan of group_step (one load per entry actually needed).
+constexpr uint64_t kPackMax = 128;
+
 // One LF step for every group of the wave.  `live` = the group takes a step
-// (false: the row is left as it is).  Every lane executes the same loads (the
-// E scan is unconditional with a clamped index, as in lf_step_fast: a guarded
-// load is sunk into a branch with a vmcnt(0) behind it).
+// (false: the row is left as it is).  The loads are shaped for request
+// efficiency (the random-line rate of HBM counts requests -- one per (load
+// instruction, line) -- not bytes: csrc/probe.hip measures 3.1 TB/s of 64-B
+// lines when 4 lanes share a line against 1.3 TB/s when every lane reads its
+// own):
+//  * the C lookup is made only by full-range rows (the others all read C[0],
+//    one shared line);
+//  * rows of <= kPackMax entries are scanned from E by the whole wave at once:
+//    the rows' entry counts are prefix-summed across the wave, and each pass
+//    gives every lane the next entry of the packed list (its row found by a
+//    binary search over the rows' offsets), so a row costs a load per entry it
+//    has -- consecutive entries of a row land in one request -- instead of 8 G
+//    clamped loads (a 1-entry row used to issue 8 requests for its one line);
+//    matches go to per-row LDS slots (min / max LF: LF is increasing over a
+//    symbol's rows, so they are the LF of the first and last match).
+// Every lane executes the same loads (unconditional, clamped or dummy index:
+// a guarded load is sunk into a branch with a vmcnt(0) behind it).
 template <int G, bool GP, bool Q>
 __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h,
                                            uint64_t& lo, uint64_t& hi) {
+  constexpr int R = 64 / G;                 // rows per wave
+  __shared__ uint64_t s_lf[kLfThreads / 64][2][R];
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
   const uint32_t j = lane & (G - 1);
+  const uint32_t slot = lane / G;
   const uint64_t h0 = h;
   if (h > v.n) h = v.n;
   const bool dead = !live || l >= h || sym < 0 || (uint64_t)sym > v.max_sym;
   const bool full = !dead && l == 0 && h == v.n;
-  const bool narrow = !dead && !full && v.E && h - l <= 8u * G;
+  const bool narrow = !dead && !full && v.E && h - l <= kPackMax;
   bool wide = live && !dead && !full && !narrow;
   const uint64_t c = dead ? 0 : (uint64_t)sym;
-  // C lookup (full range), the group's E scan and (GP) its transition probe,
-  // issued together
-  const uint64_t ca = v.C[c], cb = v.C[c + 1];
+  // C lookup (full-range rows only) and (GP) the group's transition probe, issued together
+  const uint64_t cf = full ? c : 0;
+  const uint64_t ca = v.C[cf], cb = v.C[cf + 1];
   uint64_t pw[GP ? 3 * (16 / G) : 1];
   const bool probe = GP && wide && v.trans_cap && h - l >= v.cache_min;
   if (GP) {
@@ -115,45 +137,48 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     const uint64_t home = probe ? trans_home(l, h, c, v.trans_cap) : 0;
 #pragma unroll
     for (int k = 0; k < 16 / G; ++k) {
-      uint64_t slot = probe ? home + j * (16 / G) + k : 0;
-      if (slot >= v.trans_cap) slot -= v.trans_cap;
+      uint64_t slot_k = probe ? home + j * (16 / G) + k : 0;
+      if (slot_k >= v.trans_cap) slot_k -= v.trans_cap;
 #pragma unroll
-      for (int w = 0; w < 3; ++w) pw[3 * k + w] = tt[3 * slot + w];
+      for (int w = 0; w < 3; ++w) pw[3 * k + w] = tt[3 * slot_k + w];
     }
   }
-  uint64_t e[8];
+  // ---- the wave-packed E scan of the narrow rows
+  const uint32_t cnt = (narrow && j == 0) ? (uint32_t)(h - l) : 0u;
+  uint32_t inc = cnt;
 #pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint64_t idx = l + j + (uint64_t)G * k;
-    const uint64_t x = v.E ? v.E[narrow ? (idx < h ? idx : h - 1) : 0] : 0;
-    e[k] = (narrow && idx < h) ? x : ~0ull;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
   }
-  uint64_t fmin = ~0ull, fmax = 0, lfmin = 0, lfmax = 0;
+  const uint32_t excl = inc - cnt;
+  const uint32_t total = __shfl(inc, 63, 64);
+  if (j == 0) {
+    s_lf[wv][0][slot] = ~0ull;
+    s_lf[wv][1][slot] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t t0 = 0; t0 < total; t0 += 64) {          // wave-uniform
+    const uint32_t e = t0 + lane;
+    const bool valid = e < total;
+    uint32_t r = 0;                                      // the last row whose offset is <= e
 #pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    if (e[k] != ~0ull && (e[k] >> kESymShift) == c) {
-      const uint64_t r = j + (uint64_t)G * k + 1;
-      if (r < fmin) {
-        fmin = r;
-        lfmin = e[k] & kELfMask;
-      }
-      fmax = r;      // k ascends: the last match of the lane
-      lfmax = e[k] & kELfMask;
+    for (int step = R / 2; step > 0; step >>= 1) {
+      const uint32_t x = __shfl(excl, (int)((r + step) * G), 64);
+      if (x <= e) r += step;
+    }
+    const uint64_t base = __shfl(l, (int)(r * G), 64);
+    const uint64_t rc = __shfl(c, (int)(r * G), 64);
+    const uint32_t off = e - __shfl(excl, (int)(r * G), 64);
+    const uint64_t x = v.E[valid ? base + off : 0];
+    if (valid && (x >> kESymShift) == rc) {
+      atomicMin(&s_lf[wv][0][r], (unsigned long long)(x & kELfMask));
+      atomicMax(&s_lf[wv][1][r], (unsigned long long)(x & kELfMask));
     }
   }
-#pragma unroll
-  for (int d = 1; d < G; d <<= 1) {
-    const uint64_t om = __shfl_xor(fmin, d, 64), ol = __shfl_xor(lfmin, d, 64);
-    const uint64_t xm = __shfl_xor(fmax, d, 64), xl = __shfl_xor(lfmax, d, 64);
-    if (om < fmin) {
-      fmin = om;
-      lfmin = ol;
-    }
-    if (xm > fmax) {
-      fmax = xm;
-      lfmax = xl;
-    }
-  }
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t fmin = s_lf[wv][0][slot], fmax = s_lf[wv][1][slot];
+  const bool found = fmin != ~0ull;
   if (!live) {
     lo = l;
     hi = h0;
@@ -164,8 +189,8 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     lo = ca < cb ? ca : 0;
     hi = ca < cb ? cb : 0;
   } else if (narrow) {
-    lo = fmax ? lfmin : 0;
-    hi = fmax ? lfmax + 1 : 0;
+    lo = found ? fmin : 0;
+    hi = found ? fmax + 1 : 0;
   }
   if (GP) {   // a probe hit (at most one slot of the group holds the key) ends a wide row's step
     const uint64_t key0 = l | (c << kTransSymShift);

@@ -17,6 +17,24 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// The OR of one word over every part.  The parts' loads are independent, so
+// they are issued 8 at a time before any is used (a plain loop over a runtime
+// part count put a wait behind every load: one HBM round trip per shard).
+// Past the last part the index is clamped (the last part again: harmless for
+// an OR), so no load sits under a branch.
+__device__ __forceinline__ uint32_t or_parts(const uint32_t* __restrict__ parts, uint32_t nparts,
+                                             uint64_t part_stride, uint64_t off) {
+  uint32_t x = 0;
+  for (uint32_t p0 = 0; p0 < nparts; p0 += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) v[q] = parts[(uint64_t)min(p0 + q, nparts - 1) * part_stride + off];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) x |= v[q];
+  }
+  return x;
+}
+
 // one thread per 16 tokens: half a word of every part, one 16-B store
 __global__ void __launch_bounds__(kThreads) k_or_unpack(const uint32_t* __restrict__ parts, uint32_t nparts,
                                                         uint64_t part_stride, uint64_t B, uint64_t wpr,
@@ -26,8 +44,7 @@ __global__ void __launch_bounds__(kThreads) k_or_unpack(const uint32_t* __restri
   const uint64_t b = g / chunks, k = g - b * chunks;
   if (b >= B) return;
   const uint64_t w = k >> 1;
-  uint32_t x = 0;
-  for (uint32_t p = 0; p < nparts; ++p) x |= parts[p * part_stride + b * wpr + w];
+  const uint32_t x = or_parts(parts, nparts, part_stride, b * wpr + w);
   const uint32_t bits = (k & 1) ? (x >> 16) : (x & 0xFFFFu);
   uint8_t* o = out + b * ld + k * 16;
   const uint64_t t0 = k * 16;
@@ -47,9 +64,7 @@ __global__ void __launch_bounds__(kThreads) k_or_words(const uint32_t* __restric
   const uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   const uint64_t b = g / wpr, w = g - b * wpr;
   if (b >= B) return;
-  uint32_t x = 0;
-  for (uint32_t p = 0; p < nparts; ++p) x |= parts[p * part_stride + b * wpr + w];
-  out[b * ldw + w] = x;
+  out[b * ldw + w] = or_parts(parts, nparts, part_stride, b * wpr + w);
 }
 
 }  // namespace

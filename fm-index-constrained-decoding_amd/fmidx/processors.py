@@ -134,6 +134,7 @@ class _DeviceStep:
         self._ev = torch.cuda.Event()
         self._ev_ready = False
         self._wait_stream = os.environ.get("FMIDX_PROC_WAIT", "event") == "stream"
+        self._verify = os.environ.get("FMIDX_PROC_VERIFY", "0") != "0"    # hard calls: read the status anyway
 
     @property
     def prev_ids(self):
@@ -162,7 +163,11 @@ class _DeviceStep:
             self._prev_ok = False
         return self._bufs
 
-    def __call__(self, input_ids, scores, cfg: _PrepConfig):
+    def __call__(self, input_ids, scores, cfg: _PrepConfig, wait: bool = True):
+        """wait=False (the hard-mask variants): the call's status is fixed by
+        its inputs -- no end marker to find, every boost 0 -- so the device
+        path always holds and the host neither copies nor waits for it: the call
+        only enqueues work (vLLM V0 calls one clone per sequence per step)."""
         dev = self.dev
         ids = input_ids if (input_ids.device == dev and input_ids.dtype == torch.int64
                             and input_ids.is_contiguous()) else input_ids.to(dev, torch.int64).contiguous()
@@ -203,14 +208,21 @@ class _DeviceStep:
         a.unigram_bits = self.core.unigram_bits(V, dev).data_ptr()
         a.eos = int(cfg.eos)
         a.ids_copy, a.copy_ld = keep.data_ptr(), keep.stride(0)
-        a.status_host = self.status_h.data_ptr()
         stream = torch.cuda.current_stream(dev)
-        if not self._ev_ready:          # torch creates the event at its first record
-            self._ev.record(stream)
-            self._ev_ready = True
-        a.status_event = self._ev.cuda_event
+        wait = wait or self._verify or B == 0
+        if wait:
+            a.status_host = self.status_h.data_ptr()
+            if not self._ev_ready:          # torch creates the event at its first record
+                self._ev.record(stream)
+                self._ev_ready = True
+            a.status_event = self._ev.cuda_event
+        else:
+            a.status_host = a.status_event = None
         check(lib().fm_processor_call(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
                                       c_void_p(stream.cuda_stream)), "processor_call")
+        if not wait:
+            self._cur, self._prev_ok = oth, True
+            return out if out.device == scores.device else out.to(scores.device)
         if self._wait_stream:
             stream.synchronize()
         else:
@@ -547,7 +559,7 @@ class CausalIndexBasedLogitsProcessor:
 
     def _process(self, input_ids, scores):
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype), wait=False)
             if out is not None:
                 return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
@@ -688,6 +700,7 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
         self._ids_dev = None        # the sequence's ids on the device (see _device_ids)
         self._ids_pin = None
         self._ids_prev = ()
+        self._ids_ev = None         # recorded behind the last staged copy
 
     def clone(self):
         return VllmIndexBasedLogitsProcessor(num_beams=self._num_beams, index=self.index,
@@ -712,18 +725,24 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
             self._ids_pin = torch.empty(cap, dtype=torch.int64).pin_memory()
             self._ids_pin_np = self._ids_pin.numpy()
             self._ids_prev = ()
+            self._ids_ev = None
         prev = self._ids_prev
         k = len(prev) if len(prev) <= L and toks[:len(prev)] == prev else 0
         if L > k:
+            if k < len(prev) and self._ids_ev is not None:
+                self._ids_ev.synchronize()      # staged slots about to be rewritten: their last copy must be done
             self._ids_pin_np[k:L] = toks[k:L]
             buf[0, k:L].copy_(self._ids_pin[k:L], non_blocking=True)
+            if self._ids_ev is None:
+                self._ids_ev = torch.cuda.Event()
+            self._ids_ev.record(torch.cuda.current_stream(buf.device))
         self._ids_prev = toks
         return buf[:, :L]
 
     def __call__(self, input_ids, scores):
         scores = scores.unsqueeze(0)
         if self._dev is not None:
-            out = self._dev(self._device_ids(tuple(input_ids)), scores, self._prep_config(scores.dtype))
+            out = self._dev(self._device_ids(tuple(input_ids)), scores, self._prep_config(scores.dtype), wait=False)
             if out is not None:
                 return out
         input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
@@ -780,7 +799,7 @@ class SeqIndexBasedLogitsProcessor(_HardMaskBase):
 
     def _process(self, input_ids, scores):
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype), wait=False)
             if out is not None:
                 return out
         B, V = scores.shape

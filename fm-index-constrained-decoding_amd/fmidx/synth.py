@@ -14,6 +14,7 @@ from __future__ import annotations
 import math
 from typing import Tuple
 
+import numpy as np
 import torch
 
 SHIFT = 10
@@ -82,6 +83,50 @@ def markov_corpus_gpu(n_tokens: int, vocab: int, seed: int, device, mean_len: fl
         text[pos] = (tok + SHIFT).to(torch.int32)
         t += 1
     return text, beginnings
+
+
+# "Paraphrase:" as three fixed token ids, and the eos id (Llama-3 <|end_of_text|>):
+# the PAQ index's docs are tokenizer("Paraphrase: " + question) + [eos]
+# (/root/reference/build_fm_index.py:46-48); the real tokenizer is not available
+# offline, so the prefix is a stand-in of the same shape.
+PAQ_PREFIX = (62, 1768, 25)
+PAQ_EOS = 128001
+
+
+def paq_corpus_gpu(n_tokens: int, vocab: int, seed: int, device, prefix=PAQ_PREFIX, eos: int = PAQ_EOS,
+                   mean_question: float = 20.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """A PAQ-shaped corpus: ~24-token docs, every one
+    ``prefix + question + [eos]``, the questions from the same Markov / Zipf
+    chain as markov_corpus_gpu (lognormal lengths around ``mean_question``,
+    sigma 0.3).  Encoded exactly as index.py:47-53 (each doc reversed, ids +
+    SHIFT, concatenated) plus the sentinel.  Every doc shares the prefix, so
+    the prefix pattern's range holds one row per doc (tens of millions at
+    n = 1.5e9) and in F every eos is followed by the prefix of the next doc.
+    Returns (T' int32 [n_tokens + 1], beginnings int64 [docs + 1])."""
+    extra = len(prefix) + 1
+    q_total = int(n_tokens * mean_question / (mean_question + extra))
+    qtext, qbeg = markov_corpus_gpu(q_total, vocab, seed, device, mean_len=mean_question, sigma=0.3,
+                                    max_len_factor=3.0)
+    qtext[qtext == eos + SHIFT] = eos - 1 + SHIFT      # eos is a special token: never inside a question
+    nd = qbeg.numel() - 1
+    qlen = qbeg[1:] - qbeg[:-1]
+    beg = torch.zeros(nd + 1, dtype=torch.int64, device=device)
+    torch.cumsum(qlen + extra, 0, out=beg[1:])
+    n = int(beg[-1].item())
+    text = torch.empty(n + 1, dtype=torch.int32, device=device)
+    text[-1] = 0
+    # per doc (reversed): [eos] + reversed question (= qtext's own doc slice) + reversed prefix
+    text[beg[:-1]] = eos + SHIFT
+    for j, t in enumerate(reversed(prefix)):
+        text[beg[1:] - len(prefix) + j] = t + SHIFT
+    chunk = 1 << 27
+    for a in range(0, q_total, chunk):
+        b = min(q_total, a + chunk)
+        pos = torch.arange(a, b, dtype=torch.int64, device=device)
+        doc = torch.searchsorted(qbeg, pos, right=True) - 1
+        text[pos + 1 + extra * doc] = qtext[a:b]
+        del pos, doc
+    return text, beg
 
 
 def suffix_array_gpu(text: torch.Tensor, sym_bits: int = 17) -> torch.Tensor:
@@ -165,6 +210,15 @@ def decode_trace(fm, text: torch.Tensor, bwt: torch.Tensor, B: int, V: int, S: i
     pats = [tok_h[off_h[b]:off_h[b + 1]] for b in range(B)]
     pats[0] = []
     pats[1].append(V + 1000)     # the eos row: an unknown id ends its pattern, as its (0, 0) state says
+    return _trace_steps(fm, bwt, lo, hi, init, pats, B, V, S, g, device)
+
+
+def _trace_steps(fm, bwt, lo, hi, init, pats, B, V, S, g, device):
+    """The steps of a decode trace from the rows' current ranges: a live row
+    appends the BWT symbol of a uniformly chosen row of its range (a random
+    occurrence's next token) with p = 0.9, else a uniform random id; an empty
+    row restarts (token -1); row 0 always restarts, row 1 gets an unknown id."""
+    n = bwt.numel()
     tokens = torch.empty((S, B), dtype=torch.int64, device=device)
     lo_hist = torch.empty((S, B), dtype=torch.int64, device=device)
     hi_hist = torch.empty((S, B), dtype=torch.int64, device=device)
@@ -187,6 +241,54 @@ def decode_trace(fm, text: torch.Tensor, bwt: torch.Tensor, B: int, V: int, S: i
         hi_hist[s] = hi
     torch.cuda.synchronize(device)
     return tokens, init, lo_hist, hi_hist, pats
+
+
+def paq_trace(fm, text: torch.Tensor, bwt: torch.Tensor, beg: torch.Tensor, B: int, V: int, S: int, seed: int,
+              device, prefix=PAQ_PREFIX):
+    """The C5 decode trace on a paq_corpus_gpu index (nq_open eval shape: the
+    processors search force_decoding_from + sentence, force_decoding_from being
+    the docs' shared prefix): a quarter of the rows start from the prefix alone
+    (one row per doc in its range), half from the prefix + the first 1..8
+    question tokens of a random doc, a quarter from random true n-grams of F
+    (U{1..32}, as decode_trace); then _trace_steps.  Rows 0 / 1 as decode_trace.
+    Returns decode_trace's tuple."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 1)
+    n = bwt.numel()
+    nd = beg.numel() - 1
+    P = len(prefix)
+    pats = []
+    kinds = torch.randint(0, 4, (B,), generator=g, device=device).tolist()
+    docs = torch.randint(0, nd, (B,), generator=g, device=device)
+    ks = torch.randint(1, 9, (B,), generator=g, device=device).tolist()
+    ends = beg[docs + 1]        # doc d occupies T'[beg[d], beg[d+1]): the prefix is its LAST P tokens (reversed)
+    q = torch.randint(0, n - 40, (B,), generator=g, device=device)
+    lens = torch.randint(1, 33, (B,), generator=g, device=device).tolist()
+    q_h = q.tolist()
+    e_h = ends.tolist()
+    dlen = (beg[docs + 1] - beg[docs]).tolist()
+    for b in range(B):
+        if kinds[b] == 0:
+            pats.append(list(prefix))
+        elif kinds[b] in (1, 2):
+            # forward doc = prefix, q1, q2, ...: T'[end - 1 - j] is forward token j
+            k = min(ks[b], dlen[b] - P - 1)       # within the question (the doc ends with eos)
+            fwd = text[torch.arange(e_h[b] - 1, e_h[b] - 1 - (P + k), -1, device=device)].to(torch.int64) - SHIFT
+            pats.append(fwd.tolist())
+        else:
+            idx = (n - 2) - (q_h[b] + torch.arange(lens[b], device=device))
+            pats.append((text[idx].to(torch.int64) - SHIFT).tolist())
+    pats[0] = []
+    flat = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=device)
+    offs = torch.tensor([0] + list(np.cumsum([len(p) for p in pats])), dtype=torch.int64, device=device)
+    lo = torch.zeros(B, dtype=torch.int64, device=device)
+    hi = torch.zeros(B, dtype=torch.int64, device=device)
+    fm.backward_search_batch(flat, offs, SHIFT, lo, hi)
+    lo[0], hi[0] = 0, n
+    lo[1], hi[1] = 0, 0
+    pats[1].append(V + 1000)
+    init = (lo.clone(), hi.clone())
+    return _trace_steps(fm, bwt, lo, hi, init, pats, B, V, S, g, device)
 
 
 def trace_patterns(patterns0, tokens, upto: int):

@@ -316,15 +316,18 @@ int fm_processor_step(fm_index* h, const fm_prep_config* cfg, const int64_t* d_i
                       fm_row_params* d_rows, uint64_t* d_mask_lo, uint64_t* d_mask_hi, int64_t* d_state,
                       uint32_t* d_status, void* stream);
 
-/* One whole soft-processor call (the three launches of the device path plus
- * the hand-offs), so the host makes one call per decode step:
- *   fm_processor_step -> fm_allowed_mask_batch(packed) of (mask_lo, mask_hi)
- *   into bits -> fm_apply_boosts(scores -> out) -> ids copied to ids_copy (the
- *   next call's prev_ids, optional).  The status is copied to status_host
- *   (pinned, optional) right after fm_processor_step, and status_event (a
- *   hipEvent_t, optional) is recorded behind that copy: the caller waits on the
- *   event -- the row bookkeeping only -- before reading status_host, while the
- *   mask and the epilogue still run.  Stream-ordered.  Replaces the per-call work of
+/* One whole processor call (the three launches of the device path plus the
+ * hand-offs), so the host makes one call per decode step:
+ *   fm_processor_step (which also copies this call's ids to ids_copy, the next
+ *   call's prev_ids, optional) -> fm_allowed_mask_batch(packed) of
+ *   (mask_lo, mask_hi) into bits -> fm_apply_boosts(scores -> out).  The status
+ *   is copied to status_host (pinned, optional) right after fm_processor_step,
+ *   and status_event (a hipEvent_t, optional) is recorded behind that copy: the
+ *   caller waits on the event -- the row bookkeeping only -- before reading
+ *   status_host, while the mask and the epilogue still run.  With neither, the
+ *   status is not even initialised (a hard-mask call's status is fixed by its
+ *   inputs: no end marker, zero boosts), so the call needs no host wait at
+ *   all.  Stream-ordered.  Replaces the per-call work of
  *   document_constrained_generation_causal_qwen.py:101-214 / causal.py:62-180. */
 typedef struct fm_processor_args {
   const int64_t* ids;          /* [B][ld] input_ids */

@@ -329,6 +329,13 @@ void cr_decode_step(void* p, const int64_t* tok, int64_t shift, int64_t reset_be
   });
 }
 
+// distinct_count (fm_index.cpp:119-144, sigma-sized zeroed scratch included) of
+// m ranges, results discarded: the bench's single-thread step breakdown.
+void cr_distinct_only(void* p, const uint64_t* lo, const uint64_t* hi, uint64_t m, int threads) {
+  const CpuRef& h = *static_cast<CpuRef*>(p);
+  parallel_rows(m, threads, [&](uint64_t i, std::vector<uint64_t>& buf) { h.distinct_count(lo[i], hi[i], buf); });
+}
+
 // index.py:103-114: get_range of tokens[a, b) from scratch, one
 // backward_search_step per token, early exit at (0, 0).
 inline void get_range(const CpuRef& h, const int64_t* tokens, int64_t a, int64_t b, int64_t shift, uint64_t& l,

@@ -29,6 +29,7 @@ def lib():
         d.cr_distinct_count.argtypes = [c_void_p, c_uint64, c_uint64, u64p, c_uint64]
         d.cr_decode_step.argtypes = [c_void_p, POINTER(c_int64), c_int64, c_int64, u64p, u64p, c_uint64,
                                      POINTER(ctypes.c_uint8), c_uint64, c_int]
+        d.cr_distinct_only.argtypes = [c_void_p, u64p, u64p, c_uint64, c_int]
         d.cr_full_step.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), c_int64, c_uint64, u64p, u64p,
                                    POINTER(ctypes.c_uint8), c_uint64, c_int, c_int]
         _lib = d
@@ -88,7 +89,10 @@ class CpuRef:
         n = bwt.numel()
         L = max(1, int(bwt.max().item()).bit_length())
         words = wt_int_levels_device(bwt, L).cpu().numpy().view(np.uint64)
-        cnt = torch.bincount(bwt.to(torch.int64), minlength=(1 << L) + 1)
+        # symbol counts in chunks (an int64 copy of a 4.5e9-row BWT would take 36 GB of HBM)
+        cnt = torch.zeros((1 << L) + 1, dtype=torch.int64, device=bwt.device)
+        for a in range(0, n, 1 << 28):
+            cnt += torch.bincount(bwt[a:a + (1 << 28)].to(torch.int64), minlength=(1 << L) + 1)
         C = torch.zeros((1 << L) + 1, dtype=torch.int64, device=bwt.device)
         torch.cumsum(cnt[: 1 << L], 0, out=C[1:])
         sigma = int((cnt > 0).sum().item())
@@ -114,6 +118,12 @@ class CpuRef:
                     mask: np.ndarray, threads: int):
         lib().cr_decode_step(self._h, _p(tok, c_int64), shift, reset_below, _p(lo), _p(hi), lo.size,
                              _p(mask, ctypes.c_uint8), mask.shape[1], threads)
+
+    def distinct_only(self, lo: np.ndarray, hi: np.ndarray, threads: int = 1):
+        """distinct_count of every (lo[i], hi[i]) with the results discarded."""
+        lo = np.ascontiguousarray(lo, dtype=np.uint64)
+        hi = np.ascontiguousarray(hi, dtype=np.uint64)
+        lib().cr_distinct_only(self._h, _p(lo), _p(hi), lo.size, threads)
 
     def full_step(self, tokens: np.ndarray, offsets: np.ndarray, shift: int, lo, hi, mask, threads: int,
                   faithful: bool = False):
