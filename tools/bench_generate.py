@@ -77,7 +77,7 @@ def corpus_prompts(text, rows, plen, rng):
     return (text[idx].to(torch.int64) - SHIFT).cpu()
 
 
-def hf_leg(kind, fm, text, B, beams, new, dev, rng):
+def hf_leg(kind, fm, text, B, beams, new, dev, rng, reps=3):
     from transformers import LlamaConfig, LlamaForCausalLM, LogitsProcessorList, Qwen3Config, Qwen3ForCausalLM
 
     import fmidx.processors as P
@@ -123,27 +123,41 @@ def hf_leg(kind, fm, text, B, beams, new, dev, rng):
 
     gen(LogitsProcessorList([]), 4)                                    # warm-up (kernels, allocator)
     res = {"model": f"{kind} random weights ({sum(p.numel() for p in model.parameters()) / 1e9:.2f} B params, bf16)",
-           "vocab": V, "rows": B, "prompts": prompts, "beams": beams, "new_tokens": new}
-    t, _ = gen(LogitsProcessorList([]), new)
-    res["no_processor_ms_per_step"] = t / new * 1e3
+           "vocab": V, "rows": B, "prompts": prompts, "beams": beams, "new_tokens": new, "reps": reps}
+    procs = {}
     for mode in ("event", "stream", "host"):
         proc = mk()
         if mode == "host":
             proc._dev = None
         elif mode == "stream":
             proc._dev._wait_stream = True
-        w = Timed(proc)
-        n_new = new if mode != "host" else min(new, 8)
-        gen(LogitsProcessorList([w]), 2)                               # first call: fresh searches, buffers
-        w.times.clear()
-        t, out = gen(LogitsProcessorList([w]), n_new)
-        if mode != "host":
-            assert proc._dev.prev_ids is not None, "device path fell back"
-        res[f"{mode}_ms_per_step"] = t / n_new * 1e3
-        res[f"{mode}_processor_ms_per_call"] = float(np.median(w.times)) * 1e3
-        res[f"{mode}_processor_share"] = float(np.sum(w.times)) / t
-        log(f"{kind} {mode}: {t / n_new * 1e3:.2f} ms/step, processor {np.median(w.times) * 1e3:.3f} ms/call")
+        procs[mode] = Timed(proc)
+        gen(LogitsProcessorList([procs[mode]]), 2)                     # first calls: fresh searches, buffers
+    # the modes interleaved, `reps` rounds (clock and allocator drift land on every mode alike)
+    times = {m: [] for m in ("none", "event", "stream", "host")}
+    calls = {m: [] for m in ("event", "stream", "host")}
+    for _ in range(reps):
+        for mode in ("none", "event", "stream", "host"):
+            n_new = new
+            if mode == "none":
+                t, _ = gen(LogitsProcessorList([]), n_new)
+            else:
+                w = procs[mode]
+                w.times.clear()
+                t, _ = gen(LogitsProcessorList([w]), n_new)
+                calls[mode].append(float(np.median(w.times)))
+                if mode != "host":
+                    assert w.proc._dev.prev_ids is not None, "device path fell back"
+            times[mode].append(t / n_new)
+    res["no_processor_ms_per_step"] = float(np.median(times["none"])) * 1e3
+    for mode in ("event", "stream", "host"):
+        res[f"{mode}_ms_per_step"] = float(np.median(times[mode])) * 1e3
+        res[f"{mode}_ms_per_step_all"] = [x * 1e3 for x in times[mode]]
+        res[f"{mode}_processor_ms_per_call"] = float(np.median(calls[mode])) * 1e3
+        log(f"{kind} {mode}: {res[f'{mode}_ms_per_step']:.2f} ms/step (no processor "
+            f"{res['no_processor_ms_per_step']:.2f}), processor {res[f'{mode}_processor_ms_per_call']:.3f} ms/call")
     res["event_overhead_ms_per_step"] = res["event_ms_per_step"] - res["no_processor_ms_per_step"]
+    res["host_overhead_ms_per_step"] = res["host_ms_per_step"] - res["no_processor_ms_per_step"]
     del model
     torch.cuda.empty_cache()
     return res
@@ -156,15 +170,17 @@ def vllm_leg(fm, text, seqs, steps, dev, rng):
     base = P.VllmIndexBasedLogitsProcessor(index=fm, num_beams=1, pad_token_id=151643, eos_token_id=151645,
                                            always_allow_eos=True)
     res = {"sequences": seqs, "steps": steps, "vocab": V}
+    per = {}
     for mode in ("suffix", "tensor"):
         clones = [base.clone() for _ in range(seqs)]
         if mode == "tensor":      # round 2: the whole tuple through torch.tensor + a pageable copy every call
             for c in clones:
                 c._device_ids = lambda toks, c=c: torch.tensor([list(toks)], dtype=torch.long)
-        outs = [[] for _ in range(seqs)]
-        logits = torch.randn((seqs, V), device=dev).to(torch.bfloat16)
-        per_step = []
-        for s in range(steps):
+        per[mode] = (clones, [[] for _ in range(seqs)], [])
+    logits = torch.randn((seqs, V), device=dev).to(torch.bfloat16)
+    for s in range(steps):
+        for mode in ("suffix", "tensor"):            # interleaved step by step
+            clones, outs, per_step = per[mode]
             torch.cuda.synchronize()
             a = time.perf_counter()
             rows = [clones[i](tuple(outs[i]), logits[i]) for i in range(seqs)]
@@ -172,7 +188,8 @@ def vllm_leg(fm, text, seqs, steps, dev, rng):
             per_step.append(time.perf_counter() - a)
             for i, t in enumerate(nxt):
                 outs[i].append(int(t))
-        res[f"{mode}_ms_per_step"] = float(np.median(per_step[2:])) * 1e3
+    for mode in ("suffix", "tensor"):
+        res[f"{mode}_ms_per_step"] = float(np.median(per[mode][2][2:])) * 1e3
         res[f"{mode}_ms_per_call"] = res[f"{mode}_ms_per_step"] / seqs
         log(f"vllm {mode}: {res[f'{mode}_ms_per_step']:.2f} ms per step of {seqs} calls")
     return res
@@ -184,6 +201,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--beams", type=int, default=2)
     ap.add_argument("--new", type=int, default=24)
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--models", default="llama,qwen")
     ap.add_argument("--vllm-seqs", type=int, default=256)
     ap.add_argument("--vllm-steps", type=int, default=12)
@@ -195,7 +213,7 @@ def main():
     rng = np.random.default_rng(5)
     result = {"n": fm.size(), "hf": {}}
     for kind in args.models.split(","):
-        result["hf"][kind] = hf_leg(kind, fm, text, args.batch, args.beams, args.new, dev, rng)
+        result["hf"][kind] = hf_leg(kind, fm, text, args.batch, args.beams, args.new, dev, rng, args.reps)
     result["vllm"] = vllm_leg(fm, text, args.vllm_seqs, args.vllm_steps, dev, rng)
     print(json.dumps(result), flush=True)
 

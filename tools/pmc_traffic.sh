@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_decode|k_lf" --output-format csv \
-      -d "$OUT/raw_$C" -o run -- python3 bench.py --no-cpu --eager-replay "$@" \
+      -d "$OUT/raw_$C" -o run -- python3 bench.py --no-cpu --no-c4 --eager-replay "$@" \
       > "$OUT/bench_$C.json" 2> "$OUT/bench_$C.log"
   find "$OUT/raw_$C" -name "*counter_collection.csv" -exec cp {} "$OUT/counters_$C.csv" \;
   rm -rf "$OUT/raw_$C"

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 # the raw trace can exceed gpurun's merge cap: never leave it behind
 trap 'rm -rf "$OUT/raw"' EXIT
 export TMPDIR=/tmp
-rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o run -- python3 bench.py --no-cpu "$@" > "$OUT/bench.json" 2> "$OUT/bench.log"
+rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/raw" -o run -- python3 bench.py --no-cpu --no-c4 "$@" > "$OUT/bench.json" 2> "$OUT/bench.log"
 find "$OUT/raw" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 TRACE=$(find "$OUT/raw" -name "*kernel_trace.csv" | head -1)
 python3 - "$TRACE" "$OUT/decode_dispatches.json" "$@" <<'PY'
@@ -34,4 +34,8 @@ res = {"kernel": "k_decode<false, true, *>", "dispatches": len(dur), "avg_us_all
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))
 PY
+# the sharded rehearsal's kernels (bench's C4 leg at N = 1): per-shard packed decode, the OR pass
+python3 tools/trace_durations.py "$TRACE" "k_decode<true, true," --out "$OUT/c4_shard_decode_dispatches.json" > /dev/null || true
+python3 tools/trace_durations.py "$TRACE" "k_or_unpack" --out "$OUT/c4_or_dispatches.json" || true
+python3 tools/trace_durations.py "$TRACE" "k_lf_group" --out "$OUT/lf_group_dispatches.json" > /dev/null || true
 rm -rf "$OUT/raw"
