@@ -108,7 +108,23 @@ constexpr uint64_t kPackMax = 128;
 //    symbol's rows, so they are the LF of the first and last match).
 // Every lane executes the same loads (unconditional, clamped or dummy index:
 // a guarded load is sunk into a branch with a vmcnt(0) behind it).
-template <int G, bool GP, bool Q>
+constexpr uint64_t kLfWideTag = 1ull << 63;
+
+// Whether a row's LF step is "wide" in group_step's sense: live, not dead, not
+// the full range, and not a <= kPackMax-row E scan.  The split launch
+// (k_lf_group in D mode, then k_lf_wide) must agree on it exactly.
+__device__ __forceinline__ bool lf_wide(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h) {
+  if (h > v.n) h = v.n;
+  const bool dead = !live || l >= h || sym < 0 || (uint64_t)sym > v.max_sym;
+  const bool full = !dead && l == 0 && h == v.n;
+  const bool narrow = !dead && !full && v.E && h - l <= kPackMax;
+  return !dead && !full && !narrow;
+}
+
+// D (defer): the wide rows are not stepped at all (no probe, no descent, none of
+// their code in the kernel, so it keeps few registers and many waves); their
+// lo / hi come out unspecified and k_lf_wide steps them.
+template <int G, bool GP, bool Q, bool D = false>
 __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h,
                                            uint64_t& lo, uint64_t& hi) {
   constexpr int R = 64 / G;                 // rows per wave
@@ -192,6 +208,7 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     lo = found ? fmin : 0;
     hi = found ? fmax + 1 : 0;
   }
+  if (D) return;
   if (GP) {   // a probe hit (at most one slot of the group holds the key) ends a wide row's step
     const uint64_t key0 = l | (c << kTransSymShift);
     uint64_t hit = 0, clo = 0, cw = 0;
@@ -346,6 +363,69 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_
     nh = v.n;
   }
   if (valid && (lane & (G - 1)) == 0) {
+    lo_out[i] = nl;
+    hi_out[i] = nh;
+  }
+}
+
+// The split launch of a large LF batch (fm_lf_step_batch above
+// FMIDX_LF_GROUP_MIN rows): this pass steps the cheap rows -- reset, dead, full
+// range, <= kPackMax-row E scans -- with no wide-row code at all (few VGPRs:
+// many waves per SIMD, the whole batch's random E reads in flight), and leaves
+// the wide rows to k_lf_wide (tagged in the outputs).  A wave whose rows are all cheap was
+// held up before by any one wide row among its 64 / G (a probe, a descent,
+// stepped one at a time by the whole wave).
+template <int G>
+__global__ void __launch_bounds__(kLfThreads) k_lf_cheap(DevView v, const int64_t* __restrict__ tok,
+                                                        int64_t shift, int64_t reset_below,
+                                                        const uint64_t* lo_in, const uint64_t* hi_in,
+                                                        uint64_t* lo_out, uint64_t* hi_out, uint64_t m) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  if (wave * (64 / G) >= m) return;      // wave-uniform
+  const uint64_t i = wave * (64 / G) + lane / G;
+  const bool valid = i < m;
+  const uint64_t ii = valid ? i : m - 1;
+  const int64_t t = (int64_t)row_load_u64(tok, m, ii);
+  const uint64_t l = row_load_u64(lo_in, m, ii), h = row_load_u64(hi_in, m, ii);
+  const bool live = valid && t >= reset_below;
+  uint64_t nl, nh;
+  group_step<G, false, false, true>(v, live, t + shift, l, h, nl, nh);
+  if (t < reset_below) {
+    nl = 0;
+    nh = v.n;
+  }
+  if (valid && (lane & (G - 1)) == 0) {
+    // a wide row is handed to k_lf_wide through the output buffers: its input
+    // range, tagged (n < 2^34, so no result has bit 63).  Through the outputs,
+    // not the inputs: an in-place launch has overwritten the cheap rows' inputs.
+    const bool wide = lf_wide(v, live, t + shift, l, h);
+    lo_out[i] = wide ? l : nl;
+    hi_out[i] = wide ? (h < v.n ? h : v.n) | kLfWideTag : nh;
+  }
+}
+
+// The split launch's second pass: only the wide rows step (group_step's probe
+// stage four at a time, then one at a time by the whole wave); the others are
+// not written.
+template <int G, bool Q>
+__global__ void __launch_bounds__(kLfThreads) k_lf_wide(DevView v, const int64_t* __restrict__ tok,
+                                                       int64_t shift, uint64_t* lo_out, uint64_t* hi_out,
+                                                       uint64_t m) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  if (wave * (64 / G) >= m) return;      // wave-uniform
+  const uint64_t i = wave * (64 / G) + lane / G;
+  const bool valid = i < m;
+  const uint64_t ii = valid ? i : m - 1;
+  const uint64_t hw = hi_out[ii];
+  const bool wide = valid && (hw & kLfWideTag);
+  if (!__ballot(wide)) return;           // wave-uniform: no wide row here
+  const int64_t t = (int64_t)row_load_u64(tok, m, ii);
+  const uint64_t l = lo_out[ii], h = hw & ~kLfWideTag;
+  uint64_t nl, nh;
+  group_step<G, false, Q>(v, wide, t + shift, l, h, nl, nh);
+  if (wide && (lane & (G - 1)) == 0) {
     lo_out[i] = nl;
     hi_out[i] = nh;
   }
@@ -822,11 +902,18 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //    loop: 2^19 cold pairs 87 vs 93 us.  Not in k_search_group, where the extra
 //    registers (155 VGPRs: 3 waves per SIMD) cost more than it saves (565 vs
 //    548 us).
+//  * FMIDX_LF_SPLIT (default 0): 1 runs a G = 2 LF launch as two passes,
+//    k_lf_cheap (every row but the wide ones: 36 VGPRs, 8 waves per SIMD) then
+//    k_lf_wide (the wide rows only).  Exact, but slower at C3: 2^19 cold pairs
+//    98.4 vs 76.0 us -- the wide rows, stepped a few at a time per wave, are
+//    the critical path either way, and the cheap rows were already hidden
+//    under them; the second sweep only adds a pass.
 struct LfTuning {
   uint32_t G;
   uint64_t min_rows;
   bool gprobe;
   bool quad;
+  bool split;
 };
 
 LfTuning load_lf_tuning() {
@@ -836,6 +923,7 @@ LfTuning load_lf_tuning() {
   t.min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
   t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
   t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
+  t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
   return t;
 }
 
@@ -847,6 +935,7 @@ LfTuning& lf_tuning() {
 uint32_t lf_group(uint64_t m) { return m > lf_tuning().min_rows ? lf_tuning().G : 64u; }
 bool lf_gprobe() { return lf_tuning().gprobe; }
 bool lf_quad() { return lf_tuning().quad; }
+bool lf_split() { return lf_tuning().split; }
 
 }  // namespace
 
@@ -859,7 +948,13 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
   if (m == 0) return 0;
   const uint32_t G = lf_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
-  if (G == 1)
+  if (G == 2 && lf_split()) {
+    k_lf_cheap<2><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
+    if (lf_quad())
+      k_lf_wide<2, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, lo_out, hi_out, m);
+    else
+      k_lf_wide<2, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, lo_out, hi_out, m);
+  } else if (G == 1)
     k_lf_group<1, false, false><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);
   else if (G == 2 && lf_quad())
     k_lf_group<2, false, true><<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m);

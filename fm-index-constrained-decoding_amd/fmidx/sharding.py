@@ -241,6 +241,10 @@ def or_bits(parts, vocab: int, out=None, unpack: bool = True):
     if out is None:
         out = (torch.empty((B, vocab), dtype=torch.uint8, device=parts.device) if unpack
                else torch.empty((B, W), dtype=torch.int32, device=parts.device))
+    want = (B, vocab) if unpack else (B, W)
+    if tuple(out.shape) != want or out.stride(1) != 1 or out.dtype != (torch.uint8 if unpack else torch.int32):
+        raise ValueError(f"or_bits: out must be a row-major {'uint8' if unpack else 'int32'} {want}, "
+                         f"got {out.dtype} {tuple(out.shape)} strides {out.stride()}")
     ld = out.stride(0) * out.element_size()
     stream = torch.cuda.current_stream(parts.device).cuda_stream
     check(lib().fm_or_bits(c_void_p(parts.data_ptr()), P, B * W, B, W, vocab, c_void_p(out.data_ptr()), ld,

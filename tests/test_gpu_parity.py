@@ -273,7 +273,8 @@ def _grouped_case(cache_min):
 
 # every launch variant of the grouped kernels (csrc/query.hip lf_tuning): lanes per
 # row, the in-group transition probe (G >= 4) and the four-at-a-time wide stage (G = 2)
-_LF_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"},
+_LF_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMIDX_LF_SPLIT": "1"},
+                {"FMIDX_LF_SPLIT": "1", "FMIDX_LF_QUAD": "0"},
                 {"FMIDX_LF_GROUP": "4", "FMIDX_LF_GPROBE": "0"}, {"FMIDX_LF_GROUP": "4", "FMIDX_LF_GPROBE": "1"},
                 {"FMIDX_LF_GROUP": "8", "FMIDX_LF_GPROBE": "0"}, {"FMIDX_LF_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
                 {"FMIDX_LF_GROUP": "16"}, {"FMIDX_LF_GROUP": "64"}]
@@ -294,7 +295,7 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
 
     ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
     m = len(pats)
-    for k in ("FMIDX_LF_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD"):
+    for k in ("FMIDX_LF_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD", "FMIDX_LF_SPLIT"):
         monkeypatch.delenv(k, raising=False)
     for k, x in variant.items():
         monkeypatch.setenv(k, x)
@@ -314,6 +315,11 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
         ours.lf_step_batch(torch.tensor(nxt, device=dev), lo_in, hi_in, 10, lo_out=lo_out, hi_out=hi_out,
                            reset_below=-2)
         got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
+        bad = [i for i in range(m) if got[i] != want_lf[i]]
+        assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
+        # in place (the decode loop's launch: outputs over the inputs)
+        ours.lf_step_batch(torch.tensor(nxt, device=dev), lo_in, hi_in, 10, reset_below=-2)
+        got = list(zip(lo_in.cpu().tolist(), hi_in.cpu().tolist()))
         bad = [i for i in range(m) if got[i] != want_lf[i]]
         assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
     finally:
