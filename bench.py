@@ -1021,6 +1021,45 @@ def main():
                     np.median([a + b for a, b in big]))
         except Exception:
             pass
+    # Memory-side read requests by size (tools/pmc_req.sh, committed under profiles/ with the
+    # library hash): on gfx950 every random read -- 8 B, a 64-B line, a 128-B line -- is one
+    # 128-B request (tools/pmc_gather_calib.py), so the random-read ceiling is a REQUEST rate,
+    # measured live here by the gather shapes (one request per line for the cooperative shapes
+    # and the 8-B words), and a kernel's requests per launch say what it really moved.
+    gm = gather_modes or {}
+    req_ceiling = max(gm.get("coop8_128B", 0) / 128, gm.get("coop4_64B", 0) / 64,
+                      gm.get("lane_8B", 0) / 8)          # G requests/s (GB/s / B per request)
+    result["rank"]["request_ceiling_G_per_s"] = req_ceiling
+    for name, where in (("pmc_req_rank.json", "rank"), ("pmc_req_c3.json", "roofline")):
+        path = os.path.join(REPO, "profiles", name)
+        if not os.path.exists(path) or n < 4e9:
+            continue
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            if t.get("lib_sha16") != lib_hash:
+                result[where]["pmc_requests_source"] = f"none: profiles/{name} was counted on lib {t.get('lib_sha16')}"
+                continue
+            if where == "rank":      # the 2^19-row launches (the by-path launches write less)
+                rows = [r for r in t["dispatches"] if "k_lf_group" in r["kernel"] and r.get("write_bytes", 0) >= 8e6]
+            else:                    # the uint8 decode launches of the C3 bench (B = 256)
+                rows = [r for r in t["dispatches"] if "k_decode<false, true" in r["kernel"]]
+            if not rows:
+                continue
+            req = float(np.median([r["rdreq"] for r in rows]))
+            rd = float(np.median([r["read_bytes"] for r in rows]))
+            wr = float(np.median([r["write_bytes"] for r in rows]))
+            us = rs_us if where == "rank" else decode_us
+            result[where].update({
+                "pmc_requests_per_launch": req, "pmc_read_bytes_per_launch": rd, "pmc_write_bytes_per_launch": wr,
+                "pmc_hbm_GBps": (rd + wr) / (us * 1e-6) / 1e9,
+                "pmc_requests_source": f"profiles/{name} (same lib_sha16; {len(rows)} launches, median)"})
+            if where == "rank":
+                rate = req / (us * 1e-6) / 1e9
+                result["rank"]["request_rate_G_per_s"] = rate
+                result["rank"]["frac_of_request_ceiling"] = rate / req_ceiling if req_ceiling else None
+        except Exception as e:
+            result[where]["pmc_requests_source"] = f"unreadable: {e!r}"
     if cpu_leg:
         try:
             result["cpu_baseline"] = cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, W,
