@@ -109,6 +109,10 @@ constexpr uint64_t kPackMax = 128;
 // Every lane executes the same loads (unconditional, clamped or dummy index:
 // a guarded load is sunk into a branch with a vmcnt(0) behind it).
 constexpr uint64_t kLfWideTag = 1ull << 63;
+#ifndef FMIDX_E_PASS
+#define FMIDX_E_PASS 1
+#endif
+constexpr int kEPass = FMIDX_E_PASS;   // wave-packed E scan: 64-entry passes per round trip
 
 // Whether a row's LF step is "wide" in group_step's sense: live, not dead, not
 // the full range, and not a <= kPackMax-row E scan.  The split launch
@@ -174,22 +178,36 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     s_lf[wv][1][slot] = 0;
   }
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t t0 = 0; t0 < total; t0 += 64) {          // wave-uniform
-    const uint32_t e = t0 + lane;
-    const bool valid = e < total;
-    uint32_t r = 0;                                      // the last row whose offset is <= e
+  // kEPass passes of 64 entries per iteration, every pass's E load issued
+  // before any is consumed.  Measured at C3 (2^19 cold pairs / 2^18 patterns):
+  // 1 pass 76.1 / 420 us, 4 passes 80.2 / 504, 8 passes 81.6 / 520 -- a wave's
+  // narrow rows rarely need a second pass, and the extra unconditional loads
+  // and registers cost more than the round trips they would save.
+  for (uint32_t t0 = 0; t0 < total; t0 += 64 * kEPass) {   // wave-uniform
+    uint64_t xs[kEPass], rcs[kEPass];
+    uint32_t rs[kEPass];
 #pragma unroll
-    for (int step = R / 2; step > 0; step >>= 1) {
-      const uint32_t x = __shfl(excl, (int)((r + step) * G), 64);
-      if (x <= e) r += step;
+    for (int k = 0; k < kEPass; ++k) {
+      const uint32_t e = t0 + 64u * k + lane;
+      const bool valid = e < total;
+      uint32_t r = 0;                                    // the last row whose offset is <= e
+#pragma unroll
+      for (int step = R / 2; step > 0; step >>= 1) {
+        const uint32_t x = __shfl(excl, (int)((r + step) * G), 64);
+        if (x <= e) r += step;
+      }
+      const uint64_t base = __shfl(l, (int)(r * G), 64);
+      rcs[k] = __shfl(c, (int)(r * G), 64);
+      const uint32_t off = e - __shfl(excl, (int)(r * G), 64);
+      xs[k] = v.E[valid ? base + off : 0];
+      rs[k] = valid ? r : ~0u;
     }
-    const uint64_t base = __shfl(l, (int)(r * G), 64);
-    const uint64_t rc = __shfl(c, (int)(r * G), 64);
-    const uint32_t off = e - __shfl(excl, (int)(r * G), 64);
-    const uint64_t x = v.E[valid ? base + off : 0];
-    if (valid && (x >> kESymShift) == rc) {
-      atomicMin(&s_lf[wv][0][r], (unsigned long long)(x & kELfMask));
-      atomicMax(&s_lf[wv][1][r], (unsigned long long)(x & kELfMask));
+#pragma unroll
+    for (int k = 0; k < kEPass; ++k) {
+      if (rs[k] != ~0u && (xs[k] >> kESymShift) == rcs[k]) {
+        atomicMin(&s_lf[wv][0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+        atomicMax(&s_lf[wv][1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -894,6 +912,10 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //    the C3 index (tools/probe_rank.py, 2^19 pairs, cold): one wave per row
 //    308 us, G = 16 / 8 / 4 / 2 / 1: 179 / 125 / 99 / 90 / 100 us; get_range of
 //    2^18 patterns 2658 us -> 539 us at G = 2.
+//  * FMIDX_SEARCH_GROUP (default 1): the same for get_range launches
+//    (k_search_group).  Since the wave-packed E scan (round 3), 2^18 patterns
+//    on the C3 index take 364 / 416 / 527 us cold at G = 1 / 2 / 4 (the LF
+//    step kernel: 79.2 / 77.3 / 79.4 us), so get_range groups one lane per row.
 //  * FMIDX_LF_GPROBE (default 1): grouped launches with G >= 4 probe the
 //    transition table inside the group, so a cached range's hit needs no
 //    wave-wide step.
@@ -910,6 +932,7 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //    under them; the second sweep only adds a pass.
 struct LfTuning {
   uint32_t G;
+  uint32_t Gs;   // get_range
   uint64_t min_rows;
   bool gprobe;
   bool quad;
@@ -920,6 +943,8 @@ LfTuning load_lf_tuning() {
   LfTuning t;
   const uint32_t g = env_u32("FMIDX_LF_GROUP", 2);
   t.G = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 64u;
+  const uint32_t gs = env_u32("FMIDX_SEARCH_GROUP", 1);
+  t.Gs = (gs == 1 || gs == 2 || gs == 4 || gs == 8 || gs == 16) ? gs : 64u;
   t.min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
   t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
   t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
@@ -933,6 +958,7 @@ LfTuning& lf_tuning() {
 }
 
 uint32_t lf_group(uint64_t m) { return m > lf_tuning().min_rows ? lf_tuning().G : 64u; }
+uint32_t search_group(uint64_t m) { return m > lf_tuning().min_rows ? lf_tuning().Gs : 64u; }
 bool lf_gprobe() { return lf_tuning().gprobe; }
 bool lf_quad() { return lf_tuning().quad; }
 bool lf_split() { return lf_tuning().split; }
@@ -980,7 +1006,7 @@ int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,
                   uint64_t* hi_out, hipStream_t s) {
   if (m == 0) return 0;
-  const uint32_t G = lf_group(m);
+  const uint32_t G = search_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
   if (G == 1)
     k_search_group<1, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
