@@ -41,6 +41,16 @@ namespace {
 // for the kernel-end writeback to flush (MI355X_MICROARCH.md "boundary":
 // + bytes / 6 TB/s behind a predecessor that leaves bytes dirty); 0 = plain.
 constexpr int kStoreAux = FMIDX_STORE_AUX;
+#ifndef FMIDX_LATE_AUX
+#define FMIDX_LATE_AUX FMIDX_STORE_AUX
+#endif
+// cache policy of the final emit of rows NOT zero-filled early (the wide rows
+// that end the step): a lone CU writes a 128-KB row in 1.0 us with plain
+// stores and 1.5 us write-through (tools/micro/cu_store.hip), but the dirty
+// lines then cost the kernel end more: C3 cold / warm 13.9 / 10.6 us with
+// plain late stores, 14.0 / 11.8 with plain stores everywhere, against 13.5 /
+// 9.9 write-through (profiles/r03_latency/store_policy.log)
+constexpr int kLateAux = FMIDX_LATE_AUX;
 constexpr int kMaxPlan = 160;                 // >= 6 * kMaxBmLevels
 constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
 // LDS window words for a slice of sw tokens: the window starts at most 127
@@ -260,6 +270,15 @@ __device__ __forceinline__ uint4 gld4(const uint32_t* p, int64_t i) {
 __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x) {
   v4u v = {x.x, x.y, x.z, x.w};
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
+}
+
+// the final emit: write-through (kStoreAux) for rows zero-filled early, kLateAux otherwise
+__device__ __forceinline__ void store16_emit(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& x, bool zeroed) {
+  v4u v = {x.x, x.y, x.z, x.w};
+  if (kLateAux == kStoreAux || zeroed)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kLateAux);
 }
 
 __device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t x) {
@@ -650,7 +669,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         if (PACKED) {
           store4(orsrc, k * 4, bits);
         } else if (aligned16 && full) {
-          store16(orsrc, k * 16, bits16_to_bytes(bits));
+          store16_emit(orsrc, k * 16, bits16_to_bytes(bits), zeroed);
         } else {
           slow |= 1u << u;
         }
@@ -682,7 +701,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       if (PACKED) {
         store4(orsrc, (uint32_t)(k * 4), bits);   // t0 and t are multiples of 32
       } else if (aligned16 && cnt == 16) {
-        store16(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits));
+        store16_emit(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits), zeroed);
       } else {
         for (uint64_t j = 0; j < cnt; ++j) out_row[t + j] = (uint8_t)((bits >> j) & 1u);
       }
