@@ -49,9 +49,7 @@ constexpr int kStoreAux = FMIDX_STORE_AUX;
 // stores and 1.5 us write-through (tools/micro/cu_store.hip), but the dirty
 // lines then cost the kernel end more: C3 cold / warm 13.9 / 10.6 us with
 // plain late stores, 14.0 / 11.8 with plain stores everywhere, against 13.5 /
-// 9.9 write-through (profiles/r03_latency/store_policy.log).  Other policies
-// of all mask stores (aux 2 = nt, 17 = sc0 sc1, 18 = nt sc1, 19) are within
-// +-0.1 us cold of sc1 and 0.5-0.8 us slower warm.
+// 9.9 write-through (profiles/r03_latency/store_policy.log)
 constexpr int kLateAux = FMIDX_LATE_AUX;
 constexpr int kMaxPlan = 160;                 // >= 6 * kMaxBmLevels
 constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
