@@ -219,6 +219,28 @@ def gather_ceiling(dev, nbytes=8 << 30):
 
 
 # ---------------------------------------------------------------------------
+def cpu_share():
+    """The CPUs this process is given, not the machine's: a shared GPU box shows
+    every core of the host to os.cpu_count() / sched_getaffinity, while its CPU
+    share is set by the cgroup quota and announced through OMP_NUM_THREADS.
+    Returns (threads, where the number came from)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = f"sched_getaffinity {n}"
+    try:                                   # cgroup v2: "quota period" or "max period"
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max" and int(per) > 0:
+            c = max(1, -(-int(q) // int(per)))
+            if c < n:
+                n, src = c, f"cgroup cpu.max {q}/{per}"
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and 0 < int(env) < n:
+        n, src = int(env), f"OMP_NUM_THREADS={env}"
+    return n, src
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -248,7 +270,7 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
     t0 = time.time()
     ref = CpuRef.from_device_bwt(bwt)
     log(f"cpu_ref build {time.time() - t0:.1f}s")
-    all_cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    all_cores, share_src = cpu_share()
     B = tokens.shape[1]
     tok_np = tokens.cpu().numpy()
     lo_all = lo_hist.cpu().numpy().astype(np.uint64)
@@ -322,11 +344,12 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
     head = legs["incremental_all"]
     return {"value": head["value"], "unit": "masks/s", "cores": all_cores, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "cores_source": share_src,
             "sample": f"trace steps {first}..{last} ({window} steps x {B} rows) of the same trace and "
                       f"n={bwt.numel()} index, after one untimed warm-up step, median of {reps} repetitions; "
                       f"sdsl-faithful wt_int + rank_support_v restatement (oracle/cpu_ref.cpp); value = the "
-                      f"incremental leg on all {all_cores} cores this process may use (the fastest CPU mode); "
-                      f"the reference's own per-step work is the full_research legs",
+                      f"incremental leg on the {all_cores} cores this process is given ({share_src}; the "
+                      f"fastest CPU mode); the reference's own per-step work is the full_research legs",
             "legs": legs,
             "one_thread_s_per_step": per_step,
             "ranges_match_gpu": all(v["ranges_match_gpu"] for v in legs.values()),

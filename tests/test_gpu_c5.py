@@ -70,7 +70,7 @@ def test_c5_paq_shape(c5):
     widths = []
     for s in range(S):
         fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
-        ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, clo, chi, cmask, 32)
+        ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, clo, chi, cmask, 16)
         assert np.array_equal(lo.cpu().numpy().astype(np.uint64), clo), f"step {s}: ranges"
         assert np.array_equal(hi.cpu().numpy().astype(np.uint64), chi), f"step {s}: ranges"
         bad = np.nonzero((mask.cpu().numpy() != cmask).any(1))[0]
