@@ -656,8 +656,9 @@ def main():
     ap.add_argument("--corpus", choices=("markov", "paq"), default="markov",
                     help="paq: PAQ-shaped docs (prefix + question + eos, C5) with the paq trace")
     ap.add_argument("--seed", type=int, default=20250905)
-    ap.add_argument("--cpu-window", type=int, default=3,
-                    help="CPU baseline: trace steps every leg times (after one untimed warm-up step)")
+    ap.add_argument("--cpu-window", type=int, default=-1,
+                    help="CPU baseline: trace steps every leg times (after one untimed warm-up step); "
+                         "-1 = enough steps for >= 768 masks per repetition (3 at B = 256, 24 at B = 32)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="CPU baseline: repetitions per leg (median reported)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the gather-ceiling probe")
@@ -695,6 +696,8 @@ def main():
     st = fm.stats()
     st["lf_e"] = os.environ.get("FMIDX_LF_E", "1") != "0" and n < (1 << 36)
     S = W + K
+    if args.cpu_window < 0:
+        args.cpu_window = max(3, -(-768 // B))
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu and args.cpu_window > 0 and args.cpu_reps > 0
     # the CPU legs replay steps W .. W + cpu_window of the same trace
     S_trace = max(S, W + args.cpu_window + 1) if cpu_leg else S
