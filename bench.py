@@ -1056,7 +1056,17 @@ def main():
     req_ceiling = max(gm.get("coop8_128B", 0) / 128, gm.get("coop4_64B", 0) / 64,
                       gm.get("lane_8B", 0) / 8)          # G requests/s (GB/s / B per request)
     result["rank"]["request_ceiling_G_per_s"] = req_ceiling
-    for name, where in (("pmc_req_rank.json", "rank"), ("pmc_req_c3.json", "roofline")):
+    # the rank figure comes from this bench's own 2^19-pair launch (pmc_req_c3.json, counted over the
+    # same command) when that file has it, else from tools/probe_rank.py's launch of the same shape
+    have_c3_rank = False
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_req_c3.json")) as f:
+            have_c3_rank = any("k_lf_group" in r["kernel"] and r.get("write_bytes", 0) >= 8e6
+                               for r in json.load(f)["dispatches"])
+    except (OSError, ValueError, KeyError):
+        pass
+    for name, where in ((("pmc_req_c3.json" if have_c3_rank else "pmc_req_rank.json"), "rank"),
+                        ("pmc_req_c3.json", "roofline")):
         path = os.path.join(REPO, "profiles", name)
         if not os.path.exists(path) or n < 4e9:
             continue
