@@ -977,8 +977,14 @@ int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
-  return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out,
-                               d_hi_out, m, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t wsb = fmidx::lf_ws_bytes(m);
+  if (!wsb) return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s);
+  if (ws_acquire(h, s, wsb)) return -1;
+  const int rc = fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s,
+                                       h->idx.ws);
+  if (ws_release(h, s)) return -1;
+  return rc;
   FM_API_END
 }
 
@@ -1196,6 +1202,26 @@ int fm_device_bwt(const fm_index* h, const uint32_t** out) {
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
   *out = h->idx.bwt;
+  return 0;
+  FM_API_END
+}
+
+int fm_device_struct(const fm_index* h, int which, const void** out, uint64_t* bytes) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  const auto& x = h->idx;
+  const void* p = nullptr;
+  uint64_t b = 0;
+  switch (which) {
+    case 0: p = x.bwt; b = x.n * 4; break;
+    case 1: p = x.E; b = x.E ? x.n * 8 : 0; break;
+    case 2: p = x.trans_tab; b = x.trans_bytes; break;
+    case 3: p = x.cache_bm; b = x.cache_bm ? x.cache_nodes * (uint64_t)x.view.bm_words * 4 : 0; break;
+    case 4: p = x.w2_blocks[0]; b = x.w2_blocks[0] ? x.view.w2[0].blk_bytes * ((x.n + fmidx::kW2Blk - 1) / fmidx::kW2Blk) : 0; break;
+    default: fmidx::set_error("fm_device_struct: unknown structure %d", which); return -1;
+  }
+  *out = p;
+  *bytes = p ? b : 0;
   return 0;
   FM_API_END
 }

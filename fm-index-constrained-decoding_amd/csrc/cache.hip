@@ -202,11 +202,13 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   }
   if (entries == 0 || cap * 24 > budget) return 0;
   uint64_t* tab = nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&tab), cap * 24) != hipSuccess) {
+  // kTransPad slots past the end mirror slots [0, kTransPad) (filled after the
+  // insert), so a probe run can be read as one contiguous span without wrapping
+  if (hipMalloc(reinterpret_cast<void**>(&tab), (cap + kTransPad) * 24) != hipSuccess) {
     (void)hipGetLastError();
     return 0;   // no room: the descent serves every step
   }
-  FM_HIP(hipMemsetAsync(tab, 0xFF, cap * 24, s));
+  FM_HIP(hipMemsetAsync(tab, 0xFF, (cap + kTransPad) * 24, s));
   DBuf<unsigned long long> d_stats;
   if (d_stats.alloc(2)) {
     (void)hipFree(tab);
@@ -222,6 +224,8 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   build_phase("transitions: insert pass", t, s);
   unsigned long long st[2] = {0, 0};
   FM_HIP(hipMemcpy(st, d_stats.p, 16, hipMemcpyDeviceToHost));
+  FM_HIP(hipMemcpyAsync(tab + 3 * cap, tab, kTransPad * 24, hipMemcpyDeviceToDevice, s));
+  FM_HIP(hipStreamSynchronize(s));
   h->trans_tab = tab;
   h->trans_entries = st[0];
   h->trans_dropped = st[1];

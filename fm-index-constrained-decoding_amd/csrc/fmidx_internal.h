@@ -461,6 +461,7 @@ constexpr uint32_t kTransSymShift = 34;
 constexpr uint64_t kMask34 = (1ull << 34) - 1;
 constexpr uint64_t kTransOne = 1ull << 25;
 constexpr uint32_t kTransProbe = 16;
+constexpr uint64_t kTransPad = 32;   // slots after the table's end mirroring its first kTransPad (cache.hip)
 constexpr uint64_t kTransEmpty = ~0ull;
 
 __host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi, uint64_t c, uint64_t cap) {
@@ -690,9 +691,11 @@ int launch_extract(const DevView& v, const SampleView& sv, const uint64_t* begin
 void reload_lf_tuning();
 // locate.hip: rows of the positions that are multiples of kSaRate, from ISA samples
 int launch_isa_walk(const DevView& v, const uint64_t* isa, uint64_t nisa, uint64_t* rows_out, hipStream_t s);
+// ws: workspace of lf_ws_bytes(m) bytes for the worklist sweeps (null: the grouped kernels)
 int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
-                   uint64_t m, hipStream_t s);
+                   uint64_t m, hipStream_t s, void* ws = nullptr);
+size_t lf_ws_bytes(uint64_t m);   // 0: this launch takes no workspace
 int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint64_t m,
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,
                   uint64_t* hi_out, hipStream_t s);

@@ -483,6 +483,341 @@ __global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const in
   }
 }
 
+// ------------------------------------------------------------ worklist LF
+// (opt-in, FMIDX_LF_WORK=1: exact -- the LF parity test runs it -- but measured
+// no faster than the grouped kernel at C3, 2^19 cold pairs: k_lf_sweep 45 us +
+// k_lf_tail 25 us + the counter memset and two dependent launches, 92 us per
+// call against 76; warm 26 + 18.  profiles/r03_rank/worklist/.)
+// Throughput form of fm_lf_step_batch above FMIDX_LF_GROUP_MIN rows, in two
+// launches that keep every lane of a wave on one kind of work.  (The grouped
+// kernels above serialise a wave's wide rows behind each other, so a wave of
+// 32 mostly-narrow rows lives as long as its slowest wide rows' chains.)
+//   k_lf_sweep  one lane per row: reset / dead rows, the full range (C
+//               lookup), every range of <= kSweepScan rows -- its E entries
+//               scanned packed end to end over the wave, so a load
+//               instruction touches about one line per row -- and every
+//               cached range's transition probe, eight rows at a time with 8
+//               lanes each (the 16-slot run staged through LDS from 128-B-wide
+//               loads, the range's own range-cache run alongside), issued in
+//               the same round trip as the E scan.  Everything else -- ranges
+//               of 65..512 rows, uncached wide ranges, probe misses -- goes to
+//               the tail list: one atomic per workgroup (returning device
+//               atomics are the expensive part of an append: two per wave cost
+//               ~30 us over 2^19 rows);
+//   k_lf_tail   persistent waves over the tail list, one row per wave: an E
+//               scan of <= 512 rows or the 2-level descent (a probe miss
+//               starts it with the range's cached bitmap word, so a symbol the
+//               range lacks ends after the first level).
+// The tail list is split into kWorkRegions regions (region = the appending
+// workgroup's index mod kWorkRegions) so the atomics spread over as many
+// counters; k_lf_tail's waves are assigned to regions the same way.  Every row
+// is written exactly once, by the kernel that settles it, so in-place launches
+// (lo_out == lo_in) stay correct.
+struct LfWork {
+  uint64_t l, h;   // the row's range (h clamped to n)
+  uint64_t sym;    // symbol | (cache id + 1 of the range, for a probe miss) << 32
+  uint64_t row;
+};
+constexpr uint32_t kWorkRegions = 64;
+constexpr uint64_t kSweepScan = 64;   // widest range k_lf_sweep scans in E
+constexpr int kSweepPass = 2;   // 64-entry passes per round trip of the packed scan (2: 92 VGPRs; 4: 100)
+constexpr uint32_t kProbeLanes = 8;
+constexpr uint32_t kProbeRows = 64 / kProbeLanes;
+constexpr uint32_t kProbeChunks = 32;   // 16-B chunks staged per probe row (a 16-slot run spans <= 25)
+
+// Transition probe of up to eight rows (8 lanes each; row k of the batch =
+// the wave's lane src[k], src < 0: none) -- loads only; probe_finish consumes.
+struct ProbeLoads {
+  uint4 c0, c1, c2, c3;   // 16-B chunks sl, sl + 8, sl + 16, sl + 24 of the row's run
+  uint4 ce;               // the range's own range-cache slot sl
+};
+__device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, uint64_t h, uint64_t c) {
+  const uint32_t sl = (threadIdx.x & 63u) % kProbeLanes;
+  const uint64_t home = trans_home(l, h, c, v.trans_cap);
+  // the run's bytes [24 home, 24 home + 384) as 16-B chunks from c0; the table
+  // carries kTransPad mirrored slots past its end, so nothing wraps
+  const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab) + ((24 * home) >> 4) + sl;
+  ProbeLoads p;
+  p.c0 = tt[0];
+  p.c1 = tt[kProbeLanes];
+  p.c2 = tt[2 * kProbeLanes];
+  p.c3 = tt[3 * kProbeLanes];
+  // the range's own range-cache run (8 slots, one per lane)
+  const uint64_t cs = (cache_hash(l, h) + sl) & v.cache_mask;
+  p.ce = v.cache_mask ? reinterpret_cast<const uint4*>(v.cache_tab)[cs] : make_uint4(~0u, ~0u, 0, 0);
+  return p;
+}
+
+// -> per lane: hit (and the child range on the row's first lane), or the
+// range's cache id + 1 (0: not found) for the tail entry of a miss
+__device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint64_t h, uint64_t c, bool act,
+                                            const ProbeLoads& p, uint4* s_run, bool& hit_row, uint64_t& clo,
+                                            uint64_t& chi, uint64_t& pid1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
+  const uint64_t home = trans_home(l, h, c, v.trans_cap);
+  uint4* sr = s_run + seg * kProbeChunks + sl;
+  sr[0] = p.c0;
+  sr[kProbeLanes] = p.c1;
+  sr[2 * kProbeLanes] = p.c2;
+  sr[3 * kProbeLanes] = p.c3;
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]) + ((24 * home) & 15) / 8;
+  const uint64_t key0 = l | (c << kTransSymShift);
+  bool hit = false;
+  uint64_t w1 = 0, w2 = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 2; ++u) {
+    const uint32_t slot = 2 * sl + u;
+    const uint64_t x0 = run[3 * slot], x1 = run[3 * slot + 1], x2 = run[3 * slot + 2];
+    const bool mt = x0 == key0 && (x1 & kMask34) == h;
+    hit |= mt;
+    w1 = mt ? x1 : w1;
+    w2 = mt ? x2 : w2;
+  }
+  __builtin_amdgcn_wave_barrier();   // a later batch's staging overwrites s_run
+  const uint64_t klo = (uint64_t)p.ce.x | ((uint64_t)p.ce.y << 32);
+  const uint64_t khi = (uint64_t)p.ce.z | ((uint64_t)p.ce.w << 32);
+  const bool pc = v.cache_mask && klo == l && (khi & kMask34) == h;
+  const uint64_t segm = 0xFFull << (kProbeLanes * seg);
+  const uint64_t hb = __ballot(act && hit) & segm, pb = __ballot(act && pc) & segm;
+  const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
+  const uint64_t hw1 = __shfl(w1, hl, 64), hw2 = __shfl(w2, hl, 64);
+  const int pl = pb ? __ffsll((long long)pb) - 1 : (int)lane;
+  const uint64_t pk = __shfl(khi, pl, 64);
+  hit_row = hb != 0;
+  clo = (hw1 >> kTransSymShift) | ((hw2 & 0xFu) << 30);
+  chi = clo + ((hw2 >> 4) & kMask34);
+  pid1 = pb ? (pk >> kCacheIdShift) + 1 : 0;
+}
+
+__global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
+                                                        int64_t reset_below, const uint64_t* lo_in,
+                                                        const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                                                        uint64_t m, LfWork* lt, uint32_t* cnt, uint64_t cap) {
+  __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
+  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
+  __shared__ uint32_t s_n[kLfThreads / 64 + 1];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t seg = lane / kProbeLanes;
+  const uint64_t i = (uint64_t)blockIdx.x * kLfThreads + threadIdx.x;
+  // (no early return: every wave of the workgroup reaches the append's barriers)
+  const bool valid = i < m;
+  const uint64_t ii = valid ? i : m - 1;
+  const int64_t t = (int64_t)row_load_u64(tok, m, ii);
+  const uint64_t l = row_load_u64(lo_in, m, ii);
+  uint64_t h = row_load_u64(hi_in, m, ii);
+  if (h > v.n) h = v.n;
+  const int64_t sym = t + shift;
+  const bool reset = valid && t < reset_below;
+  const bool live = valid && !reset;
+  const bool dead = live && (l >= h || sym < 0 || (uint64_t)sym > v.max_sym);
+  const bool full = live && !dead && l == 0 && h == v.n;
+  const bool step = live && !dead && !full;
+  const bool narrow = step && v.E && h - l <= kSweepScan;
+  const bool probe = step && !narrow && v.trans_cap && h - l >= v.cache_min;
+  bool tail = step && !narrow && !probe;
+  const uint64_t c = (uint64_t)sym;
+  const uint64_t cf = full ? c : 0;   // the others all read C[0..1]: one shared line
+  const uint64_t ca = v.C[cf], cb = v.C[cf + 1];
+  // ---- packed E scan: the narrow rows' entries end to end over the wave
+  const uint32_t cnt_e = narrow ? (uint32_t)(h - l) : 0u;
+  uint32_t inc = cnt_e;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  const uint32_t excl = inc - cnt_e;
+  const uint32_t total = __shfl(inc, 63, 64);
+  s_mm[wv][0][lane] = ~0ull;
+  s_mm[wv][1][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  uint64_t pmask = __ballot(probe);   // probe rows left, batches of kProbeRows
+  uint64_t res_lo = 0, res_hi = 0, pid1 = 0;   // a probe row's result (on its own lane)
+  bool probed = false;
+  for (uint32_t t0 = 0; t0 < total || pmask; t0 += 64 * kSweepPass) {   // wave-uniform
+    uint64_t xs[kSweepPass], cs[kSweepPass];
+    uint32_t rs[kSweepPass];
+#pragma unroll
+    for (int k = 0; k < kSweepPass; ++k) {
+      const uint32_t e = t0 + 64u * k + lane;
+      uint32_t r = 0;   // the last row whose offset is <= e (rows of no entries are never it)
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+        const uint32_t x = __shfl(excl, (int)(r + st), 64);
+        if (x <= e) r += st;
+      }
+      const uint64_t base = __shfl(l, (int)r, 64);
+      const uint32_t off = e - __shfl(excl, (int)r, 64);
+      cs[k] = __shfl(c, (int)r, 64);
+      // unconditional (a surplus lane reads E[0]: one shared line)
+      xs[k] = v.E[e < total ? base + off : 0];
+      rs[k] = e < total ? r : ~0u;
+    }
+    // the next batch of probe rows, in the same round trip
+    int src = -1;
+    {
+      uint64_t pm = pmask;
+      for (uint32_t k = 0; k < kProbeRows && pm; ++k) {
+        const int s = __ffsll((long long)pm) - 1;
+        pm &= pm - 1;
+        if (seg == k) src = s;
+      }
+      pmask = pm;
+    }
+    const bool pact = src >= 0;
+    const int ps = pact ? src : 0;
+    const uint64_t pl = __shfl(l, ps, 64), ph = __shfl(h, ps, 64), pc = __shfl(c, ps, 64);
+    // (no transition table: no row is a probe row and this batch is empty;
+    // the loads are skipped wave-uniformly)
+    ProbeLoads pld = {};
+    if (v.trans_cap) pld = probe_issue(v, pl, ph, pc);
+#pragma unroll
+    for (int k = 0; k < kSweepPass; ++k) {
+      if (rs[k] != ~0u && (xs[k] >> kESymShift) == cs[k]) {
+        atomicMin(&s_mm[wv][0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+        atomicMax(&s_mm[wv][1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+      }
+    }
+    if (v.trans_cap && __ballot(pact)) {
+      bool hit;
+      uint64_t clo, chi, p1;
+      probe_finish(v, pl, ph, pc, pact, pld, s_run[wv], hit, clo, chi, p1);
+      // hand each probed row its result (the batch's k-th row sits in segment k)
+#pragma unroll
+      for (uint32_t k = 0; k < kProbeRows; ++k) {
+        const int sk = __shfl(src, (int)(k * kProbeLanes), 64);
+        const uint64_t xl = __shfl(clo, (int)(k * kProbeLanes), 64), xh = __shfl(chi, (int)(k * kProbeLanes), 64);
+        const uint64_t xp = __shfl(p1, (int)(k * kProbeLanes), 64);
+        const int xhit = __shfl((int)hit, (int)(k * kProbeLanes), 64);
+        if (sk >= 0 && (int)lane == sk) {
+          probed = xhit != 0;
+          res_lo = xl;
+          res_hi = xh;
+          pid1 = xp;
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // LF is increasing over a symbol's rows: the new range is [min LF, max LF + 1) of the matches
+  const uint64_t fmin = s_mm[wv][0][lane], fmax = s_mm[wv][1][lane];
+  uint64_t nl = 0, nh = 0;
+  if (reset) {
+    nl = 0;
+    nh = v.n;
+  } else if (full) {
+    nl = ca < cb ? ca : 0;
+    nh = ca < cb ? cb : 0;
+  } else if (narrow && fmin != ~0ull) {
+    nl = fmin;
+    nh = fmax + 1;
+  } else if (probed) {
+    nl = res_lo;
+    nh = res_hi;
+  }
+  tail = tail || (probe && !probed);
+  if (valid && !tail) {
+    lo_out[i] = nl;
+    hi_out[i] = nh;
+  }
+  // ---- tail rows: one atomic per workgroup (LDS-only barriers: nothing
+  // crossing them is global data, so the stores above need not drain)
+  const uint64_t tb = __ballot(tail);
+  if (lane == 0) s_n[wv] = (uint32_t)__popcll(tb);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const uint32_t r = (uint32_t)(blockIdx.x % kWorkRegions);
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < kLfThreads / 64; ++w) tot += s_n[w];
+    s_n[kLfThreads / 64] = tot ? atomicAdd(&cnt[r], tot) : 0u;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (tail) {
+    uint32_t pos = s_n[kLfThreads / 64];
+    for (uint32_t w = 0; w < wv; ++w) pos += s_n[w];
+    pos += (uint32_t)__popcll(tb & ((1ull << lane) - 1));
+    lt[(uint64_t)r * cap + pos] = LfWork{l, h, c | (pid1 << 32), i};
+  }
+}
+
+// The 2-level descent / wide E scan, by a whole wave (uniform inputs;
+// lo < hi <= n, not the full range, sym valid).  pword = the range's cached
+// bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
+// step after the descent's first level.
+__device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint32_t pword, uint64_t& lo,
+                                             uint64_t& hi) {
+  if (v.E && hi - lo <= kENarrow) {
+    uint32_t cm = 0;
+    lf_step_fast<false>(v, (int64_t)c, lo, hi, nullptr, cm);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
+  const uint32_t c32 = (uint32_t)c;
+  const int64_t dd = v.D2[c32];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  uint64_t pos = side ? hi : lo;
+#pragma unroll 1
+  for (int l = 0; l < (int)v.NL2; ++l) {
+    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
+    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {
+      lo = 0;
+      hi = 0;
+      return;
+    }
+    pos = z[l] + r;
+  }
+  const uint64_t other = __shfl_xor(pos, 32, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
+// persistent over the tail list: wave w serves region w mod kWorkRegions, one
+// row per iteration; the next row's entry is loaded ahead of the current step
+__global__ void __launch_bounds__(kLfThreads) k_lf_tail(DevView v, const LfWork* __restrict__ lt,
+                                                       const uint32_t* __restrict__ cnt, uint64_t cap,
+                                                       uint64_t* lo_out, uint64_t* hi_out, uint32_t waves_per_region) {
+  FM_PRELOAD_VIEW(v);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  const uint32_t r = (uint32_t)(wave % kWorkRegions);
+  const uint64_t nt = cnt[r];
+  const LfWork* st = lt + (uint64_t)r * cap;
+  uint64_t j = wave / kWorkRegions;
+  if (j >= nt) return;   // wave-uniform
+  LfWork it = st[j];
+  for (; j < nt; j += waves_per_region) {   // wave-uniform
+    const uint64_t jn = j + waves_per_region;
+    const LfWork nx = st[jn < nt ? jn : j];
+    uint64_t l = it.l, h = it.h;
+    const uint32_t c32 = (uint32_t)it.sym;
+    const uint64_t pid1 = it.sym >> 32;
+    // a probe miss: the range's bitmap word for c (unconditional: bwt[0] as a dummy)
+    const uint32_t* pw = pid1 ? v.cache_bm + (pid1 - 1) * v.bm_words + (c32 >> 5) : v.bwt;
+    const uint32_t pword = pid1 ? *pw : ~0u;
+    lf_step_tail(v, c32, pword, l, h);
+    if (lane == 0) {
+      lo_out[it.row] = l;
+      hi_out[it.row] = h;
+    }
+    it = nx;
+  }
+}
+
 // [sdsl] backward_search on an inclusive range with unsigned wrap-around.
 __device__ void sdsl_backward_search(const DevView& v, uint64_t c, uint64_t l, uint64_t r,
                                      uint64_t& lr, uint64_t& rr) {
@@ -937,6 +1272,7 @@ struct LfTuning {
   bool gprobe;
   bool quad;
   bool split;
+  bool work;     // worklist sweeps (k_lf_sweep / k_lf_probe / k_lf_tail) when a workspace is given
 };
 
 LfTuning load_lf_tuning() {
@@ -949,6 +1285,7 @@ LfTuning load_lf_tuning() {
   t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
   t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
   t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
+  t.work = env_u32("FMIDX_LF_WORK", 0) != 0;
   return t;
 }
 
@@ -962,16 +1299,40 @@ uint32_t search_group(uint64_t m) { return m > lf_tuning().min_rows ? lf_tuning(
 bool lf_gprobe() { return lf_tuning().gprobe; }
 bool lf_quad() { return lf_tuning().quad; }
 bool lf_split() { return lf_tuning().split; }
+bool lf_work() { return lf_tuning().work; }
+
+// worklist geometry for m rows: entries per region, sweep-1 waves
+uint64_t lf_work_cap(uint64_t m) {
+  return (((m + kLfThreads - 1) / kLfThreads + kWorkRegions - 1) / kWorkRegions) * kLfThreads;
+}
 
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
 void reload_lf_tuning() { lf_tuning() = load_lf_tuning(); }
 
+size_t lf_ws_bytes(uint64_t m) {
+  return m > lf_tuning().min_rows && lf_work() ? kWorkRegions * lf_work_cap(m) * sizeof(LfWork) + kWorkRegions * 4 : 0;
+}
+
 int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
-                   uint64_t m, hipStream_t s) {
+                   uint64_t m, hipStream_t s, void* ws) {
   if (m == 0) return 0;
+  if (ws && m > lf_tuning().min_rows && lf_work()) {
+    const uint64_t cap = lf_work_cap(m);
+    LfWork* lt = reinterpret_cast<LfWork*>(ws);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lt + kWorkRegions * cap);
+    FM_HIP(hipMemsetAsync(cnt, 0, kWorkRegions * 4, s));
+    const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
+    k_lf_sweep<<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, lt, cnt, cap);
+    // persistent: at most 8192 waves (the chip's slots at 8 waves per SIMD),
+    // no more per region than its worst-case row count
+    const uint32_t q = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192 / kWorkRegions, cap));
+    k_lf_tail<<<q * kWorkRegions / (kLfThreads / 64), kLfThreads, 0, s>>>(v, lt, cnt, cap, lo_out, hi_out, q);
+    FM_HIP(hipGetLastError());
+    return 0;
+  }
   const uint32_t G = lf_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
   if (G == 2 && lf_split()) {

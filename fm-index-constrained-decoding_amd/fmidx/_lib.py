@@ -68,6 +68,7 @@ SIGNATURES = {
                             c_void_p]),
     "fm_probe_gather": (c_int, [c_void_p, c_uint64, c_int, c_uint64, c_uint32, c_void_p, c_void_p]),
     "fm_device_bwt": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "fm_device_struct": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_uint64)]),
     "fm_synchronize": (c_int, [c_void_p]),
     "fm_reload_tuning": (c_int, []),
     "fm_attach_isa_samples_device": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),

@@ -440,6 +440,14 @@ class FMIndex:
         check(lib().fm_device_bwt(self._h, byref(p)), "device_bwt")
         return int(p.value or 0)
 
+    def device_struct(self, which: int):
+        """(device pointer, bytes) of one index structure (fm_device_struct:
+        0 BWT, 1 E, 2 transition table, 3 range-bitmap cache, 4 first wavelet
+        level); (0, 0) when it is not built.  Measurement only."""
+        p, b = c_void_p(), c_uint64()
+        check(lib().fm_device_struct(self._h, which, byref(p), byref(b)), "device_struct")
+        return int(p.value or 0), int(b.value)
+
     def synchronize(self) -> None:
         check(lib().fm_synchronize(self._h), "synchronize")
 

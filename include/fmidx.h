@@ -405,6 +405,13 @@ int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads
 /* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces. */
 int fm_device_bwt(const fm_index* h, const uint32_t** out);
 
+/* Device pointer and byte size of one index structure, for the bench's
+ * gather ceilings over the index's own allocations: which = 0 plain BWT,
+ * 1 E array, 2 transition table, 3 range-bitmap cache, 4 first level of the
+ * 2-level wavelet matrix.  *out = NULL, *bytes = 0 when the structure is not
+ * built.  (Measurement only; no reference counterpart.) */
+int fm_device_struct(const fm_index* h, int which, const void** out, uint64_t* bytes);
+
 /* Synchronise the handle's device (hipDeviceSynchronize on its device). */
 int fm_synchronize(fm_index* h);
 

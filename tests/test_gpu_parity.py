@@ -271,16 +271,18 @@ def _grouped_case(cache_min):
     return _GROUPED_CASES[cache_min]
 
 
-# every launch variant of the grouped kernels (csrc/query.hip lf_tuning): lanes per
-# row, the in-group transition probe (G >= 4) and the four-at-a-time wide stage (G = 2)
-_LF_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMIDX_LF_SPLIT": "1"},
-                {"FMIDX_LF_SPLIT": "1", "FMIDX_LF_QUAD": "0"}, {"FMIDX_SEARCH_GROUP": "2"},
-                {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "0"},
-                {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "1"},
-                {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "0"},
-                {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
-                {"FMIDX_LF_GROUP": "16", "FMIDX_SEARCH_GROUP": "16"},
-                {"FMIDX_LF_GROUP": "64", "FMIDX_SEARCH_GROUP": "64"}]
+# every launch variant of the LF kernels (csrc/query.hip lf_tuning): the grouped
+# kernels -- lanes per row, the in-group transition probe (G >= 4), the
+# four-at-a-time wide stage (G = 2) -- and the opt-in worklist sweeps
+_GROUPED_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMIDX_LF_SPLIT": "1"},
+                     {"FMIDX_LF_SPLIT": "1", "FMIDX_LF_QUAD": "0"}, {"FMIDX_SEARCH_GROUP": "2"},
+                     {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "0"},
+                     {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "1"},
+                     {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "0"},
+                     {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
+                     {"FMIDX_LF_GROUP": "16", "FMIDX_SEARCH_GROUP": "16"},
+                     {"FMIDX_LF_GROUP": "64", "FMIDX_SEARCH_GROUP": "64"}]
+_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}]
 
 
 @pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k[6:]}{x}" for k, x in v.items()) or "default")
@@ -298,7 +300,8 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
 
     ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
     m = len(pats)
-    for k in ("FMIDX_LF_GROUP", "FMIDX_SEARCH_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD", "FMIDX_LF_SPLIT"):
+    for k in ("FMIDX_LF_GROUP", "FMIDX_SEARCH_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD", "FMIDX_LF_SPLIT",
+              "FMIDX_LF_WORK"):
         monkeypatch.delenv(k, raising=False)
     for k, x in variant.items():
         monkeypatch.setenv(k, x)
