@@ -591,6 +591,50 @@ __device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint6
   pid1 = pb ? (pk >> kCacheIdShift) + 1 : 0;
 }
 
+// The 2-level descent / wide E scan, by a whole wave (uniform inputs;
+// lo < hi <= n, not the full range, sym valid).  pword = the range's cached
+// bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
+// step after the descent's first level.
+__device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint32_t pword, uint64_t& lo,
+                                             uint64_t& hi) {
+  if (v.E && hi - lo <= kENarrow) {
+    uint32_t cm = 0;
+    lf_step_fast<false>(v, (int64_t)c, lo, hi, nullptr, cm);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
+  const uint32_t c32 = (uint32_t)c;
+  const int64_t dd = v.D2[c32];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  uint64_t pos = side ? hi : lo;
+#pragma unroll 1
+  for (int l = 0; l < (int)v.NL2; ++l) {
+    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
+    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {
+      lo = 0;
+      hi = 0;
+      return;
+    }
+    pos = z[l] + r;
+  }
+  const uint64_t other = __shfl_xor(pos, 32, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
+template <bool INLINE>
 __global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
                                                         int64_t reset_below, const uint64_t* lo_in,
                                                         const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
@@ -719,6 +763,28 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_
     nh = res_hi;
   }
   tail = tail || (probe && !probed);
+  if (INLINE) {
+    // the wave's tail rows one at a time by the whole wave (lf_step_tail), then every row is written
+    uint64_t tb = __ballot(tail);
+    while (tb) {
+      const int src = __ffsll((long long)tb) - 1;
+      tb &= tb - 1;
+      uint64_t tl = __shfl(l, src, 64), th = __shfl(h, src, 64);
+      const uint64_t tc = __shfl(c, src, 64), tp = __shfl(pid1, src, 64);
+      const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5) : v.bwt;
+      const uint32_t pword = tp ? *pw : ~0u;
+      lf_step_tail(v, tc, pword, tl, th);
+      if ((int)lane == src) {
+        nl = tl;
+        nh = th;
+      }
+    }
+    if (valid) {
+      lo_out[i] = nl;
+      hi_out[i] = nh;
+    }
+    return;
+  }
   if (valid && !tail) {
     lo_out[i] = nl;
     hi_out[i] = nh;
@@ -741,49 +807,6 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_
     pos += (uint32_t)__popcll(tb & ((1ull << lane) - 1));
     lt[(uint64_t)r * cap + pos] = LfWork{l, h, c | (pid1 << 32), i};
   }
-}
-
-// The 2-level descent / wide E scan, by a whole wave (uniform inputs;
-// lo < hi <= n, not the full range, sym valid).  pword = the range's cached
-// bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
-// step after the descent's first level.
-__device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint32_t pword, uint64_t& lo,
-                                             uint64_t& hi) {
-  if (v.E && hi - lo <= kENarrow) {
-    uint32_t cm = 0;
-    lf_step_fast<false>(v, (int64_t)c, lo, hi, nullptr, cm);
-    return;
-  }
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t q = lane & 31u;
-  const bool side = lane >= 32;
-  const uint32_t c32 = (uint32_t)c;
-  const int64_t dd = v.D2[c32];
-  uint64_t z[kW2MaxLevels];
-#pragma unroll
-  for (int l = 0; l < kW2MaxLevels; ++l)
-    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
-  uint64_t pos = side ? hi : lo;
-#pragma unroll 1
-  for (int l = 0; l < (int)v.NL2; ++l) {
-    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
-    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {
-      lo = 0;
-      hi = 0;
-      return;
-    }
-    pos = z[l] + r;
-  }
-  const uint64_t other = __shfl_xor(pos, 32, 64);
-  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
-  if (l2 >= h2) {
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  lo = (uint64_t)((int64_t)l2 + dd);
-  hi = (uint64_t)((int64_t)h2 + dd);
 }
 
 // persistent over the tail list: wave w serves region w mod kWorkRegions, one
@@ -1272,7 +1295,8 @@ struct LfTuning {
   bool gprobe;
   bool quad;
   bool split;
-  bool work;     // worklist sweeps (k_lf_sweep / k_lf_probe / k_lf_tail) when a workspace is given
+  bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
+  bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
 };
 
 LfTuning load_lf_tuning() {
@@ -1285,7 +1309,8 @@ LfTuning load_lf_tuning() {
   t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
   t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
   t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
-  t.work = env_u32("FMIDX_LF_WORK", 0) != 0;
+  t.work = env_u32("FMIDX_LF_WORK", 0) == 1;
+  t.work_inline = env_u32("FMIDX_LF_WORK", 0) == 2;
   return t;
 }
 
@@ -1319,13 +1344,20 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s, void* ws) {
   if (m == 0) return 0;
+  if (m > lf_tuning().min_rows && lf_tuning().work_inline) {   // one launch, tail rows stepped in-wave
+    const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
+    k_lf_sweep<true><<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, nullptr,
+                                               nullptr, 0);
+    FM_HIP(hipGetLastError());
+    return 0;
+  }
   if (ws && m > lf_tuning().min_rows && lf_work()) {
     const uint64_t cap = lf_work_cap(m);
     LfWork* lt = reinterpret_cast<LfWork*>(ws);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(lt + kWorkRegions * cap);
     FM_HIP(hipMemsetAsync(cnt, 0, kWorkRegions * 4, s));
     const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
-    k_lf_sweep<<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, lt, cnt, cap);
+    k_lf_sweep<false><<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, lt, cnt, cap);
     // persistent: at most 8192 waves (the chip's slots at 8 waves per SIMD),
     // no more per region than its worst-case row count
     const uint32_t q = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192 / kWorkRegions, cap));

@@ -282,7 +282,7 @@ _GROUPED_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMID
                      {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
                      {"FMIDX_LF_GROUP": "16", "FMIDX_SEARCH_GROUP": "16"},
                      {"FMIDX_LF_GROUP": "64", "FMIDX_SEARCH_GROUP": "64"}]
-_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}]
+_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}, {"FMIDX_LF_WORK": "2"}]
 
 
 @pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k[6:]}{x}" for k, x in v.items()) or "default")
