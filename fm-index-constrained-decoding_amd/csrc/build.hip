@@ -530,7 +530,14 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   FM_HIP(hipFree(nxt));
 
   // -- range bitmaps
-  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", 12);
+  // Base block of the aligned bitmap hierarchy.  A decode step never reads the
+  // hierarchy at scale (every range of >= cache_min rows it can reach is in
+  // the range cache, and a narrower range holds no aligned 4096-row block);
+  // it serves arbitrary user ranges and the cache's own construction.  At C3
+  // 2^14-row blocks instead of 2^12 free 16.5 GiB (200.4 -> 183.9) with the
+  // same step (13.4 us cold) and build time (profiles/r03_memory/bm_log2/);
+  // small indexes keep 2^12 so that they still get a hierarchy and a cache.
+  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", n >= (1ull << 26) ? 14 : 12);
   const uint32_t words = (uint32_t)(((uint64_t)max_sym + 1 + 127) / 128 * 4);
   const uint64_t nb0 = n >> log2b0;
   uint32_t bm_levels = 0;
