@@ -1285,9 +1285,9 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //  * FMIDX_LF_SPLIT (default 0): 1 runs a G = 2 LF launch as two passes,
 //    k_lf_cheap (every row but the wide ones: 36 VGPRs, 8 waves per SIMD) then
 //    k_lf_wide (the wide rows only).  Exact, but slower at C3: 2^19 cold pairs
-//    98.4 vs 76.0 us -- the wide rows, stepped a few at a time per wave, are
-//    the critical path either way, and the cheap rows were already hidden
-//    under them; the second sweep only adds a pass.
+//    98.4 vs 76.0 us (the second pass still steps wide rows a few per wave).
+//  * FMIDX_LF_WORK (default 0): 1 / 2 = the worklist sweeps above (k_lf_sweep
+//    + k_lf_tail, or tail rows in-wave); exact, not faster cold.
 struct LfTuning {
   uint32_t G;
   uint32_t Gs;   // get_range
