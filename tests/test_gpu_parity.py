@@ -829,3 +829,50 @@ def test_distinct_count_batch_capacity_overflow(dev):
         for j in range(int(k[i])):
             got += [int(syms[s0 + j]), int(counts[s0 + j])]
         assert tuple(got) == ora.distinct_count(a, b), i
+
+
+def _device_u8(ptr, nbytes, owner):
+    """A uint8 torch view of nbytes of device memory at ptr (kept alive by owner)."""
+    import torch
+
+    class _V:
+        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 2,
+                                    "strides": None}
+
+        def __init__(self):
+            self.owner = owner
+
+    return torch.as_tensor(_V(), device=torch.device("cuda", 0))
+
+
+def test_device_structs(dev):
+    """fm_device_struct (the bench's gather ceilings over the index's own
+    allocations) reports each structure's pointer and size, and the structures
+    are what the kernels assume: E[i] = LF(i) | BWT[i] << 36 with LF the
+    stable order of the BWT by symbol (LF(i) = C[BWT[i]] + rank), and the
+    transition table's kTransPad (32) slots past its end mirror its first 32
+    (csrc/cache.hip), so a probe run is read without wrapping."""
+    import torch
+
+    docs = markov_docs(11, 300, 200, 120)
+    ours = ours_index(docs, bm_log2=5, cache_min=4)
+    n = ours.size()
+    p0, b0 = ours.device_struct(0)
+    assert p0 == ours.device_bwt_ptr() and b0 == 4 * n
+    bwt = ours.device_bwt().to(torch.int64)
+    p1, b1 = ours.device_struct(1)
+    assert p1 and b1 == 8 * n
+    E = _device_u8(p1, b1, ours).view(torch.int64)
+    assert torch.equal(E >> 36, bwt)
+    lf = E & ((1 << 36) - 1)
+    order = torch.argsort(bwt, stable=True)
+    assert torch.equal(lf[order], torch.arange(n, device=dev))
+    p2, b2 = ours.device_struct(2)
+    assert p2 and b2 > 0 and b2 % 24 == 0
+    tab = _device_u8(p2, b2 + 32 * 24, ours)
+    assert torch.equal(tab[b2:], tab[:32 * 24])
+    for w in (3, 4):
+        p, b = ours.device_struct(w)
+        assert p and b > 0
+    with pytest.raises(Exception):
+        ours.device_struct(9)
