@@ -333,6 +333,38 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
         lib().fm_reload_tuning()
 
 
+@pytest.mark.parametrize("cache_min", [None, 4])
+def test_small_lf_batches_vs_oracle(dev, cache_min):
+    """fm_lf_step_batch launches of <= 8192 rows (one wave per row, k_lf) --
+    every row of the grouped test's 20011 (state, token) pairs (dead, empty,
+    full, narrow, wide and cached ranges, unknown ids, hi past n, reset rows)
+    in launches of 256 and of 37 rows, out of place and in place, against the
+    oracle.  (One 1024-thread workgroup per row -- the fused kernel's LF stage
+    alone, whose workgroup E scan replaces the descent of a 513..4095-row
+    range -- was measured slower at C3, B = 256: 6.9 vs 6.4 us cold.)"""
+    import torch
+
+    ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
+    tok_all = torch.tensor(nxt, device=dev)
+    lo_all = torch.tensor(li, dtype=torch.int64, device=dev)
+    hi_all = torch.tensor(hv, dtype=torch.int64, device=dev)
+    M = len(nxt)
+    for width in (256, 37):
+        got_lo = torch.empty_like(lo_all)
+        got_hi = torch.empty_like(hi_all)
+        for a in range(0, M, width):
+            b = min(M, a + width)
+            t, l, h = tok_all[a:b].contiguous(), lo_all[a:b].clone(), hi_all[a:b].clone()
+            ol, oh = torch.empty_like(l), torch.empty_like(h)
+            ours.lf_step_batch(t, l, h, 10, lo_out=ol, hi_out=oh, reset_below=-2)
+            ours.lf_step_batch(t, l, h, 10, reset_below=-2)   # in place
+            assert torch.equal(ol, l) and torch.equal(oh, h), (width, a)
+            got_lo[a:b], got_hi[a:b] = ol, oh
+        got = list(zip(got_lo.cpu().tolist(), got_hi.cpu().tolist()))
+        bad = [i for i in range(M) if got[i] != want_lf[i]]
+        assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
+
+
 @pytest.mark.parametrize("cache_min,e2", [(None, "0"), (4, "0"), (None, "1"), (4, "1")])
 def test_decode_step_fused_and_reset(dev, cache_min, e2, monkeypatch):
     """Fused LF + mask against the oracle, with and without E2 (the narrow
