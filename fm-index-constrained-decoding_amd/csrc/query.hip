@@ -90,6 +90,88 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
 // wave-packed scan of group_step (one load per entry actually needed).
 constexpr uint64_t kPackMax = 128;
 
+// Transition probe of a wave's cached rows eight at a time (8 lanes per row):
+// the row's 16-slot run as four 16-B loads per lane (128 B contiguous per
+// row and instruction) staged through LDS, and (CE) the range's own
+// range-cache run alongside.  Used by get_range (group_step<P8>) and the
+// opt-in LF sweep (k_lf_sweep).
+constexpr uint32_t kProbeLanes = 8;
+constexpr uint32_t kProbeRows = 64 / kProbeLanes;
+constexpr uint32_t kProbeChunks = 32;   // 16-B chunks staged per probe row (a 16-slot run spans <= 25)
+
+// Transition probe of up to eight rows (8 lanes each; row k of the batch =
+// the wave's lane src[k], src < 0: none) -- loads only; probe_finish consumes.
+struct ProbeLoads {
+  uint4 c0, c1, c2, c3;   // 16-B chunks sl, sl + 8, sl + 16, sl + 24 of the row's run
+  uint4 ce;               // the range's own range-cache slot sl
+};
+template <bool CE = true>
+__device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, uint64_t h, uint64_t c) {
+  const uint32_t sl = (threadIdx.x & 63u) % kProbeLanes;
+  const uint64_t home = trans_home(l, h, c, v.trans_cap);
+  // the run's bytes [24 home, 24 home + 384) as 16-B chunks from c0; the table
+  // carries kTransPad mirrored slots past its end, so nothing wraps
+  const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab) + ((24 * home) >> 4) + sl;
+  ProbeLoads p;
+  p.c0 = tt[0];
+  p.c1 = tt[kProbeLanes];
+  p.c2 = tt[2 * kProbeLanes];
+  p.c3 = tt[3 * kProbeLanes];
+  // the range's own range-cache run (8 slots, one per lane)
+  if (CE) {
+    const uint64_t cs = (cache_hash(l, h) + sl) & v.cache_mask;
+    p.ce = v.cache_mask ? reinterpret_cast<const uint4*>(v.cache_tab)[cs] : make_uint4(~0u, ~0u, 0, 0);
+  } else {
+    p.ce = make_uint4(~0u, ~0u, 0, 0);
+  }
+  return p;
+}
+
+// -> per lane: hit (and the child range on the row's first lane), or the
+// range's cache id + 1 (0: not found) for the tail entry of a miss
+template <bool CE = true>
+__device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint64_t h, uint64_t c, bool act,
+                                            const ProbeLoads& p, uint4* s_run, bool& hit_row, uint64_t& clo,
+                                            uint64_t& chi, uint64_t& pid1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
+  const uint64_t home = trans_home(l, h, c, v.trans_cap);
+  uint4* sr = s_run + seg * kProbeChunks + sl;
+  sr[0] = p.c0;
+  sr[kProbeLanes] = p.c1;
+  sr[2 * kProbeLanes] = p.c2;
+  sr[3 * kProbeLanes] = p.c3;
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]) + ((24 * home) & 15) / 8;
+  const uint64_t key0 = l | (c << kTransSymShift);
+  bool hit = false;
+  uint64_t w1 = 0, w2 = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 2; ++u) {
+    const uint32_t slot = 2 * sl + u;
+    const uint64_t x0 = run[3 * slot], x1 = run[3 * slot + 1], x2 = run[3 * slot + 2];
+    const bool mt = x0 == key0 && (x1 & kMask34) == h;
+    hit |= mt;
+    w1 = mt ? x1 : w1;
+    w2 = mt ? x2 : w2;
+  }
+  __builtin_amdgcn_wave_barrier();   // a later batch's staging overwrites s_run
+  const uint64_t klo = (uint64_t)p.ce.x | ((uint64_t)p.ce.y << 32);
+  const uint64_t khi = (uint64_t)p.ce.z | ((uint64_t)p.ce.w << 32);
+  const bool pc = CE && v.cache_mask && klo == l && (khi & kMask34) == h;
+  const uint64_t segm = 0xFFull << (kProbeLanes * seg);
+  const uint64_t hb = __ballot(act && hit) & segm, pb = __ballot(act && pc) & segm;
+  const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
+  const uint64_t hw1 = __shfl(w1, hl, 64), hw2 = __shfl(w2, hl, 64);
+  const int pl = pb ? __ffsll((long long)pb) - 1 : (int)lane;
+  const uint64_t pk = __shfl(khi, pl, 64);
+  hit_row = hb != 0;
+  clo = (hw1 >> kTransSymShift) | ((hw2 & 0xFu) << 30);
+  chi = clo + ((hw2 >> 4) & kMask34);
+  pid1 = pb ? (pk >> kCacheIdShift) + 1 : 0;
+}
+
+
 // One LF step for every group of the wave.  `live` = the group takes a step
 // (false: the row is left as it is).  The loads are shaped for request
 // efficiency (the random-line rate of HBM counts requests -- one per (load
@@ -128,7 +210,9 @@ __device__ __forceinline__ bool lf_wide(const DevView& v, bool live, int64_t sym
 // D (defer): the wide rows are not stepped at all (no probe, no descent, none of
 // their code in the kernel, so it keeps few registers and many waves); their
 // lo / hi come out unspecified and k_lf_wide steps them.
-template <int G, bool GP, bool Q, bool D = false>
+// P8 (get_range, G = 1): cached wide rows probe the transition table eight at
+// a time (probe_issue / probe_finish) before the one-at-a-time loop.
+template <int G, bool GP, bool Q, bool D = false, bool P8 = false>
 __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t sym, uint64_t l, uint64_t h,
                                            uint64_t& lo, uint64_t& hi) {
   constexpr int R = 64 / G;                 // rows per wave
@@ -227,6 +311,39 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     hi = found ? fmax + 1 : 0;
   }
   if (D) return;
+  if (P8) {
+    // cached wide rows eight per round trip; a hit settles the row, a miss (a
+    // symbol the range lacks, or a key the table left out) stays wide
+    __shared__ uint4 s_run8[kLfThreads / 64][kProbeRows * kProbeChunks];
+    const uint32_t seg = lane / kProbeLanes;
+    uint64_t pm = __ballot(wide && j == 0 && v.trans_cap && h - l >= v.cache_min);
+    while (pm) {   // wave-uniform
+      int src = -1;
+      for (uint32_t k = 0; k < kProbeRows && pm; ++k) {
+        const int s_ = __ffsll((long long)pm) - 1;
+        pm &= pm - 1;
+        if (seg == k) src = s_;
+      }
+      const bool act = src >= 0;
+      const int ps = act ? src : 0;
+      const uint64_t pl = __shfl(l, ps, 64), ph = __shfl(h, ps, 64), pc = __shfl(c, ps, 64);
+      const ProbeLoads pld = probe_issue<false>(v, pl, ph, pc);
+      bool hit;
+      uint64_t clo, chi, p1;
+      probe_finish<false>(v, pl, ph, pc, act, pld, s_run8[wv], hit, clo, chi, p1);
+#pragma unroll
+      for (uint32_t k = 0; k < kProbeRows; ++k) {
+        const int sk = __shfl(src, (int)(k * kProbeLanes), 64);
+        const uint64_t xl = __shfl(clo, (int)(k * kProbeLanes), 64), xh = __shfl(chi, (int)(k * kProbeLanes), 64);
+        const int xhit = __shfl((int)hit, (int)(k * kProbeLanes), 64);
+        if (sk >= 0 && xhit && (lane / G) == ((uint32_t)sk / G)) {
+          lo = xl;
+          hi = xh;
+          wide = false;
+        }
+      }
+    }
+  }
   if (GP) {   // a probe hit (at most one slot of the group holds the key) ends a wide row's step
     const uint64_t key0 = l | (c << kTransSymShift);
     uint64_t hit = 0, clo = 0, cw = 0;
@@ -449,8 +566,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_wide(DevView v, const int64_t
   }
 }
 
-template <int G, bool GP, bool Q>
-__global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const int64_t* __restrict__ tok,
+template <int G, bool GP, bool Q, bool P8 = false>
+__global__ void __launch_bounds__(kLfThreads, P8 ? 4 : 1) k_search_group(DevView v, const int64_t* __restrict__ tok,
                                                             const int64_t* __restrict__ off, uint64_t m,
                                                             int64_t shift, const uint64_t* lo_in,
                                                             const uint64_t* hi_in, uint64_t* lo_out,
@@ -469,7 +586,7 @@ __global__ void __launch_bounds__(kLfThreads) k_search_group(DevView v, const in
   while (__ballot(active)) {           // wave-uniform: until every group's pattern is done
     const int64_t t = tok[active ? j : 0];   // some group is active: tok has an element
     uint64_t nl, nh;
-    group_step<G, GP, Q>(v, active, t + shift, l, h, nl, nh);
+    group_step<G, GP, Q, false, P8>(v, active, t + shift, l, h, nl, nh);
     if (active) {
       l = nl;
       h = nh;
@@ -521,76 +638,6 @@ struct LfWork {
 constexpr uint32_t kWorkRegions = 64;
 constexpr uint64_t kSweepScan = 64;   // widest range k_lf_sweep scans in E
 constexpr int kSweepPass = 2;   // 64-entry passes per round trip of the packed scan (2: 92 VGPRs; 4: 100)
-constexpr uint32_t kProbeLanes = 8;
-constexpr uint32_t kProbeRows = 64 / kProbeLanes;
-constexpr uint32_t kProbeChunks = 32;   // 16-B chunks staged per probe row (a 16-slot run spans <= 25)
-
-// Transition probe of up to eight rows (8 lanes each; row k of the batch =
-// the wave's lane src[k], src < 0: none) -- loads only; probe_finish consumes.
-struct ProbeLoads {
-  uint4 c0, c1, c2, c3;   // 16-B chunks sl, sl + 8, sl + 16, sl + 24 of the row's run
-  uint4 ce;               // the range's own range-cache slot sl
-};
-__device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, uint64_t h, uint64_t c) {
-  const uint32_t sl = (threadIdx.x & 63u) % kProbeLanes;
-  const uint64_t home = trans_home(l, h, c, v.trans_cap);
-  // the run's bytes [24 home, 24 home + 384) as 16-B chunks from c0; the table
-  // carries kTransPad mirrored slots past its end, so nothing wraps
-  const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab) + ((24 * home) >> 4) + sl;
-  ProbeLoads p;
-  p.c0 = tt[0];
-  p.c1 = tt[kProbeLanes];
-  p.c2 = tt[2 * kProbeLanes];
-  p.c3 = tt[3 * kProbeLanes];
-  // the range's own range-cache run (8 slots, one per lane)
-  const uint64_t cs = (cache_hash(l, h) + sl) & v.cache_mask;
-  p.ce = v.cache_mask ? reinterpret_cast<const uint4*>(v.cache_tab)[cs] : make_uint4(~0u, ~0u, 0, 0);
-  return p;
-}
-
-// -> per lane: hit (and the child range on the row's first lane), or the
-// range's cache id + 1 (0: not found) for the tail entry of a miss
-__device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint64_t h, uint64_t c, bool act,
-                                            const ProbeLoads& p, uint4* s_run, bool& hit_row, uint64_t& clo,
-                                            uint64_t& chi, uint64_t& pid1) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
-  const uint64_t home = trans_home(l, h, c, v.trans_cap);
-  uint4* sr = s_run + seg * kProbeChunks + sl;
-  sr[0] = p.c0;
-  sr[kProbeLanes] = p.c1;
-  sr[2 * kProbeLanes] = p.c2;
-  sr[3 * kProbeLanes] = p.c3;
-  __builtin_amdgcn_wave_barrier();
-  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]) + ((24 * home) & 15) / 8;
-  const uint64_t key0 = l | (c << kTransSymShift);
-  bool hit = false;
-  uint64_t w1 = 0, w2 = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < 2; ++u) {
-    const uint32_t slot = 2 * sl + u;
-    const uint64_t x0 = run[3 * slot], x1 = run[3 * slot + 1], x2 = run[3 * slot + 2];
-    const bool mt = x0 == key0 && (x1 & kMask34) == h;
-    hit |= mt;
-    w1 = mt ? x1 : w1;
-    w2 = mt ? x2 : w2;
-  }
-  __builtin_amdgcn_wave_barrier();   // a later batch's staging overwrites s_run
-  const uint64_t klo = (uint64_t)p.ce.x | ((uint64_t)p.ce.y << 32);
-  const uint64_t khi = (uint64_t)p.ce.z | ((uint64_t)p.ce.w << 32);
-  const bool pc = v.cache_mask && klo == l && (khi & kMask34) == h;
-  const uint64_t segm = 0xFFull << (kProbeLanes * seg);
-  const uint64_t hb = __ballot(act && hit) & segm, pb = __ballot(act && pc) & segm;
-  const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
-  const uint64_t hw1 = __shfl(w1, hl, 64), hw2 = __shfl(w2, hl, 64);
-  const int pl = pb ? __ffsll((long long)pb) - 1 : (int)lane;
-  const uint64_t pk = __shfl(khi, pl, 64);
-  hit_row = hb != 0;
-  clo = (hw1 >> kTransSymShift) | ((hw2 & 0xFu) << 30);
-  chi = clo + ((hw2 >> 4) & kMask34);
-  pid1 = pb ? (pk >> kCacheIdShift) + 1 : 0;
-}
-
 // The 2-level descent / wide E scan, by a whole wave (uniform inputs;
 // lo < hi <= n, not the full range, sym valid).  pword = the range's cached
 // bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
@@ -1274,6 +1321,11 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //    (k_search_group).  Since the wave-packed E scan (round 3), 2^18 patterns
 //    on the C3 index take 364 / 416 / 527 us cold at G = 1 / 2 / 4 (the LF
 //    step kernel: 79.2 / 77.3 / 79.4 us), so get_range groups one lane per row.
+//  * FMIDX_SEARCH_P8 (default 1): get_range at one lane per row probes its
+//    cached wide rows eight per round trip (group_step<P8>, LDS-staged runs,
+//    123 VGPRs under a 4-wave cap) before the one-at-a-time loop: 2^18
+//    patterns 314-316 vs 367-374 us cold.  (The same stage in place of the
+//    four-row one of G = 2 LF launches measured no better: 75-87 vs 72-75 us.)
 //  * FMIDX_LF_GPROBE (default 1): grouped launches with G >= 4 probe the
 //    transition table inside the group, so a cached range's hit needs no
 //    wave-wide step.
@@ -1297,6 +1349,7 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
+  bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
 
 LfTuning load_lf_tuning() {
@@ -1311,6 +1364,7 @@ LfTuning load_lf_tuning() {
   t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
   t.work = env_u32("FMIDX_LF_WORK", 0) == 1;
   t.work_inline = env_u32("FMIDX_LF_WORK", 0) == 2;
+  t.search_p8 = env_u32("FMIDX_SEARCH_P8", 1) != 0;
   return t;
 }
 
@@ -1401,7 +1455,10 @@ int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint
   if (m == 0) return 0;
   const uint32_t G = search_group(m);
   const unsigned g = (unsigned)(((m + 64 / G - 1) / (64 / G) * 64 + kLfThreads - 1) / kLfThreads);
-  if (G == 1)
+  if (G == 1 && lf_tuning().search_p8)
+    k_search_group<1, false, false, true><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out,
+                                                                    hi_out);
+  else if (G == 1)
     k_search_group<1, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);
   else if (G == 2)
     k_search_group<2, false, false><<<g, kLfThreads, 0, s>>>(v, tok, off, m, shift, lo_in, hi_in, lo_out, hi_out);

@@ -282,7 +282,7 @@ _GROUPED_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMID
                      {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
                      {"FMIDX_LF_GROUP": "16", "FMIDX_SEARCH_GROUP": "16"},
                      {"FMIDX_LF_GROUP": "64", "FMIDX_SEARCH_GROUP": "64"}]
-_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}, {"FMIDX_LF_WORK": "2"}]
+_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}, {"FMIDX_LF_WORK": "2"}, {"FMIDX_SEARCH_P8": "0"}]
 
 
 @pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k[6:]}{x}" for k, x in v.items()) or "default")
@@ -301,7 +301,7 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
     ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
     m = len(pats)
     for k in ("FMIDX_LF_GROUP", "FMIDX_SEARCH_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD", "FMIDX_LF_SPLIT",
-              "FMIDX_LF_WORK"):
+              "FMIDX_LF_WORK", "FMIDX_SEARCH_P8"):
         monkeypatch.delenv(k, raising=False)
     for k, x in variant.items():
         monkeypatch.setenv(k, x)
