@@ -33,8 +33,9 @@ import contextlib
 import csv
 import multiprocessing
 import re
+from dataclasses import dataclass
 from functools import partial
-from typing import Callable, Iterable, Iterator, List, Optional, Sequence
+from typing import Callable, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -47,69 +48,105 @@ except ImportError:                     # pragma: no cover - not in this image
         return text
 
 
+_WHITESPACE = re.compile(r"\s+")
+_WIKI_MARKERS = ("BULLET::::", "SECTION::::")
+
+
+@dataclass(frozen=True)
+class PassageRules:
+    """How a passage becomes index text (build_fm_index.py:69-95 and its
+    ``--include_title / --delim / --lowercase / --tokenize`` flags)."""
+    include_title: bool = False
+    delim: str = "@@"
+    lowercase: bool = False
+    word_tokenize: Optional[Callable[[str], List[str]]] = None
+
+
+def read_records(f, format: str) -> Iterator[Tuple[str, str, str]]:
+    """(id, title, text) for every well-formed record of an open passage file:
+    KILT lines ``id<TAB>title<TAB>text`` (build_fm_index.py:61-65), DPR csv
+    rows ``id<TAB>text<TAB>title`` after one header line (:55-59); records
+    without exactly three fields are skipped, as there."""
+    if format == "kilt":
+        for line in f:
+            fields = line.strip().split("\t", 2)
+            if len(fields) == 3:
+                yield fields[0], fields[1], fields[2]
+    elif format == "dpr":
+        next(f, None)
+        for fields in csv.reader(f, delimiter="\t", quotechar='"'):
+            if len(fields) == 3:
+                pid, text, title = fields
+                yield pid, title, text
+    else:
+        raise ValueError(f"unknown format {format!r}")
+
+
+def clean_passage(title: str, text: str, rules: PassageRules) -> Optional[str]:
+    """One passage's index text, or None when nothing is left of it
+    (build_fm_index.py:74-93)."""
+    body = _fix_text(_WHITESPACE.sub(" ", text))
+    for marker in _WIKI_MARKERS:
+        body = body.replace(marker, "")
+    body = body.strip()
+    if not body:
+        return None
+    title = title.strip()
+    if rules.word_tokenize is not None:
+        title = " ".join(rules.word_tokenize(title))
+        body = " ".join(rules.word_tokenize(body))
+    if rules.include_title:
+        # the reference tests the title after appending the delimiter, so an
+        # empty title still contributes " {delim} "
+        body = f"{title} {rules.delim} {body}"
+    return body.lower() if rules.lowercase else body
+
+
 def preprocess_file(input_path: str, labels: List[str], format: str = "kilt", lowercase: bool = False,
                     tokenize: bool = False, include_title: bool = False, delim: str = "@@",
                     word_tokenize: Optional[Callable[[str], List[str]]] = None) -> Iterator[str]:
     """build_fm_index.py:52-97: the cleaned passage texts, in file order;
     ``labels`` receives each kept passage's id."""
+    if tokenize and word_tokenize is None:
+        raise RuntimeError("--tokenize needs a word tokenizer (spacy's English, build_fm_index.py:148-154)")
+    rules = PassageRules(include_title, delim, lowercase, word_tokenize if tokenize else None)
     with open(input_path, "r", 2 ** 16) as f:
-        if format == "dpr":
-            next(f)
-            rows = csv.reader(f, delimiter="\t", quotechar='"')
-            pieces = ((pp[0], pp[2], pp[1]) for pp in rows if len(pp) == 3)
-        elif format == "kilt":
-            lines = (line.strip() for line in f)
-            split = (line.split("\t", 2) for line in lines)
-            pieces = ((pp[0], pp[1], pp[2]) for pp in split if len(pp) == 3)
-        else:
-            raise ValueError(f"unknown format {format!r}")
-        for idx, title, text in pieces:
-            idx = idx.strip()
-            title = title.strip()
-            text = re.sub(r"\s+", " ", text)
-            text = _fix_text(text)
-            text = text.replace("BULLET::::", "")
-            text = text.replace("SECTION::::", "")
-            text = text.strip()
-            if not text:
-                continue
-            if tokenize:
-                if word_tokenize is None:
-                    raise RuntimeError("--tokenize needs a word tokenizer (spacy's English, build_fm_index.py:148-154)")
-                title = " ".join(word_tokenize(title))
-                text = " ".join(word_tokenize(text))
-            title = f"{title} {delim}"
-            if include_title and title:
-                text = f"{title} {text}"
-            if lowercase:
-                text = text.lower()
-            labels.append(idx)
-            yield text
+        for pid, title, text in read_records(f, format):
+            cleaned = clean_passage(title, text, rules)
+            if cleaned is not None:
+                labels.append(pid.strip())
+                yield cleaned
 
 
-# -- tokenization (build_fm_index.py:25-50), one tokenizer per worker ---------
-_tokenizer = None
+# -- tokenization (build_fm_index.py:25-50): one tokenizer per pool worker ----
+_worker_tokenizer = None
 
 
 def init_worker(model_name: Optional[str]) -> None:
-    global _tokenizer
+    """Pool initializer: load the worker's tokenizer (local files only)."""
+    global _worker_tokenizer
     if model_name is None:
         raise RuntimeError("the reference's default tokenizer is fairseq BART from torch.hub, which needs the "
                            "network; pass --hf_model <local tokenizer path or cached name>")
     from transformers import AutoTokenizer
 
-    _tokenizer = AutoTokenizer.from_pretrained(model_name, use_fast=False)
+    _worker_tokenizer = AutoTokenizer.from_pretrained(model_name, use_fast=False)
+
+
+def encode_passage(tokenizer, text: str, bart: bool = False) -> List[int]:
+    """Token ids of one passage: ``"Paraphrase: "`` + text (a leading space
+    first for BART vocabularies), no special tokens, then eos
+    (build_fm_index.py:40-48)."""
+    prompt = "Paraphrase: " + (" " if bart else "") + text.strip()
+    target = getattr(tokenizer, "as_target_tokenizer", None)
+    with (target() if target is not None else contextlib.nullcontext()):
+        ids = tokenizer(prompt, add_special_tokens=False)["input_ids"]
+    return [*ids, tokenizer.eos_token_id]
 
 
 def process(line: str, model_name: Optional[str]) -> List[int]:
-    is_bart = model_name is not None and "bart" in model_name
-    line = line.strip()
-    if is_bart:
-        line = " " + line
-    ctx = getattr(_tokenizer, "as_target_tokenizer", None)
-    with (ctx() if ctx is not None else contextlib.nullcontext()):
-        line = "Paraphrase: " + line
-        return list(_tokenizer(line, add_special_tokens=False)["input_ids"]) + [_tokenizer.eos_token_id]
+    """The pool's map function (build_fm_index.py:37)."""
+    return encode_passage(_worker_tokenizer, line, bart=model_name is not None and "bart" in model_name)
 
 
 class CorpusBuffer:

@@ -51,6 +51,38 @@ def test_preprocess_dpr(tmp_path):
     assert labels == ["10", "11"]
 
 
+def test_clean_passage_edges(tmp_path):
+    from fmidx.build_index import PassageRules, clean_passage
+
+    # an empty title still contributes "<title> <delim> " (build_fm_index.py:87-90)
+    assert clean_passage("  ", "x\n y", PassageRules(include_title=True)) == " @@ x y"
+    assert clean_passage("T", "BULLET:::: SECTION::::", PassageRules(include_title=True)) is None
+    split = PassageRules(include_title=True, delim="|", word_tokenize=lambda s: s.replace(",", " , ").split())
+    assert clean_passage("A,B", "c,d  e", split) == "A , B | c , d e"
+    # --tokenize without a word tokenizer is refused before the file is read
+    with pytest.raises(RuntimeError):
+        list(preprocess_file(str(tmp_path / "absent.tsv"), [], "kilt", tokenize=True))
+    with pytest.raises(ValueError):
+        list(preprocess_file(_write(tmp_path, "x.tsv", KILT), [], "csv"))
+
+
+def test_encode_passage_prompt():
+    from fmidx.build_index import encode_passage
+
+    class Tok:                                   # records the prompt; ids = its bytes
+        eos_token_id = 2
+        seen = []
+
+        def __call__(self, text, add_special_tokens):
+            assert add_special_tokens is False
+            self.seen.append(text)
+            return {"input_ids": list(text.encode())}
+
+    tok = Tok()
+    assert encode_passage(tok, "  hi ") == list(b"Paraphrase: hi") + [2]
+    assert encode_passage(tok, "hi", bart=True) == list(b"Paraphrase:  hi") + [2]
+
+
 def test_corpus_buffer_matches_encoding():
     rng = np.random.default_rng(3)
     docs = [rng.integers(-9, 300000, size=int(rng.integers(0, 50))).tolist() for _ in range(300)]
