@@ -16,9 +16,14 @@ uniform random id; a row whose range is empty restarts as a fresh sequence
 (empty pattern = full range); row 0 is an empty-pattern row, row 1 an
 eos-terminated (empty-range) row.
 
-Multi-GPU (--gpus N under torch.distributed.run): replicas -- every rank holds
-the full index and decodes its own B rows (weak scaling, no data-path
-collective); value = N*B*K / max-over-ranks time.
+Multi-GPU (--gpus N): replicas -- every rank holds the full index and decodes
+its own B rows (weak scaling, no data-path collective); value = N*B*K /
+max-over-ranks time.  Launched either by torch.distributed.run (WORLD_SIZE in
+the environment) or plainly as ``python bench.py --gpus N``: then this process
+never touches the GPU -- it starts N fresh child processes (one per GPU, RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set), waits for
+them and exits with the worst exit code (spawn_ranks).  After the replica
+run, N > 1 also runs the doc-range sharded config (C4) over RCCL.
 """
 from __future__ import annotations
 
@@ -54,6 +59,61 @@ def lib_sha16():
 
     with open(os.path.join(PKG, "fmidx", "libfmidx.so"), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, cmd: list, grace_s: float = 30.0, env: dict | None = None) -> int:
+    """One fresh child process per GPU running ``cmd`` with the torchrun-style
+    rank environment; returns the worst exit code.  The caller must not have
+    touched the GPU (no HIP call, no torch.cuda.is_available()): the children
+    are started as new programs, never by exec of this one.  When a child fails,
+    the others get ``grace_s`` to finish on their own (a rank stuck in a
+    collective with a dead peer would otherwise wait for the RCCL timeout), then
+    are terminated by PID.  Returns the first failing rank's code (the cause),
+    not the SIGTERM of the peers stopped after it."""
+    import signal
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(n):
+        e = dict(os.environ if env is None else env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                  "FMIDX_BENCH_LAUNCHER": "spawn"})
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")      # RCCL on this host needs dmabuf IPC
+        procs.append(subprocess.Popen(cmd, env=e))
+    codes = [None] * n
+    fail_at, first_bad = None, 0
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+                if codes[i] not in (None, 0) and fail_at is None:
+                    fail_at, first_bad = time.time(), codes[i]
+                    print(f"[bench] rank {i} exited with {codes[i]}", file=sys.stderr, flush=True)
+        if fail_at is not None and time.time() - fail_at > grace_s:
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    print(f"[bench] terminating rank {i} (pid {p.pid})", file=sys.stderr, flush=True)
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.2)
+    return first_bad or next((c for c in codes if c), 0)
 
 
 def log(*a):
@@ -674,18 +734,38 @@ def main():
                     help="after the timed region, launch the K timed decode steps and the K standalone LF "
                          "steps once more eagerly (no graph) so PMC counters can be collected per dispatch "
                          "(tools/pmc_traffic.sh)")
+    ap.add_argument("--dist-timeout", type=float, default=float(os.environ.get("FMIDX_DIST_TIMEOUT", 600)),
+                    help="seconds before a stuck RCCL collective aborts the rank (N > 1)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: this process only launches the ranks and never
+        # touches the GPU (device_count does not initialise it on this image)
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"[bench] --gpus {args.gpus} but only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+            sys.exit(2)
+        rc = spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+        sys.exit(rc if rc >= 0 else 128 - rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    launcher = os.environ.get("FMIDX_BENCH_LAUNCHER", "torchrun" if "WORLD_SIZE" in os.environ else "single")
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE {world} != --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
     # one process per GPU: bind the device BEFORE the RCCL communicator exists
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rccl_world = 1
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=args.dist_timeout))
+        rccl_world = dist.get_world_size()
+        assert rccl_world == args.gpus, f"RCCL world {rccl_world} != --gpus {args.gpus}"
     n_tokens = int(args.tokens)
     B, V, K, W = args.batch, args.vocab, args.steps, max(1, args.warmup)
 
@@ -929,6 +1009,8 @@ def main():
         "value": value,
         "unit": "masks/s",
         "n_gpus": world,
+        "rccl_world": rccl_world,
+        "launcher": launcher,
         "steps": K,
         "warmup": W,
         "ms_per_step": step_ms,

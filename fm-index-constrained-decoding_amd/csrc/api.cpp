@@ -980,6 +980,7 @@ int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t wsb = fmidx::lf_ws_bytes(m);
   if (!wsb) return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s);
+  std::lock_guard<std::mutex> lk(h->mu);     // the workspace and its event are shared (ws_acquire)
   if (ws_acquire(h, s, wsb)) return -1;
   const int rc = fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s,
                                        h->idx.ws);

@@ -270,7 +270,18 @@ int device_samples_from_isa(Index* h, const uint64_t* d_isa, uint64_t nisa, hipS
     cleanup();
     return -1;
   }
-  FM_HIP(hipMemcpyAsync(isa, d_isa, nisa * 8, hipMemcpyDeviceToDevice, s));
+  // every HIP failure below frees what this function allocated (ISA_CK), the
+  // sort's temporary included
+#define ISA_CK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      ::fmidx::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+      cleanup();                                                                          \
+      return -1;                                                                          \
+    }                                                                                     \
+  } while (0)
+  ISA_CK(hipMemcpyAsync(isa, d_isa, nisa * 8, hipMemcpyDeviceToDevice, s));
   uint64_t bad = 0;
   if (count_where(IsaOutOfRange{isa, n}, nisa, d_cnt, bad, s) || bad) {
     if (bad) set_error("ISA samples: %llu rows out of range (n = %llu)", (unsigned long long)bad, (unsigned long long)n);
@@ -291,9 +302,9 @@ int device_samples_from_isa(Index* h, const uint64_t* d_isa, uint64_t nisa, hipS
     size_t tb = 0;
     int bits = 1;
     while (bits < 64 && (n - 1) >> bits) ++bits;
-    FM_HIP(rocprim::radix_sort_pairs(nullptr, tb, rows, rows2, seq, samp, (size_t)nsamp, 0, bits, s));
+    ISA_CK(rocprim::radix_sort_pairs(nullptr, tb, rows, rows2, seq, samp, (size_t)nsamp, 0, bits, s));
     void* t = nullptr;
-    FM_HIP(hipMalloc(&t, tb ? tb : 1));
+    ISA_CK(hipMalloc(&t, tb ? tb : 1));
     hipError_t e = hipSuccess;
     k_iota_u32<<<(unsigned)((nsamp + kThreads - 1) / kThreads), kThreads, 0, s>>>(seq, nsamp);
     e = hipGetLastError();
@@ -310,15 +321,16 @@ int device_samples_from_isa(Index* h, const uint64_t* d_isa, uint64_t nisa, hipS
     cleanup();
     return -1;
   }
-  FM_HIP(hipMemsetAsync(mark, 0, nwords * 8, s));
+  ISA_CK(hipMemsetAsync(mark, 0, nwords * 8, s));
   k_mark_from_sorted<<<(unsigned)((nsamp + kThreads - 1) / kThreads), kThreads, 0, s>>>(rows2, nsamp, mark);
   k_mark_blocks<<<(unsigned)((nblocks + kThreads - 1) / kThreads), kThreads, 0, s>>>(mark, nwords, nblocks, tmp);
-  FM_HIP(hipGetLastError());
+  ISA_CK(hipGetLastError());
   if (exclusive_scan_u64(tmp, cnt, nblocks, s, nullptr)) {
     cleanup();
     return -1;
   }
-  FM_HIP(hipStreamSynchronize(s));
+  ISA_CK(hipStreamSynchronize(s));
+#undef ISA_CK
   for (void* p : {(void*)h->mark, (void*)h->mark_cnt, (void*)h->sa_samp, (void*)h->isa_samp})
     if (p) (void)hipFree(p);
   h->mark = mark;

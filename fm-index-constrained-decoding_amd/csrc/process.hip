@@ -333,6 +333,22 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
     set_error("processor step: ids copy row of %llu < %llu", (unsigned long long)copy_ld, (unsigned long long)L);
     return -1;
   }
+  // k_prep reads prev_ids (and ids) in the same kernel that writes ids_copy, all
+  // __restrict__: a copy buffer overlapping either would race with those reads
+  if (ids_copy && B) {
+    auto overlaps = [&](const int64_t* p, uint64_t rows, uint64_t pld, uint64_t cols) {
+      if (!p || !rows) return false;
+      const char* a0 = reinterpret_cast<const char*>(ids_copy);
+      const char* a1 = reinterpret_cast<const char*>(ids_copy + (B - 1) * copy_ld + L);
+      const char* b0 = reinterpret_cast<const char*>(p);
+      const char* b1 = reinterpret_cast<const char*>(p + (rows - 1) * pld + cols);
+      return a0 < b1 && b0 < a1;
+    };
+    if (overlaps(prev_ids, prev_B, prev_ld, prev_ld) || overlaps(ids, B, ld, L)) {
+      set_error("processor step: ids_copy must not overlap prev_ids or ids");
+      return -1;
+    }
+  }
   if (init_status) {   // a caller that never reads the status (fm_processor_call without a host copy) skips this
     FM_HIP(hipMemsetAsync(status, 0, 16, s));
     FM_HIP(hipMemsetAsync(status + 1, 0xFF, 4, s));

@@ -168,6 +168,9 @@ class _DeviceStep:
         its inputs -- no end marker to find, every boost 0 -- so the device
         path always holds and the host neither copies nor waits for it: the call
         only enqueues work (vLLM V0 calls one clone per sequence per step)."""
+        if not wait and not (cfg.flags & PREP_HARD):
+            raise ValueError("wait=False is only valid for hard-mask (PREP_HARD) calls: a soft call's status "
+                             "(end markers, boost overflow) depends on its input and must be read")
         dev = self.dev
         ids = input_ids if (input_ids.device == dev and input_ids.dtype == torch.int64
                             and input_ids.is_contiguous()) else input_ids.to(dev, torch.int64).contiguous()
@@ -559,7 +562,9 @@ class CausalIndexBasedLogitsProcessor:
 
     def _process(self, input_ids, scores):
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype), wait=False)
+            # a soft variant: its status (end markers, boost overflow) depends on the
+            # input, so the call waits for it (wait=False is for PREP_HARD only)
+            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
             if out is not None:
                 return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))

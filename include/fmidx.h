@@ -353,7 +353,7 @@ typedef struct fm_processor_args {
   uint64_t V, ld_scores, ld_out;
   const uint32_t* unigram_bits;
   int64_t eos;
-  int64_t* ids_copy;           /* [B][copy_ld] or null */
+  int64_t* ids_copy;           /* [B][copy_ld] or null; must not overlap prev_ids or ids (rejected) */
   uint64_t copy_ld;
   uint32_t* status_host;       /* pinned [4] or null */
   void* status_event;          /* hipEvent_t recorded after the status copy, or null */

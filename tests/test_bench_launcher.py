@@ -1,0 +1,86 @@
+"""bench.py's N-rank launcher (``python bench.py --gpus N`` without torchrun):
+one child per GPU with the torchrun rank environment, worst exit code
+returned, stuck peers of a failed rank terminated.  The worker is a stub
+script, so no GPU is touched (CPU test)."""
+import json
+import os
+import sys
+import textwrap
+import time
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+
+def _stub(tmp_path, body):
+    p = tmp_path / "stub.py"
+    p.write_text(textwrap.dedent(body))
+    return [sys.executable, str(p)]
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_spawn_sets_rank_environment(tmp_path, n):
+    cmd = _stub(tmp_path, f"""
+        import json, os
+        keys = ["RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                "FMIDX_BENCH_LAUNCHER", "HSA_ENABLE_IPC_MODE_LEGACY"]
+        with open(os.path.join({str(tmp_path)!r}, "rank%s.json" % os.environ["RANK"]), "w") as f:
+            json.dump({{k: os.environ.get(k) for k in keys}}, f)
+    """)
+    assert bench.spawn_ranks(n, cmd) == 0
+    envs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(n)]
+    assert [int(e["RANK"]) for e in envs] == list(range(n))
+    assert [int(e["LOCAL_RANK"]) for e in envs] == list(range(n))
+    assert {e["WORLD_SIZE"] for e in envs} == {str(n)}
+    assert {e["LOCAL_WORLD_SIZE"] for e in envs} == {str(n)}
+    assert {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1 and int(envs[0]["MASTER_PORT"]) > 0
+    assert {e["FMIDX_BENCH_LAUNCHER"] for e in envs} == {"spawn"}
+    assert {e["HSA_ENABLE_IPC_MODE_LEGACY"] for e in envs} == {"0"}
+
+
+def test_spawn_children_rendezvous_over_gloo(tmp_path):
+    """The environment is enough for init_process_group's env:// rendezvous:
+    two children form a world of 2 and all-reduce (gloo, CPU)."""
+    cmd = _stub(tmp_path, f"""
+        import os, torch, torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.tensor([int(os.environ["RANK"]) + 1])
+        dist.all_reduce(t)
+        assert dist.get_world_size() == 2 and int(t) == 3, (dist.get_world_size(), int(t))
+        open(os.path.join({str(tmp_path)!r}, "ok%d" % dist.get_rank()), "w").close()
+        dist.destroy_process_group()
+    """)
+    assert bench.spawn_ranks(2, cmd) == 0
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
+def test_spawn_failure_terminates_stuck_peers(tmp_path):
+    """Rank 1 fails; rank 0 (stuck, as in a collective with a dead peer) is
+    terminated after the grace period and the failure code is returned."""
+    cmd = _stub(tmp_path, """
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(600)
+    """)
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, cmd, grace_s=1.0)
+    assert rc == 3
+    assert time.time() - t0 < 60
+
+
+def test_bench_refuses_more_gpus_than_visible(tmp_path):
+    """`bench.py --gpus N` on a machine with fewer GPUs exits 2 before any
+    rank starts (this container has none)."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "GPU(s) visible" in r.stderr
