@@ -439,13 +439,17 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     replica run at N > 1.  The trace (tokens + initial patterns) and the
     reference masks of its last step come from the replica (unsharded) index;
     then every rank indexes its doc range + halo (one slice of T', built on the
-    device), decodes all B rows against it into bit-packed rows, and a step is:
-    fused LF + packed mask (fm_decode_step_batch) + RCCL all_gather of the
-    packed rows + one fused OR/unpack pass (fm_or_bits) to the uint8 [B, V]
-    mask of the whole corpus.  The last step's mask must equal the replica's."""
+    device) and decodes all B rows against it into bit-packed rows.  A step is
+    the fused LF + packed mask (fm_decode_step_batch), then the exchange:
+    "sparse" (the default) -- fm_shard_pack (per row the shard's BWT slice when
+    smaller than the bitmap, else the bitmap), an all_gather of the payload
+    sizes (read on the host), an all_gather of the payloads and ONE fused OR /
+    scatter / unpack pass (fm_shard_or_rows); "dense" -- RCCL all_gather of
+    every row's packed bitmap and fm_or_bits.  Both are timed over the same K
+    steps; the last step's mask of each must equal the replica's."""
     import torch.distributed as dist
 
-    from fmidx.sharding import or_bits, shard_text_device
+    from fmidx.sharding import gather_payloads, or_bits, or_payloads, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
     S = W + K
@@ -475,51 +479,73 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     assert max(lens) + S <= halo - 1, "trace patterns would outgrow the halo"
     offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
     toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
-    lo = torch.zeros(B, dtype=torch.int64, device=dev)
-    hi = torch.zeros(B, dtype=torch.int64, device=dev)
-    ix.backward_search_batch(toks, offs, SHIFT, lo, hi)
+    lo0 = torch.zeros(B, dtype=torch.int64, device=dev)
+    hi0 = torch.zeros(B, dtype=torch.int64, device=dev)
+    ix.backward_search_batch(toks, offs, SHIFT, lo0, hi0)
     Wd = (V + 31) // 32
     mine = torch.empty((B, Wd), dtype=torch.int32, device=dev)
     parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
     out = torch.empty((B, V), dtype=torch.uint8, device=dev)
-    bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+    payload = None
+    words_seen = []
 
-    def step(i, k):
-        src, dst = bufs[k % 2], bufs[(k + 1) % 2]
-        ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1],
-                       packed=True)
-        dist.all_gather_into_tensor(parts, mine)
-        or_bits(parts, V, out=out)
+    def run(mode):
+        nonlocal payload
+        lo, hi = lo0.clone(), hi0.clone()
+        bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
 
-    for i in range(W):
-        step(i, i)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    a_ev = torch.cuda.Event(enable_timing=True)
-    b_ev = torch.cuda.Event(enable_timing=True)
-    a_ev.record()
-    for i in range(W, S):
-        step(i, i)
-    b_ev.record()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    ms = a_ev.elapsed_time(b_ev) / K
-    t = torch.tensor([ms], device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms = float(t.item())
-    exact = bool(torch.equal(out, ref))
-    ok = torch.tensor([1 if exact else 0], device=dev)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        def step(i):
+            nonlocal payload
+            src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+            ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1],
+                           packed=True)
+            if mode == "dense":
+                dist.all_gather_into_tensor(parts, mine)
+                or_bits(parts, V, out=out)
+            else:
+                payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
+                pp, words = gather_payloads(payload, None)
+                if i >= W:
+                    words_seen.append(words)
+                or_payloads(pp, B, V, SHIFT, out=out)
+
+        for i in range(W):
+            step(i)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        a_ev = torch.cuda.Event(enable_timing=True)
+        b_ev = torch.cuda.Event(enable_timing=True)
+        a_ev.record()
+        for i in range(W, S):
+            step(i)
+        b_ev.record()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([a_ev.elapsed_time(b_ev) / K], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ok = torch.tensor([1 if bool(torch.equal(out, ref)) else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        return float(t.item()), bool(ok.item())
+
+    ms_dense, exact_dense = run("dense")
+    ms, exact = run("sparse")
     st = ix.stats()
+    per_step = [sum(w) for w in words_seen]
     return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": B / (ms / 1e3),
             "unit": "masks/s", "ms_per_step": ms, "scaling": "strong", "shards": world, "halo": halo,
             "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": st["bwt_bytes"] // 4,
             "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
-            "masks_equal_unsharded": bool(ok.item()),
-            "step": "fused LF + packed mask, RCCL all_gather of packed rows (4 B x ceil(V/32) per row), "
-                    "fused OR + unpack (fm_or_bits) to uint8 [B, V]; eager launches"}
+            "masks_equal_unsharded": exact,
+            "exchange": "sparse: per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",
+            "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
+            "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
+                                                if words_seen else None),
+            "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
+                      "exchange_bytes_per_step": world * B * Wd * 4},
+            "step": "fused LF + packed mask; sparse payload (fm_shard_pack), all_gather of sizes (host read) + "
+                    "payloads, fused OR / scatter / unpack (fm_shard_or_rows) to uint8 [B, V]; eager launches"}
 
 
 COMPACT_ENV = {"FMIDX_TRANS": "1", "FMIDX_LF_E": "0", "FMIDX_PROBE_FIRST": "0"}
@@ -544,7 +570,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
     the same way and checked against the replica's uint8 mask.  The exchange
     itself (all_gather of 8 x B x V/8 bytes over xGMI) cannot run on one GPU;
     ``predicted_step_us`` adds a stated model of it."""
-    from fmidx.sharding import or_bits, shard_text_device
+    from fmidx.sharding import or_bits, or_payloads, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()
     S = W + K
@@ -623,7 +649,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
         Wd = (V + 31) // 32
         parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
-        shards = []
+        shards, last_pay, pay_words = [], [], []
         for r in range(world):
             t0 = time.time()
             t_r, (a, b) = shard_text_device(text, beg, world, r, halo)
@@ -655,10 +681,31 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
             lo.copy_(s_lo)
             hi.copy_(s_hi)
             cold = replay(g, True) / K * 1e3          # leaves parts[r] = this shard's last-step rows
+            fin_lo, fin_hi = bufs[K % 2][0].clone(), bufs[K % 2][1].clone()
+            # sparse exchange: this shard's payload of every timed step (sizes), the last one kept
+            pay = ix.shard_pack(fin_lo, fin_hi, parts[r], V)
+            g_pack = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_pack):
+                for _ in range(K):
+                    ix.shard_pack(fin_lo, fin_hi, parts[r], V, payload=pay)
+            pack_cold = replay(g_pack, True) / K * 1e3
+            last_pay.append(pay[:int(pay[0].item())].clone())
+            lo.copy_(s_lo)
+            hi.copy_(s_hi)
+            scratch = torch.empty_like(parts[r])
+            sizes = []
+            for i in range(K):
+                src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+                ix.decode_step(tokens[W + i], src[0], src[1], scratch, V, SHIFT, reset_below=0,
+                               lo_out=dst[0], hi_out=dst[1], packed=True)
+                sizes.append(int(ix.shard_pack(dst[0], dst[1], scratch, V, payload=pay)[0].item()))
+            pay_words.append(sizes)
+            del g_pack, pay, scratch
             st = ix.stats()
             shards.append({"docs": [int(a), int(b)], "rows": int(rows), "device_bytes": int(st["device_bytes"]),
                            "build_s": round(build_s, 2), "cold_us_per_step": cold,
-                           "warm_us_per_step": float(np.median(warm))})
+                           "warm_us_per_step": float(np.median(warm)), "pack_cold_us": pack_cold,
+                           "payload_bytes_per_step_median": 4.0 * float(np.median(sizes))})
             mem_log(f"c4 shard {r} built", dev)
             log(f"c4 shard {r}: rows {rows}, build {build_s:.1f}s, step cold {cold:.1f}us warm {np.median(warm):.1f}us")
             del g, ix, bufs, lo, hi, s_lo, s_hi
@@ -678,6 +725,26 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         or_cold = replay(g_or, True) / K * 1e3
         exact = exact and bool(torch.equal(out, ref))
         del pk, g_or
+        # the sparse exchange's OR / scatter / unpack over the 8 last-step payloads (padded to the
+        # largest, as the all_gather delivers them), timed the same way
+        m = max(p.numel() for p in last_pay)
+        sp = torch.zeros((world, m), dtype=torch.int32, device=dev)
+        for r, p in enumerate(last_pay):
+            sp[r, :p.numel()] = p
+        out.zero_()
+        or_payloads(sp, B, V, SHIFT, out=out)
+        exact_sparse = bool(torch.equal(out, ref))
+        spk = sp.unsqueeze(0).expand(K, *sp.shape).contiguous()
+        g_sp = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_sp):
+            for i in range(K):
+                or_payloads(spk[i], B, V, SHIFT, out=out)
+        sp_warm = float(np.median([replay(g_sp, False) for _ in range(3)])) / K * 1e3
+        sp_cold = replay(g_sp, True) / K * 1e3
+        exact_sparse = exact_sparse and bool(torch.equal(out, ref))
+        del spk, g_sp, sp
+        step_words = [sum(w[i] for w in pay_words) for i in range(K)]
+        step_max = [max(w[i] for w in pay_words) for i in range(K)]
         # exchange model: every rank receives (world - 1) packed slices of B x 4 ceil(V/32)
         # bytes over its 7 point-to-point xGMI links (~153 GB/s each, direct: one slice per
         # link in parallel) plus a ~15 us collective latency; a ring (one link, 7 hops) is the
@@ -686,7 +753,24 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         ag_direct = slice_b / 153e9 * 1e6 + 15.0
         ag_ring = (world - 1) * slice_b / 153e9 * 1e6 + 15.0
         slow = max(s["cold_us_per_step"] for s in shards)
+        pack = max(s["pack_cold_us"] for s in shards)
+        sp_slice = 4.0 * float(np.median(step_max))          # the largest rank's payload: what every link carries
+        ag_sp_direct = sp_slice / 153e9 * 1e6 + 15.0
+        ag_sp_ring = (world - 1) * sp_slice / 153e9 * 1e6 + 15.0
+        sizes_us = 15.0                                       # the all_gather of the sizes + the host read
+        sparse = {"masks_equal_unsharded": exact_sparse, "or_rows_cold_us": sp_cold, "or_rows_warm_us": sp_warm,
+                  "pack_cold_us_slowest_shard": pack,
+                  "payload_bytes_per_step_all_ranks_median": 4.0 * float(np.median(step_words)),
+                  "payload_bytes_per_step_largest_rank_median": sp_slice,
+                  "dense_bytes_per_step_all_ranks": world * slice_b,
+                  "allgather_model_us": {"direct_7_links": ag_sp_direct, "ring": ag_sp_ring,
+                                         "sizes_exchange_us_assumed": sizes_us},
+                  "predicted_step_us": {"direct": slow + pack + sizes_us + ag_sp_direct + sp_cold,
+                                        "ring": slow + pack + sizes_us + ag_sp_ring + sp_cold},
+                  "note": "per row the shard's BWT slice when hi - lo < ceil(V/32), else its bitmap "
+                          "(fm_shard_pack); OR / scatter / unpack of the 8 payloads (fm_shard_or_rows)"}
         return {"shards": world, "halo": halo, "global_batch": B, "steps": K, "per_shard": shards,
+                "sparse_exchange": sparse,
                 "slowest_shard_cold_us": slow, "or_pass_cold_us": or_cold, "or_pass_warm_us": or_warm,
                 "or_pass_bytes": world * slice_b + B * V,
                 "or_pass_GBps_cold": (world * slice_b + B * V) / (or_cold * 1e-6) / 1e9,

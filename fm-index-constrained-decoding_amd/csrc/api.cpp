@@ -1191,6 +1191,35 @@ int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, u
   FM_API_END
 }
 
+int fm_shard_payload_capacity(uint64_t B, uint64_t vocab, uint64_t* words) {
+  FM_API_BEGIN
+  if (!words) {
+    set_error("null out");
+    return -1;
+  }
+  *words = fmidx::shard_payload_capacity(B, vocab);
+  return 0;
+  FM_API_END
+}
+
+int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
+                  uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_shard_pack(h->idx.view, d_lo, d_hi, B, d_bits, ldw, vocab, d_payload, cap_words,
+                                  reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
+                     int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
+  FM_API_BEGIN
+  return fmidx::launch_shard_or_rows(d_parts, nparts, part_stride, B, vocab, shift, d_out, ld_out, unpack,
+                                     reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream) {
   FM_API_BEGIN

@@ -194,4 +194,264 @@ int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride,
   return 0;
 }
 
+
+// ---- the sparse exchange (C4): per row either the shard's BWT slice or its bitmap
+//
+// A rank's payload (uint32 words, every offset a multiple of 4 words):
+//   [0] total words (a multiple of 4)   [1] B   [2] words per bitmap row W   [3] kPayloadMagic
+//   [4, 4 + B)        desc[b] = count | (dense << 31)
+//   [4 + B, 4 + 2B)   off[b]  = word offset of row b's data in this payload
+//   data: row b's `count` words at off[b] (zero-padded to a multiple of 4):
+//         dense  -- the W words of its allowed-token bitmap (the decode step's packed row)
+//         sparse -- BWT[lo, hi) of the shard (T' symbols; token = symbol - shift when in [0, V)),
+//                   chosen when hi - lo < W, i.e. when the slice is smaller than the bitmap.
+// Most decode rows are narrow on a shard (median width 1 at C3), so a payload is a few
+// hundred KB where the packed rows of every row are B * W * 4 bytes (4.1 MB at B = 256).
+namespace {
+
+constexpr uint32_t kPayloadMagic = 0x58534D46u;   // "FMSX"
+
+__host__ __device__ __forceinline__ uint64_t payload_header_words(uint64_t B) { return 4 + ((2 * B + 3) & ~3ull); }
+
+// One workgroup per row, one launch: the workgroup sums the padded sizes of
+// the rows before its own (every thread loads a few (lo, hi) pairs -- B * 16
+// bytes, L2-resident after the first workgroup -- then a wave reduction), so
+// no separate scan launch precedes the copy: two dependent round trips
+// (the states, then the row's source) in all.  Workgroup B - 1 writes the
+// header words, workgroup 0 zeroes the header's padding.
+constexpr int kPackRowThreads = 256;
+
+__device__ __forceinline__ uint64_t pack_row_words(uint64_t l, uint64_t h, uint64_t n, uint32_t W, uint32_t& desc) {
+  h = min(h, n);                                       // a state past the BWT reads none of it
+  const uint64_t w = h > l ? h - l : 0;
+  const bool dense = w >= W;
+  const uint64_t count = dense ? W : w;
+  desc = (uint32_t)count | (dense ? 0x80000000u : 0u);
+  return (count + 3) & ~3ull;
+}
+
+__global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint64_t* __restrict__ lo,
+                                                          const uint64_t* __restrict__ hi,
+                                                          const uint32_t* __restrict__ bits, uint64_t ldw,
+                                                          uint64_t B, uint32_t W, uint32_t* __restrict__ pay) {
+  __shared__ uint64_t s_part[kPackRowThreads / 64];
+  const uint64_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint64_t H = payload_header_words(B);
+  if (B == 0) {   // the empty payload: its header alone
+    if (t < H) pay[t] = t == 0 ? (uint32_t)H : t == 2 ? W : t == 3 ? kPayloadMagic : 0u;
+    return;
+  }
+  // the padded sizes of rows [0, b): every load issued before any is used
+  uint64_t before = 0;
+  for (uint64_t j0 = 0; j0 < b; j0 += 4 * kPackRowThreads) {
+    uint64_t l[4], h[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t j = min(j0 + u * kPackRowThreads + t, B - 1);
+      l[u] = lo[j];
+      h[u] = hi[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint32_t d;
+      const uint64_t words = pack_row_words(l[u], h[u], v.n, W, d);
+      before += (j0 + u * kPackRowThreads + t < b) ? words : 0;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o);
+  if (lane == 0) s_part[wv] = before;
+  const uint64_t l0 = lo[b], h0 = hi[b];
+  uint32_t desc;
+  const uint64_t words = pack_row_words(l0, h0, v.n, W, desc);
+  __syncthreads();
+  uint64_t off = H;
+#pragma unroll
+  for (int k = 0; k < kPackRowThreads / 64; ++k) off += s_part[k];
+  if (t == 0) {
+    pay[4 + b] = desc;
+    pay[4 + B + b] = (uint32_t)off;
+    if (b == B - 1) {
+      pay[0] = (uint32_t)(off + words);
+      pay[1] = (uint32_t)B;
+      pay[2] = W;
+      pay[3] = kPayloadMagic;
+    }
+  }
+  if (b == 0)
+    for (uint64_t i = 4 + 2 * B + t; i < H; i += kPackRowThreads) pay[i] = 0u;
+  const uint32_t count = desc & 0x7FFFFFFFu;
+  const uint32_t* src = (desc >> 31) ? bits + b * ldw : v.bwt + min(l0, v.n - 1);
+  uint32_t* dst = pay + off;
+  // up to 8 loads per thread in flight before the stores (W <= 8192 words: one pass)
+  for (uint32_t i0 = 0; i0 < (uint32_t)words; i0 += 8 * kPackRowThreads) {
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + u * kPackRowThreads + t;
+      x[u] = src[min(i, count ? count - 1 : 0u)];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + u * kPackRowThreads + t;
+      if (i < (uint32_t)words) dst[i] = i < count ? x[u] : 0u;
+    }
+  }
+}
+
+// One workgroup (1024 threads) per row.  Every part's (desc, off) for the row
+// is staged in LDS first (one round trip); then the dense parts' words are
+// loaded four parts at a time for all of a thread's words (thread t owns
+// words t + 1024 k) and ORed in registers; then every sparse symbol of every
+// part -- one flat index space over the parts' lists, so a thread's loads do
+// not wait part by part -- is set with an LDS atomic; then the row is emitted
+// as uint8 (16 tokens per lane-chunk, 16-B write-through stores) or as words.
+constexpr int kOrRowThreads = 1024;
+constexpr int kOrRowMaxWords = 8 * kOrRowThreads;   // V <= 262144
+constexpr int kOrMaxParts = 64;
+
+__global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts, uint32_t nparts,
+                                                            uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
+                                                            int64_t shift, void* __restrict__ out, uint64_t ld,
+                                                            int unpack) {
+  extern __shared__ uint32_t s_bits[];   // [W]
+  __shared__ uint32_t s_desc[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
+  __shared__ uint32_t s_nd;
+  const uint64_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  if (t < nparts) {
+    const uint32_t* pp = parts + (uint64_t)t * stride;
+    s_desc[t] = pp[4 + b];
+    s_off[t] = pp[4 + B + b];
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t nd = 0, run = 0;
+    for (uint32_t p = 0; p < nparts; ++p) {
+      s_pre[p] = run;
+      if (s_desc[p] >> 31) s_dense[nd++] = p;
+      else run += s_desc[p];
+    }
+    s_pre[nparts] = run;
+    s_nd = nd;
+  }
+  __syncthreads();
+  const uint32_t nd = s_nd;
+  constexpr int kSlots = kOrRowMaxWords / kOrRowThreads;
+  uint32_t acc[kSlots];
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0u;
+  if (nd) {
+    for (uint32_t j0 = 0; j0 < nd; j0 += 4) {
+      const uint32_t* src[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
+        src[q] = parts + (uint64_t)p * stride + s_off[p];
+      }
+      uint32_t x[4][kSlots];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < kSlots; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < kSlots; ++k) acc[k] |= x[q][k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) {
+    const uint32_t w = t + k * kOrRowThreads;
+    if (w < W) s_bits[w] = acc[k];
+  }
+  __syncthreads();
+  const uint32_t total = s_pre[nparts];
+  for (uint32_t i0 = 0; i0 < total; i0 += 4 * kOrRowThreads) {
+    uint32_t sym[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = min(i0 + u * kOrRowThreads + t, total - 1);
+      uint32_t p = 0;                                   // the part whose list holds flat index i
+      for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
+        if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
+      while (p + 1 < nparts && s_pre[p + 1] <= i) ++p;    // parts with empty lists
+      sym[u] = parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t tok = (int64_t)sym[u] - shift;
+      if (i0 + u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+        atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+    }
+  }
+  __syncthreads();
+  if (!unpack) {
+    uint32_t* o = static_cast<uint32_t*>(out) + b * (ld / 4);
+    for (uint32_t w = t; w < W; w += kOrRowThreads) o[w] = s_bits[w];
+    return;
+  }
+  uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
+  __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
+  const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+  for (uint64_t c = t; 16 * c < vocab; c += kOrRowThreads) {   // 16-token chunk c
+    const uint64_t t0 = 16 * c;
+    const uint32_t bits16 = (s_bits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+    uint32_t q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = (((bits16 >> (4 * i)) & 0xFu) * 0x204081u) & 0x01010101u;
+    if (t0 + 16 <= vocab && aligned) {
+      or_v4u vv = {q[0], q[1], q[2], q[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(vv, r, (uint32_t)t0, 0, kOrStoreAux);
+    } else {
+      for (uint64_t i = 0; i < 16 && t0 + i < vocab; ++i) row[t0 + i] = (bits16 >> i) & 1u;
+    }
+  }
+}
+
+}  // namespace
+
+uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab) {
+  const uint64_t W = (vocab + 31) / 32;
+  return payload_header_words(B) + B * ((W + 3) & ~3ull);
+}
+
+int launch_shard_pack(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t B, const uint32_t* bits,
+                      uint64_t ldw, uint64_t vocab, uint32_t* pay, uint64_t cap, hipStream_t s) {
+  const uint64_t W = (vocab + 31) / 32;
+  if (!lo || !hi || !pay || (B && !bits) || ldw < W || B >= (1ull << 31) ||
+      W > (uint64_t)kOrRowMaxWords) {
+    set_error("shard_pack: bad arguments (B %llu, vocab %llu, ld %llu words)", (unsigned long long)B,
+              (unsigned long long)vocab, (unsigned long long)ldw);
+    return -1;
+  }
+  if (cap < shard_payload_capacity(B, vocab) || cap >= (1ull << 32)) {
+    set_error("shard_pack: payload of %llu words, %llu needed (< 2^32)", (unsigned long long)cap,
+              (unsigned long long)shard_payload_capacity(B, vocab));
+    return -1;
+  }
+  k_pack<<<(unsigned)(B ? B : 1), kPackRowThreads, 0, s>>>(v, lo, hi, bits, ldw, B, (uint32_t)W, pay);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride, uint64_t B, uint64_t vocab,
+                         int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s) {
+  const uint64_t W = (vocab + 31) / 32;
+  if (!parts || !out || !nparts || nparts > (uint64_t)kOrMaxParts || W > (uint64_t)kOrRowMaxWords ||
+      stride < payload_header_words(B) ||
+      (unpack ? ld < vocab : (ld < 4 * W || ld % 4))) {
+    set_error("shard_or_rows: bad arguments (parts %llu, stride %llu, vocab %llu, ld %llu)",
+              (unsigned long long)nparts, (unsigned long long)stride, (unsigned long long)vocab,
+              (unsigned long long)ld);
+    return -1;
+  }
+  if (B == 0) return 0;
+  k_or_rows<<<(unsigned)B, kOrRowThreads, W * 4, s>>>(parts, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift,
+                                                      out, ld, unpack);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace fmidx

@@ -64,6 +64,11 @@ SIGNATURES = {
                                   c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_processor_call": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "fm_shard_payload_capacity": (c_int, [c_uint64, c_uint64, u64p]),
+    "fm_shard_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p,
+                              c_uint64, c_void_p]),
+    "fm_shard_or_rows": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p, c_uint64,
+                                 c_int, c_void_p]),
     "fm_or_bits": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_void_p, c_uint64, c_int,
                             c_void_p]),
     "fm_probe_gather": (c_int, [c_void_p, c_uint64, c_int, c_uint64, c_uint32, c_void_p, c_void_p]),

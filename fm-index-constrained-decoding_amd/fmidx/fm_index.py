@@ -69,6 +69,13 @@ def _default_device() -> int:
     return 0
 
 
+def payload_capacity(B: int, vocab: int) -> int:
+    """uint32 words a sparse-exchange payload of B rows may need (fm_shard_payload_capacity)."""
+    out = c_uint64()
+    check(lib().fm_shard_payload_capacity(int(B), int(vocab), ctypes.byref(out)), "shard_payload_capacity")
+    return int(out.value)
+
+
 def _stream_of(t) -> int:
     import torch
 
@@ -345,6 +352,22 @@ class FMIndex:
             lo.copy_(lo_out)
             hi.copy_(hi_out)
         return mask
+
+    def shard_pack(self, lo, hi, bits, vocab: int, payload=None):
+        """The sparse exchange payload of this shard's rows (fm_shard_pack):
+        per row its BWT slice when narrower than a bitmap, else its packed
+        allowed-bit row from ``bits`` (int32 [B, >= ceil(vocab/32)], the
+        decode step's packed output).  Returns the int32 payload tensor
+        (capacity for the worst case; word 0 = words used)."""
+        import torch
+
+        B = lo.numel()
+        if payload is None:
+            payload = torch.empty(payload_capacity(B, vocab), dtype=torch.int32, device=lo.device)
+        check(lib().fm_shard_pack(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), B,
+                                  c_void_p(bits.data_ptr()), bits.stride(0), int(vocab), c_void_p(payload.data_ptr()),
+                                  payload.numel(), c_void_p(_stream_of(lo))), "shard_pack")
+        return payload
 
     def distinct_count_batch(self, lo, hi, cap=None):
         """Device interval_symbols for m ranges -> (syms, counts, k, cap_off).

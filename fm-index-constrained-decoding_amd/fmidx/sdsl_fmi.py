@@ -5,44 +5,75 @@ index.py:197-207 opens ``path + '.fmi'``), i.e. sdsl-lite's serialisation of
 ``csa_wt_int<>`` = ``csa_wt<wt_int<>, 32, 64, sa_order_sa_sampling<>,
 isa_sampling<>, int_alphabet<>>``.
 
-PARITY UNPINNED.  sdsl-lite is not vendored in the reference, cannot be built
-offline, and no ``.fmi`` file exists in the reference or this environment, so
-the layout below is restated from sdsl-lite's ``serialize()`` member order and
-is tested only against this repository's own writer of the same layout
-(tests/sdsl_writer.py) -- a round trip, not a reference file.  The reader
-validates everything it can from the file itself (sizes, widths, the alphabet's
-C array against the decoded symbol counts, every ISA sample against the BWT's
-LF walks, and the SA samples against locate), so a layout mismatch on a real
-sdsl file fails loudly instead of yielding a wrong index.
+PARITY UNPINNED.  sdsl-lite is not vendored in the reference (README.md:23
+clones simongog/sdsl-lite HEAD, i.e. 2.1.x; README.md:43 xxsds/sdsl-lite on
+macOS), cannot be built offline, and no ``.fmi`` file exists in the reference
+or this environment.  The layout below is re-derived member by member from
+sdsl-lite 2.1's ``serialize()`` / ``load()`` (each field cites its class and
+member) and the test writer (tests/sdsl_writer.py) restates the same
+derivation, so the round trip pins the reader against the derivation, not
+against a file sdsl wrote.  The reader validates everything it can from the
+file itself (sizes, widths, the alphabet's C array against the decoded symbol
+counts, every ISA sample against the BWT's LF walks, the SA samples against
+locate), so a layout mismatch on a real sdsl file fails loudly instead of
+yielding a wrong index.
 
-Layout read (little endian, sdsl-lite 2.x):
+Layout (little endian; ``store_to_file`` writes ``csa.serialize(out)`` with no
+header):
 
-* ``bit_vector`` / ``int_vector<64>``: size in bits (u64), then
-  ceil(size / 64) u64 words.
-* ``int_vector<0>``: size in bits (u64), width (u8), then ceil(size / 64) u64
-  words; element i occupies bits [i w, (i + 1) w), LSB first.
-* ``rank_support_v``: its directory (an ``int_vector<64>``).
-* ``select_support_mcl``: arg_cnt (u64); if arg_cnt > 0: superblock
-  (``int_vector<0>``), mini_or_long (``bit_vector``), then one
-  ``int_vector<0>`` per superblock of 4096 ones (long superblock or
-  miniblock).  Skipped: the reader needs no select.
-* ``wt_int``: size (u64), sigma (u64), tree (``bit_vector`` of size * max_level
-  bits: level l at bits [l size, (l + 1) size), the sequence stably sorted by
-  its top l bits, bit (max_level - 1 - l) of each symbol), tree_rank,
-  tree_select1, tree_select0, max_level (u32), zero_cnt and rank_level
-  (``int_vector<64>``, max_level entries each).
-* ``csa_wt``: wavelet tree (over the compact alphabet), sa samples (SA[32 i]),
-  isa samples (ISA[64 k] = the row of text position 64 k), alphabet.
-* ``int_alphabet``: char (``bit_vector``, empty when the alphabet is
-  0 .. sigma - 1), char_rank, char_select, C (``int_vector<64>``, sigma + 1),
-  sigma (u64).
+* ``int_vector<1>`` (``bit_vector``) / ``int_vector<64>``: ``int_vector::
+  write_header`` -- m_size in bits (u64) -- then ceil(m_size / 64) u64 words.
+* ``int_vector<0>``: m_size in bits (u64), m_width (u8), then ceil(m_size /
+  64) u64 words; element i occupies bits [i w, (i + 1) w), LSB first.
+* ``rank_support_v<1>::serialize``: m_basic_block (``int_vector<64>``).
+* ``select_support_mcl<b,1>::serialize``: m_arg_cnt (u64); if m_arg_cnt > 0:
+  m_superblock (``int_vector<0>``), mini_or_long (``bit_vector``, empty when
+  there is no long superblock), then for each of the ceil(m_arg_cnt / 4096)
+  superblocks its m_longsuperblock[i] or m_miniblock[i] (``int_vector<0>``).
+  Skipped: the reader needs no select.
+* ``rank_support_sd`` / ``select_support_sd`` / ``*_scan``: nothing
+  (``serialize_empty_object``).
+* ``csa_wt::serialize``: m_wavelet_tree, m_sa_sample, m_isa_sample,
+  m_alphabet -- in that order (csa_wt has no size member of its own).
+* ``wt_int<>::serialize``: m_size (u64), m_sigma (u64: the number of distinct
+  symbols, counted over the non-empty leaves at construction), m_tree
+  (``bit_vector`` of m_size * m_max_level bits: level l at bits [l m_size,
+  (l + 1) m_size), the sequence stably sorted by its top l bits, bit
+  (max_level - 1 - l) of each symbol), m_tree_rank (``rank_support_v``),
+  m_tree_select1 / m_tree_select0 (``select_support_mcl``), m_max_level
+  (u32).  Nothing follows: m_path_off / m_path_rank_off are rebuilt by
+  ``init_buffers(m_max_level)`` in ``load()`` (the zero_cnt / rank_level
+  vectors belong to the wavelet matrix ``wm_int``, not to ``wt_int``).
+  csa_wt constructs its wavelet tree from the cached BWT in the ORIGINAL
+  alphabet (``KEY_BWT``), so the tree holds T' symbols (token id + 10 and the
+  sentinel 0), not compact codes: ``interval_symbols(index.wavelet_tree, ...)``
+  in fm_index.cpp:111,136 returns those symbols, which index.py:156,170 then
+  filters (d > 0) and shifts back; m_max_level = hi(max symbol) + 1 (17 for a
+  128k vocabulary).
+* ``_sa_order_sampling`` (an ``int_vector<0>``): SA[32 i], width hi(n) + 1.
+* ``_isa_sampling`` (an ``int_vector<0>``): ISA[64 k] = the row of text
+  position 64 k, (n - 1) / 64 + 1 entries.
+* ``int_alphabet<>`` (sdsl-lite 2.1: ``t_bit_vector = sd_vector<>``, rank /
+  select ``rank_support_sd`` / ``select_support_sd``): m_char
+  (``sd_vector<>::serialize``: m_size (u64), m_wl (u8), m_low (``int_vector<0>``
+  of width m_wl), m_high (``bit_vector``), m_high_1_select, m_high_0_select
+  (``select_support_mcl``)), m_char_rank and m_char_select (nothing), m_C
+  (``int_vector<64>``, sigma + 1 cumulative counts), m_sigma (u64).  m_char is
+  left default-constructed (m_size 0) when the alphabet is 0 .. sigma - 1.
+  Two other alphabet encodings are accepted when the sd_vector one does not
+  parse to the end of the file: ``bit_vector`` m_char with ``*_scan`` supports
+  (nothing serialised) and ``bit_vector`` + ``rank_support_v`` +
+  ``select_support_mcl`` (sdsl forks that changed the default).  The alphabet is
+  the last member, so at most one of them consumes the file exactly and
+  agrees with the decoded symbol counts; ``alphabet_layout`` says which.
 
 Conversion: the wavelet tree is inverted on the GPU (torch, one pass per
-level: ~40 bytes of device memory per row at peak) into the compact BWT,
-mapped through the alphabet to T' symbols (token id + 10, sentinel 0), handed
-to ``fm_initialize_from_bwt_device``; the ISA samples then give locate /
-extract through ``fm_attach_isa_samples_device`` (every sample checked by an LF
-walk), and the file's SA samples are compared with ``locate`` of their rows.
+level: ~40 bytes of device memory per row at peak) straight into the BWT of T'
+(its symbols are already T' symbols), checked against the alphabet (characters
+and C), handed to ``fm_initialize_from_bwt_device``; the ISA samples then give
+locate / extract through ``fm_attach_isa_samples_device`` (every sample
+checked by an LF walk), and the file's SA samples are compared with ``locate``
+of their rows.
 """
 from __future__ import annotations
 
@@ -94,12 +125,14 @@ class _Cursor:
         return w
 
     def bit_vector(self, what: str, max_bits: int):
+        """int_vector<1>: m_size (bits), words."""
         size = self.u64(what)
         if size > max_bits:
             raise SdslFormatError(f"{self.path}: {what} of {size} bits is implausible")
         return size, self.words(size, what)
 
     def int_vector0(self, what: str, max_bits: int):
+        """int_vector<0>: m_size (bits), m_width (u8), words -> (count, width, words)."""
         size = self.u64(what)
         width = self.u8(what)
         if not 1 <= width <= 64 or size % width or size > max_bits:
@@ -113,9 +146,12 @@ class _Cursor:
         return self.words(size, what)
 
     def skip_select_mcl(self, what: str, max_bits: int):
+        """select_support_mcl<b,1>::serialize (read past it)."""
         arg_cnt = self.u64(what)
         if arg_cnt == 0:
             return
+        if arg_cnt > max_bits:
+            raise SdslFormatError(f"{self.path}: {what}: {arg_cnt} ones is implausible")
         sb = (arg_cnt + 4095) >> 12
         self.int_vector0(what + ".superblock", max_bits)
         mol_bits, _ = self.bit_vector(what + ".mini_or_long", max_bits)
@@ -123,6 +159,63 @@ class _Cursor:
             raise SdslFormatError(f"{self.path}: {what}: mini_or_long of {mol_bits} bits for {sb} superblocks")
         for _ in range(sb):
             self.int_vector0(what + ".block", max_bits)
+
+
+def _bits_of(words: np.ndarray, nbits: int) -> np.ndarray:
+    return np.unpackbits(np.ascontiguousarray(words).view(np.uint8), bitorder="little")[:nbits]
+
+
+def _sd_vector_ones(c: "_Cursor", what: str, max_bits: int):
+    """sd_vector<>::serialize -> (m_size, positions of its ones).  The i-th
+    one at position p is stored as m_low[i] = p mod 2^wl and a set bit of
+    m_high at (p >> wl) + i."""
+    size = c.u64(what + ".size")
+    wl = c.u8(what + ".wl")
+    if size >= (1 << 40) or wl > 64:        # a logical size: sparse, so not bounded by the file
+        raise SdslFormatError(f"{c.path}: {what}: size {size}, wl {wl}")
+    lsize = c.u64(what + ".low")
+    lw = c.u8(what + ".low")
+    if lsize % max(1, lw) or lsize > max_bits or lw > 64:
+        raise SdslFormatError(f"{c.path}: {what}.low: size {lsize} bits, width {lw}")
+    lwords = c.words(lsize, what + ".low")
+    cnt = lsize // lw if lw else 0
+    hbits, hwords = c.bit_vector(what + ".high", max_bits)
+    c.skip_select_mcl(what + ".high_1_select", max_bits)
+    c.skip_select_mcl(what + ".high_0_select", max_bits)
+    if size == 0:
+        if cnt:
+            raise SdslFormatError(f"{c.path}: {what}: empty vector with {cnt} ones")
+        return 0, np.zeros(0, dtype=np.int64)
+    if lw != wl:
+        raise SdslFormatError(f"{c.path}: {what}: low width {lw} != wl {wl}")
+    hpos = np.flatnonzero(_bits_of(hwords, hbits)).astype(np.int64)
+    if hpos.size != cnt:
+        raise SdslFormatError(f"{c.path}: {what}: {hpos.size} high bits for {cnt} ones")
+    low = unpack_int_vector(lwords, cnt, wl).astype(np.int64) if wl else np.zeros(cnt, dtype=np.int64)
+    pos = ((hpos - np.arange(cnt, dtype=np.int64)) << wl) | low
+    if cnt and (np.any(np.diff(pos) <= 0) or pos[-1] >= size):
+        raise SdslFormatError(f"{c.path}: {what}: ones not strictly increasing inside {size} bits")
+    return size, pos
+
+
+def _read_alphabet(c: "_Cursor", layout: str, cap: int):
+    """int_alphabet<...>::serialize in one of the accepted encodings ->
+    (chars or None for the identity, C, sigma)."""
+    if layout == "sd_vector":
+        size, chars = _sd_vector_ones(c, "alphabet.char", cap)
+        chars = chars if size else None
+    else:
+        nbits, words = c.bit_vector("alphabet.char", cap)
+        chars = np.flatnonzero(_bits_of(words, nbits)).astype(np.int64) if nbits else None
+        if layout == "bit_vector+v+mcl":
+            c.int_vector64("alphabet.char_rank", cap)
+            c.skip_select_mcl("alphabet.char_select", cap)
+    C = c.int_vector64("alphabet.C", cap).copy()
+    sigma = c.u64("alphabet.sigma")
+    return chars, C, sigma
+
+
+ALPHABET_LAYOUTS = ("sd_vector", "bit_vector+scan", "bit_vector+v+mcl")
 
 
 def unpack_int_vector(words: np.ndarray, count: int, width: int) -> np.ndarray:
@@ -148,35 +241,20 @@ class SdslCsaWtInt:
         buf = np.fromfile(path, dtype=np.uint8)
         c = _Cursor(buf, path)
         cap = 8 * buf.size                     # no structure can hold more bits than the file
-        # ---- wt_int
-        self.n = c.u64("wt_int.size")
-        self.wt_sigma = c.u64("wt_int.sigma")
+        # ---- csa_wt::m_wavelet_tree (wt_int<>::serialize)
+        self.n = c.u64("wt_int.m_size")
+        self.wt_sigma = c.u64("wt_int.m_sigma")
         if self.n == 0 or self.n >= (1 << 34):
             raise SdslFormatError(f"{path}: wt_int size {self.n} out of range (0 < n < 2^34)")
-        tree_bits, self.tree = c.bit_vector("wt_int.tree", cap)
-        c.int_vector64("wt_int.tree_rank", cap)
-        c.skip_select_mcl("wt_int.tree_select1", cap)
-        c.skip_select_mcl("wt_int.tree_select0", cap)
-        save = c.p
-        self.max_level = None
-        for width in (4, 8):       # u32 in sdsl-lite 2.x; a u64 variant is accepted if it is the one that parses
-            c.p = save
-            L = c.u32("wt_int.max_level") if width == 4 else c.u64("wt_int.max_level")
-            if L == 0 or L > 64 or L * self.n != tree_bits:
-                continue
-            try:
-                z = c.int_vector64("wt_int.zero_cnt", cap)
-                r = c.int_vector64("wt_int.rank_level", cap)
-            except SdslFormatError:
-                continue
-            if z.size == L and r.size == L:
-                self.max_level = L
-                self.zero_cnt = z.copy()
-                break
-        if self.max_level is None:
-            raise SdslFormatError(f"{path}: wt_int max_level / zero_cnt do not match a tree of {tree_bits} bits "
-                                  f"over {self.n} rows")
-        # ---- samples
+        tree_bits, self.tree = c.bit_vector("wt_int.m_tree", cap)
+        c.int_vector64("wt_int.m_tree_rank", cap)
+        c.skip_select_mcl("wt_int.m_tree_select1", cap)
+        c.skip_select_mcl("wt_int.m_tree_select0", cap)
+        self.max_level = c.u32("wt_int.m_max_level")
+        if not 1 <= self.max_level <= 64 or self.max_level * self.n != tree_bits:
+            raise SdslFormatError(f"{path}: wt_int m_max_level {self.max_level} does not match a tree of "
+                                  f"{tree_bits} bits over {self.n} rows")
+        # ---- csa_wt::m_sa_sample, m_isa_sample
         cnt, width, words = c.int_vector0("sa_samples", cap)
         if cnt != (self.n + SDSL_SA_RATE - 1) // SDSL_SA_RATE:
             raise SdslFormatError(f"{path}: {cnt} SA samples for n = {self.n}")
@@ -185,32 +263,46 @@ class SdslCsaWtInt:
         if cnt != (self.n - 1) // SDSL_ISA_RATE + 1:
             raise SdslFormatError(f"{path}: {cnt} ISA samples for n = {self.n}")
         self.isa_samples = unpack_int_vector(words, cnt, width)
-        # ---- int_alphabet
-        char_bits, char_words = c.bit_vector("alphabet.char", cap)
-        c.int_vector64("alphabet.char_rank", cap)
-        c.skip_select_mcl("alphabet.char_select", cap)
-        self.C = c.int_vector64("alphabet.C", cap).copy()
-        self.sigma = c.u64("alphabet.sigma")
-        if c.p != buf.size:
-            raise SdslFormatError(f"{path}: {buf.size - c.p} trailing bytes after the alphabet")
-        if self.C.size != self.sigma + 1 or int(self.C[-1]) != self.n or np.any(np.diff(self.C.astype(np.int64)) < 0):
-            raise SdslFormatError(f"{path}: alphabet C array inconsistent with sigma {self.sigma} / n {self.n}")
+        # ---- csa_wt::m_alphabet: the first encoding that ends exactly at the end of the file
+        start, errors = c.p, []
+        for layout in ALPHABET_LAYOUTS:
+            c.p = start
+            try:
+                chars, C, sigma = _read_alphabet(c, layout, cap)
+            except SdslFormatError as e:
+                errors.append(f"{layout}: {e}")
+                continue
+            if c.p != buf.size:
+                errors.append(f"{layout}: {buf.size - c.p} trailing bytes")
+                continue
+            if C.size != sigma + 1 or int(C[-1]) != self.n or np.any(np.diff(C.astype(np.int64)) < 0):
+                errors.append(f"{layout}: C array inconsistent with sigma {sigma} / n {self.n}")
+                continue
+            if chars is not None and chars.size != sigma:
+                errors.append(f"{layout}: {chars.size} characters for sigma {sigma}")
+                continue
+            self.alphabet_layout = layout
+            self.C, self.sigma = C, sigma
+            self.chars = chars if chars is not None else np.arange(sigma, dtype=np.int64)
+            break
+        else:
+            raise SdslFormatError(f"{path}: the alphabet does not parse in any accepted encoding: " +
+                                  "; ".join(errors))
+        # m_sigma counts the distinct symbols of the tree (= the alphabet's sigma)
         if self.wt_sigma != self.sigma:
             raise SdslFormatError(f"{path}: wavelet tree sigma {self.wt_sigma} != alphabet sigma {self.sigma}")
-        if char_bits:
-            bits = np.unpackbits(char_words.view(np.uint8), bitorder="little")[:char_bits]
-            self.comp2char = np.flatnonzero(bits).astype(np.int64)
-        else:
-            self.comp2char = np.arange(self.sigma, dtype=np.int64)
-        if self.comp2char.size != self.sigma:
-            raise SdslFormatError(f"{path}: alphabet has {self.comp2char.size} characters, sigma {self.sigma}")
-        if self.sigma and (self.max_level < max(1, int(self.sigma - 1).bit_length())):
-            raise SdslFormatError(f"{path}: {self.max_level} levels cannot hold {self.sigma} symbols")
+        if self.sigma and self.max_level < max(1, int(self.chars[-1]).bit_length()):
+            raise SdslFormatError(f"{path}: {self.max_level} levels cannot hold symbol {int(self.chars[-1])}")
+
+    @property
+    def comp2char(self) -> np.ndarray:
+        """Compact code -> character (the alphabet's characters, ascending)."""
+        return self.chars
 
 
 def decode_wt_int_device(tree_words: np.ndarray, n: int, L: int, device, chunk: int = 1 << 27):
-    """The sequence a wt_int tree encodes (compact symbols, int64 [n] on
-    ``device``), by one pass per level: every position carries its prefix
+    """The sequence a wt_int tree encodes (int64 [n] on ``device``; for a
+    csa_wt_int<> these are the BWT's T' symbols), by one pass per level: every position carries its prefix
     (the symbol's top l bits) and its position in level l's order; level l's
     bit there is the next bit, and the position in level l + 1's order is its
     node's start + its rank among the node's zeros (or the node's zero count +
@@ -256,12 +348,16 @@ def load_sdsl_fmi(path: str, device: Optional[int] = None, verify_samples: bool 
     f = SdslCsaWtInt(path)
     dev_index = _default_device() if device is None else int(device)
     dev = torch.device("cuda", dev_index)
-    comp = decode_wt_int_device(f.tree, f.n, f.max_level, dev)
-    counts = torch.bincount(comp, minlength=int(f.sigma)).cpu().numpy()
-    if counts.size != f.sigma or not np.array_equal(counts.astype(np.uint64), np.diff(f.C)):
-        raise SdslFormatError(f"{path}: decoded wavelet tree disagrees with the alphabet's C array")
-    bwt = torch.from_numpy(f.comp2char).to(dev)[comp].to(torch.int32)
-    del comp
+    sym = decode_wt_int_device(f.tree, f.n, f.max_level, dev)     # T' symbols (csa_wt builds from KEY_BWT)
+    counts = torch.bincount(sym, minlength=int(f.chars[-1]) + 1 if f.sigma else 1).cpu().numpy()
+    want = np.zeros(counts.size, dtype=np.int64)
+    if counts.size != (int(f.chars[-1]) + 1 if f.sigma else 1):
+        raise SdslFormatError(f"{path}: the wavelet tree holds symbols beyond the alphabet")
+    want[f.chars] = np.diff(f.C.astype(np.int64))
+    if not np.array_equal(counts.astype(np.int64), want):
+        raise SdslFormatError(f"{path}: decoded wavelet tree disagrees with the alphabet's characters / C array")
+    bwt = sym.to(torch.int32)
+    del sym
     if int((bwt == 0).sum()) != 1:
         raise SdslFormatError(f"{path}: the decoded BWT must hold exactly one sentinel 0")
     ix = FMIndex(device=dev_index)
@@ -285,5 +381,5 @@ def is_sdsl_file(path: str) -> bool:
         return fh.read(8) != b"FMIDXAMD"
 
 
-__all__ = ["SdslCsaWtInt", "SdslFormatError", "decode_wt_int_device", "load_sdsl_fmi", "is_sdsl_file",
+__all__ = ["ALPHABET_LAYOUTS", "SdslCsaWtInt", "SdslFormatError", "decode_wt_int_device", "load_sdsl_fmi", "is_sdsl_file",
            "unpack_int_vector"]

@@ -19,8 +19,13 @@ masks / emptiness are comparable across shard layouts (the reference's only
 count consumer, stop_at_count, is 0 at every call site).
 
 The collective is the only data-path exchange: ``all_reduce(MAX)`` of the
-uint8 [B, V] mask (0/1, so MAX == OR), or ``all_gather`` of bit-packed masks
-followed by a local OR (8x fewer bytes on the wire).
+uint8 [B, V] mask (0/1, so MAX == OR), ``all_gather`` of bit-packed masks
+followed by a local OR (8x fewer bytes on the wire), or -- the default on the
+GPU -- the sparse exchange: each rank ships, per row, its shard's BWT slice
+when that is smaller than the row's bitmap, else the bitmap (fm_shard_pack;
+most rows are a few rows wide on a shard), one tiny all_gather of the payload
+sizes, one all_gather of the payloads (the largest rank's prefix), then one
+fused OR / scatter / unpack pass (fm_shard_or_rows).
 """
 from __future__ import annotations
 
@@ -110,11 +115,14 @@ class ShardedDecoder:
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8",
                  halo: Optional[int] = None):
+        """reduce: "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
+        (all_gather of the packed rows + fm_or_bits) or "sparse" (BWT slices /
+        bitmaps per row, fm_shard_pack + fm_shard_or_rows)."""
         self.index = index
         self.vocab = vocab
         self.shift = shift
         self.group = group
-        if reduce not in ("max_u8", "gather_bits"):
+        if reduce not in ("max_u8", "gather_bits", "sparse"):
             raise ValueError(reduce)
         self.reduce = reduce
         self.halo = halo
@@ -126,6 +134,8 @@ class ShardedDecoder:
         self._bound = 0        # host upper bound of max(_plen)
         self._parts = None     # gathered packed rows of every rank (device path)
         self._out = None
+        self._payload = None   # this rank's sparse-exchange payload
+        self.exchange_words = []   # sparse: words every rank shipped, per step (host ints)
 
     def _check_halo(self):
         """Exactness needs every pattern to be at most halo - 1 tokens.  The
@@ -171,7 +181,7 @@ class ShardedDecoder:
         if not self.fused:
             self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
             return self.mask()
-        packed = self.group is not None and self.reduce == "gather_bits"
+        packed = self.group is not None and self.reduce in ("gather_bits", "sparse")
         if self._buf is None:
             B = self.lo.numel()
             if packed:
@@ -184,7 +194,22 @@ class ShardedDecoder:
                                packed=packed, lo_out=self._lo2, hi_out=self._hi2)
         self.lo, self._lo2 = self._lo2, self.lo
         self.hi, self._hi2 = self._hi2, self.hi
+        if self.group is not None and self.reduce == "sparse":
+            return self._combine_sparse(self._buf)
         return self._combine(self._buf, packed)
+
+    def _combine_sparse(self, bits):
+        """The sparse exchange of this step's rows (new state self.lo/hi,
+        their packed bits from the decode step)."""
+        import torch
+
+        self._payload = self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=self._payload)
+        parts, words = gather_payloads(self._payload, self.group)
+        self.exchange_words.append(words)
+        B = self.lo.numel()
+        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != parts.device:
+            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=parts.device)
+        return or_payloads(parts, B, self.vocab, self.shift, out=self._out)
 
     def local_mask(self):
         return self.index.allowed_mask(self.lo, self.hi, self.vocab, self.shift)
@@ -225,6 +250,114 @@ class ShardedDecoder:
         if packed:
             acc = acc.view(torch.uint8)
         return unpack_bits(acc, self.vocab)
+
+
+def payload_capacity(B: int, vocab: int) -> int:
+    """Worst-case uint32 words of a sparse-exchange payload of B rows."""
+    from .fm_index import payload_capacity as _cap
+
+    return _cap(B, vocab)
+
+
+def gather_payloads(payload, group):
+    """all_gather of every rank's sparse-exchange payload: the sizes first
+    (one int64 per rank, read on the host), then each rank's first
+    max(size) words -> (int32 [world, max], [words per rank])."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    used = payload[:1].to(torch.int64)
+    sizes = torch.empty(world, dtype=torch.int64, device=payload.device)
+    dist.all_gather_into_tensor(sizes, used, group=group)
+    words = [int(x) for x in sizes.tolist()]
+    m = max(words)
+    mine = payload[:m]
+    if mine.numel() < m:                  # a host payload is exactly its size
+        mine = torch.cat([mine, torch.zeros(m - mine.numel(), dtype=mine.dtype, device=mine.device)])
+    parts = torch.empty(world * m, dtype=torch.int32, device=payload.device)
+    dist.all_gather_into_tensor(parts, mine.contiguous(), group=group)
+    return parts.view(world, m), words
+
+
+def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+    """OR of the ranks' sparse-exchange payloads ``parts`` (int32 [P, stride])
+    -> uint8 [B, vocab] (unpack) or int32 [B, ceil(vocab/32)] words.  GPU:
+    fm_shard_or_rows; CPU tensors (gloo tests): the same format read with
+    torch ops (or_payloads_host)."""
+    import torch
+    from ctypes import c_void_p
+
+    from ._lib import check, lib
+
+    if not parts.is_cuda:
+        return or_payloads_host(parts, B, vocab, shift, unpack=unpack)
+    P, stride = parts.shape
+    W = (vocab + 31) // 32
+    if out is None:
+        out = (torch.empty((B, vocab), dtype=torch.uint8, device=parts.device) if unpack
+               else torch.empty((B, W), dtype=torch.int32, device=parts.device))
+    assert parts.dtype == torch.int32 and parts.is_contiguous() and out.stride(1) == 1
+    ld = out.stride(0) * out.element_size()
+    stream = torch.cuda.current_stream(parts.device).cuda_stream
+    check(lib().fm_shard_or_rows(c_void_p(parts.data_ptr()), P, stride, B, vocab, int(shift), c_void_p(out.data_ptr()),
+                                 ld, 1 if unpack else 0, c_void_p(stream)), "shard_or_rows")
+    return out
+
+
+_PAYLOAD_MAGIC = 0x58534D46
+
+
+def pack_payload_host(lo, hi, bwt, bits_words, vocab: int):
+    """The sparse-exchange payload (csrc/shard.hip's layout) built on the host
+    from a shard's BWT (int array) and its packed rows (int32 [B, >= W]) --
+    for CPU indexes (gloo tests); the GPU path is fm_shard_pack."""
+    import torch
+
+    lo = np.asarray(lo, dtype=np.int64)
+    hi = np.minimum(np.asarray(hi, dtype=np.int64), len(bwt))
+    B = lo.size
+    W = (vocab + 31) // 32
+    H = 4 + ((2 * B + 3) & ~3)
+    bw = np.asarray(bits_words, dtype=np.int64).astype(np.uint32)
+    desc, off, data = np.zeros(B, dtype=np.uint32), np.zeros(B, dtype=np.uint32), []
+    at = H
+    for b in range(B):
+        w = max(0, int(hi[b] - lo[b]))
+        dense = w >= W
+        row = bw[b, :W] if dense else np.asarray(bwt[lo[b]:lo[b] + w], dtype=np.uint32)
+        pad = (-row.size) % 4
+        desc[b] = row.size | (0x80000000 if dense else 0)
+        off[b] = at
+        data.append(np.concatenate([row, np.zeros(pad, dtype=np.uint32)]))
+        at += row.size + pad
+    head = np.zeros(H, dtype=np.uint32)
+    head[:4] = [at, B, W, _PAYLOAD_MAGIC]
+    head[4:4 + B] = desc
+    head[4 + B:4 + 2 * B] = off
+    out = np.concatenate([head] + data)
+    return torch.from_numpy(out.view(np.int32).copy())
+
+
+def or_payloads_host(parts, B: int, vocab: int, shift: int, unpack: bool = True):
+    import torch
+
+    W = (vocab + 31) // 32
+    bits = np.zeros((B, W * 32), dtype=np.uint8)
+    for p in parts.cpu().numpy().view(np.uint32):
+        assert int(p[3]) == _PAYLOAD_MAGIC and int(p[1]) == B and int(p[2]) == W
+        for b in range(B):
+            d, o = int(p[4 + b]), int(p[4 + B + b])
+            cnt = d & 0x7FFFFFFF
+            if d >> 31:
+                bits[b] |= np.unpackbits(p[o:o + W].view(np.uint8), bitorder="little")
+            else:
+                tok = p[o:o + cnt].astype(np.int64) - shift
+                tok = tok[(tok >= 0) & (tok < vocab)]
+                bits[b, tok] = 1
+    if unpack:
+        return torch.from_numpy(bits[:, :vocab].copy())
+    return torch.from_numpy(np.packbits(bits, axis=1, bitorder="little").view(np.int32).copy())
 
 
 def or_bits(parts, vocab: int, out=None, unpack: bool = True):
@@ -276,4 +409,5 @@ def unpack_bits(packed, vocab: int):
 
 
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
-           "or_bits", "pack_bits", "unpack_bits"]
+           "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "gather_payloads", "or_payloads",
+           "pack_payload_host", "or_payloads_host"]

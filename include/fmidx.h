@@ -264,6 +264,24 @@ int fm_apply_boosts(int dtype, const void* d_scores, void* d_out, uint64_t B, ui
 int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t words_per_row,
                uint64_t vocab, void* d_out, uint64_t ld_out, int unpack, void* stream);
 
+/* The sparse exchange (replaces shipping every row's bitmap): a rank packs,
+ * per row of its post-step state (d_lo, d_hi) on its shard, either the BWT
+ * slice [lo, hi) (when hi - lo < W = ceil(vocab / 32): smaller than the
+ * bitmap) or the row's bitmap from d_bits (its fm_decode_step_batch(packed=1)
+ * output, ldw words per row) into d_payload (cap_words uint32; word 0 = the
+ * words used, a multiple of 4: an all_gather needs only the largest rank's
+ * prefix).  fm_shard_or_rows ORs the payloads of nparts ranks (part p at
+ * d_parts + p * part_stride words) into the uint8 [B, vocab] mask (unpack != 0)
+ * or the packed words -- bit for bit what fm_or_bits gives for the ranks'
+ * bitmaps (a BWT symbol s is token s - shift, kept when in [0, vocab)).
+ * Layout: csrc/shard.hip.  Replaces the dense OR-exchange SURVEY §8e
+ * describes (all_gather of packed [B, V/32] rows). */
+int fm_shard_payload_capacity(uint64_t B, uint64_t vocab, uint64_t* words);
+int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
+                  uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
+int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
+                     int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
+
 /* ---- logits-processor step on the device --------------------------------- */
 
 /* The per-row bookkeeping of the soft processors' _process

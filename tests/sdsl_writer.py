@@ -1,10 +1,24 @@
 """TEST INFRASTRUCTURE: a writer of sdsl-lite's csa_wt_int<> serialisation (the
 reference's ``.fmi``, fm_index.cpp:196-199) for the reader's round-trip tests.
 
-It follows the member order and encodings fmidx/sdsl_fmi.py documents, from a
-text T' by definition (suffix array by sorting, oracle/fm_oracle.py).  The
-rank directories are computed as sdsl's rank_support_v lays them out; the
-select structures (which the reader skips) are written in sdsl's shape --
+It is restated from sdsl-lite 2.1's ``serialize()`` member order, member by
+member (the class and member of every field are named below and in
+fmidx/sdsl_fmi.py's header), from a text T' by definition (suffix array by
+sorting, oracle/fm_oracle.py):
+
+* csa_wt: m_wavelet_tree, m_sa_sample, m_isa_sample, m_alphabet.
+* wt_int<>: m_size, m_sigma (distinct symbols), m_tree (levels of the
+  ORIGINAL BWT symbols -- csa_wt builds its tree from KEY_BWT), m_tree_rank
+  (rank_support_v), m_tree_select1, m_tree_select0 (select_support_mcl),
+  m_max_level (u32) -- and nothing after it.
+* int_alphabet<> with sd_vector<> m_char (m_size, m_wl, m_low, m_high,
+  m_high_1_select, m_high_0_select; sdsl's sd_vector(bit_vector) choice of
+  wl), rank_support_sd / select_support_sd (empty), m_C (int_vector<64>),
+  m_sigma.  ``alphabet_layout`` writes the two other encodings the reader
+  accepts.
+
+The rank directories are computed as sdsl's rank_support_v lays them out;
+the select structures (which the reader skips) are written in sdsl's shape --
 arg_cnt, a superblock vector, an empty mini_or_long, one miniblock vector per
 4096 ones -- without claiming sdsl's exact long/mini choice.  No sdsl file
 exists here, so this pins the reader against this restatement only (parity
@@ -107,7 +121,43 @@ def wt_int_tree(seq: np.ndarray, L: int) -> np.ndarray:
     return out
 
 
-def write_csa_wt_int(path: str, text: np.ndarray, contiguous_alphabet=None, max_level_u64: bool = False):
+def _hi(x: int) -> int:
+    """sdsl bits::hi: index of the most significant set bit (-1 for 0)."""
+    return int(x).bit_length() - 1
+
+
+def sd_vector(w: "_W", bits: np.ndarray):
+    """sd_vector<>::serialize of the bit_vector ``bits`` (sd_vector(const
+    bit_vector&): logm = hi(m) + 1, logn = hi(size) + 1, logm decremented when
+    equal, wl = logn - logm; m_low[i] = p & (2^wl - 1); m_high[(p >> wl) + i]
+    set; m_high of m + 2^logm bits)."""
+    size = bits.size
+    ones = np.flatnonzero(bits).astype(np.int64)
+    m = ones.size
+    if size == 0:                              # default-constructed: the continuous alphabet
+        w.u64(0)
+        w.u8(0)
+        w.int_vector0(np.zeros(0, dtype=np.uint64), 64)
+        w.bit_vector(np.zeros(0, dtype=np.uint8))
+        w.select_support_mcl(np.zeros(0, dtype=np.uint8), True)
+        w.select_support_mcl(np.zeros(0, dtype=np.uint8), False)
+        return
+    logm = _hi(m) + 1
+    logn = _hi(size) + 1
+    if logm == logn:
+        logm -= 1
+    wl = logn - logm
+    high = np.zeros(m + (1 << logm), dtype=np.uint8)
+    high[(ones >> wl) + np.arange(m)] = 1
+    w.u64(size)
+    w.u8(wl)
+    w.int_vector0(ones & ((1 << wl) - 1), wl)
+    w.bit_vector(high)
+    w.select_support_mcl(high, True)
+    w.select_support_mcl(high, False)
+
+
+def write_csa_wt_int(path: str, text: np.ndarray, contiguous_alphabet=None, alphabet_layout: str = "sd_vector"):
     """Serialise the csa_wt_int<> of T' (``text``: int array, unique 0 last)."""
     text = np.asarray(text, dtype=np.int64)
     n = text.size
@@ -116,47 +166,40 @@ def write_csa_wt_int(path: str, text: np.ndarray, contiguous_alphabet=None, max_
     chars = np.unique(text)
     contiguous = bool(chars.size == chars[-1] + 1) if contiguous_alphabet is None else contiguous_alphabet
     sigma = chars.size
-    char2comp = np.zeros(int(chars[-1]) + 1, dtype=np.int64)
-    char2comp[chars] = np.arange(sigma)
-    comp = char2comp[bwt]
-    L = _bits_needed(sigma - 1) if sigma > 1 else 1
-    tree = wt_int_tree(comp, L)
+    # wt_int over the original BWT symbols: m_max_level = hi(max(1, max symbol)) + 1
+    L = _hi(max(1, int(bwt.max()))) + 1
+    tree = wt_int_tree(bwt, L)
     w = _W()
-    # wt_int
-    w.u64(n)
-    w.u64(sigma)
-    w.bit_vector(tree)
-    w.rank_support_v(tree)
-    w.select_support_mcl(tree, True)
-    w.select_support_mcl(tree, False)
-    if max_level_u64:
-        w.u64(L)
-    else:
-        w.u32(L)
-    zero_cnt = [int((tree[lev * n:(lev + 1) * n] == 0).sum()) for lev in range(L)]
-    rank_level = [int(tree[: lev * n].sum()) for lev in range(L)]
-    w.int_vector64(zero_cnt)
-    w.int_vector64(rank_level)
-    # samples
-    wid = _bits_needed(n)
+    # csa_wt::m_wavelet_tree = wt_int<>::serialize
+    w.u64(n)                      # m_size
+    w.u64(sigma)                  # m_sigma: distinct symbols (non-empty leaves)
+    w.bit_vector(tree)            # m_tree
+    w.rank_support_v(tree)        # m_tree_rank
+    w.select_support_mcl(tree, True)    # m_tree_select1
+    w.select_support_mcl(tree, False)   # m_tree_select0
+    w.u32(L)                      # m_max_level (uint32_t); m_path_off / m_path_rank_off are not stored
+    # csa_wt::m_sa_sample (_sa_order_sampling = int_vector<0>, width hi(n) + 1), m_isa_sample
+    wid = _hi(n) + 1
     w.int_vector0(sa[::32], wid)
     isa = np.empty(n, dtype=np.int64)
     isa[sa] = np.arange(n)
     w.int_vector0(isa[::64], wid)
-    # int_alphabet
-    if contiguous:
-        w.bit_vector(np.zeros(0, dtype=np.uint8))
-        w.rank_support_v(np.zeros(0, dtype=np.uint8))
-        w.select_support_mcl(np.zeros(0, dtype=np.uint8), True)
-    else:
-        cb = np.zeros(int(chars[-1]) + 1, dtype=np.uint8)
-        cb[chars] = 1
+    # csa_wt::m_alphabet = int_alphabet<>::serialize
+    cb = np.zeros(0 if contiguous else int(chars[-1]) + 1, dtype=np.uint8)
+    cb[chars[chars < cb.size]] = 1
+    if alphabet_layout == "sd_vector":
+        sd_vector(w, cb)          # m_char; m_char_rank (rank_support_sd), m_char_select: nothing
+    elif alphabet_layout == "bit_vector+scan":
+        w.bit_vector(cb)          # m_char; rank_support_scan / select_support_scan: nothing
+    elif alphabet_layout == "bit_vector+v+mcl":
         w.bit_vector(cb)
         w.rank_support_v(cb)
         w.select_support_mcl(cb, True)
-    C = np.concatenate([[0], np.cumsum(np.bincount(comp, minlength=sigma))]).astype(np.uint64)
-    w.int_vector64(C)
-    w.u64(sigma)
+    else:
+        raise ValueError(alphabet_layout)
+    C = np.concatenate([[0], np.cumsum(np.bincount(np.searchsorted(chars, bwt), minlength=sigma))]).astype(np.uint64)
+    w.int_vector64(C)             # m_C
+    w.u64(sigma)                  # m_sigma
     with open(path, "wb") as f:
         f.write(w.f.getvalue())
-    return {"n": n, "sa": sa, "bwt": bwt, "comp": comp, "L": L, "sigma": sigma}
+    return {"n": n, "sa": sa, "bwt": bwt, "L": L, "sigma": sigma, "chars": chars}

@@ -68,3 +68,64 @@ def test_or_bits_rejects_short_rows(dev):
     with pytest.raises(ValueError):
         or_bits(parts, 100, out=torch.empty((3, 100), dtype=torch.uint8, device=dev)[:, :50])
     np.testing.assert_array_equal(or_bits(parts, 100).cpu().numpy(), np.zeros((3, 100), np.uint8))
+
+
+@pytest.mark.parametrize("V", [100, 128256, 151936])
+@pytest.mark.parametrize("world", [2, 5])
+def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
+    """fm_shard_pack + fm_shard_or_rows (the sparse C4 exchange) against the
+    dense exchange (fm_or_bits over every shard's packed rows) and the
+    unsharded index's mask, over doc-range shards with a halo: rows from
+    empty to the full range, so both payload kinds (BWT slice, bitmap) occur;
+    the gathered payloads are padded to the largest, as the all_gather does."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from fmidx.sharding import or_bits, or_payloads, shard_corpus
+
+    rng = np.random.default_rng(V + world)
+    vocab_used = min(V, 3000)
+    docs = [rng.integers(0, vocab_used, size=int(rng.integers(5, 400))).tolist() for _ in range(300)]
+    # a repeated phrase so some patterns are wide on every shard
+    for d in docs[::3]:
+        d[:4] = [1, 2, 3, 4]
+    F = [t for d in reversed(docs) for t in d]
+    B = 64
+    pats = [[]] + [[1, 2]] + [[1]] + [F[s:s + int(rng.integers(1, 5))] for s in rng.integers(0, len(F) - 8, B - 4)]
+    pats.append([vocab_used + 7])                 # never in the corpus: empty everywhere
+    full = FMIndex()
+    full.initialize(docs, in_memory=True)
+    lo, hi = full.get_range_batch(pats, 10)
+    want = full.allowed_mask(torch.tensor(lo.astype(np.int64), device=dev), torch.tensor(hi.astype(np.int64), device=dev),
+                             V, 10)
+    W = (V + 31) // 32
+    payloads, packed = [], []
+    for r in range(world):
+        sd, _ = shard_corpus(docs, world, r, 8)
+        ix = FMIndex()
+        ix.initialize(sd, in_memory=True)
+        slo, shi = ix.get_range_batch(pats, 10)
+        lo_t = torch.tensor(slo.astype(np.int64), device=dev)
+        hi_t = torch.tensor(shi.astype(np.int64), device=dev)
+        bits = ix.allowed_mask(lo_t, hi_t, V, 10, packed=True)
+        packed.append(bits)
+        pay = ix.shard_pack(lo_t, hi_t, bits, V)
+        used = int(pay[0].item())
+        assert used % 4 == 0 and used <= pay.numel()
+        desc = pay[4:4 + B].cpu().numpy().view(np.uint32)
+        widths = (np.minimum(shi, ix.size()) - slo).astype(np.int64)
+        np.testing.assert_array_equal(desc >> 31, (widths >= W).astype(np.uint32))
+        payloads.append(pay[:used])
+        del ix
+    m = max(p.numel() for p in payloads)
+    parts = torch.zeros((world, m), dtype=torch.int32, device=dev)
+    for r, p in enumerate(payloads):
+        parts[r, :p.numel()] = p
+    got = or_payloads(parts, B, V, 10)
+    dense = or_bits(torch.stack(packed).contiguous(), V)
+    assert torch.equal(dense, want)
+    assert torch.equal(got, want)
+    assert torch.equal(or_payloads(parts, B, V, 10, unpack=False), or_bits(torch.stack(packed).contiguous(), V,
+                                                                           unpack=False))
+    if V > 1000:   # most rows ship a slice, not a 16-KB bitmap
+        assert sum(p.numel() for p in payloads) * 4 < world * B * W * 4 / 2

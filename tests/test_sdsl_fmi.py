@@ -31,26 +31,96 @@ CASES = [(1, 3, 5, 4), (2, 40, 30, 60), (3, 200, 500, 120), (4, 30, 128256, 80),
 
 
 @pytest.mark.parametrize("seed,n_docs,vocab,max_len", CASES)
-@pytest.mark.parametrize("u64_level", [False, True])
-def test_parse_and_invert_on_cpu(tmp_path, seed, n_docs, vocab, max_len, u64_level):
+@pytest.mark.parametrize("layout", ["sd_vector", "bit_vector+scan", "bit_vector+v+mcl"])
+def test_parse_and_invert_on_cpu(tmp_path, seed, n_docs, vocab, max_len, layout):
     import torch
 
     from fmidx.sdsl_fmi import SdslCsaWtInt, decode_wt_int_device
 
     text = _text(_docs(seed, n_docs, vocab, max_len))
     p = str(tmp_path / "x.fmi")
-    ref = write_csa_wt_int(p, text, max_level_u64=u64_level)
+    ref = write_csa_wt_int(p, text, alphabet_layout=layout)
     f = SdslCsaWtInt(p)
     n = text.size
     assert f.n == n and f.max_level == ref["L"] and f.sigma == ref["sigma"]
-    assert np.array_equal(f.comp2char, np.unique(text))
+    assert f.alphabet_layout == layout
+    assert np.array_equal(f.chars, np.unique(text))
     assert np.array_equal(f.sa_samples.astype(np.int64), ref["sa"][::32])
     isa = np.empty(n, dtype=np.int64)
     isa[ref["sa"]] = np.arange(n)
     assert np.array_equal(f.isa_samples.astype(np.int64), isa[::64])
-    comp = decode_wt_int_device(f.tree, n, f.max_level, torch.device("cpu"), chunk=1000)
-    assert np.array_equal(comp.numpy(), ref["comp"])
-    assert np.array_equal(f.comp2char[comp.numpy()], ref["bwt"])
+    # the tree holds the BWT's T' symbols themselves (csa_wt builds it from KEY_BWT)
+    sym = decode_wt_int_device(f.tree, n, f.max_level, torch.device("cpu"), chunk=1000)
+    assert np.array_equal(sym.numpy(), ref["bwt"])
+
+
+def _hand_fmi_bytes() -> bytes:
+    """csa_wt_int<> of T' = [11, 12, 11, 0] assembled field by field by hand
+    (independent of tests/sdsl_writer.py): SA = [3, 2, 0, 1], BWT = [11, 12,
+    0, 11], 4 levels (hi(12) + 1); level bits 1101 | 0010 | 0110 | 0110 (level
+    l+1 in the stable order of the top l+1 bits) = word 0x664B; alphabet {0,
+    11, 12} as an sd_vector of 13 bits (wl = 4 - 2 = 2: low [0, 3, 0], high
+    bits 0, 3, 5 of 7), C = [0, 1, 3, 4]."""
+    import struct
+
+    q = lambda v: struct.pack("<Q", v)      # noqa: E731
+    b = lambda v: struct.pack("<B", v)      # noqa: E731
+    i32 = lambda v: struct.pack("<I", v)    # noqa: E731
+    rank_word = sum(8 << (9 * j) for j in range(7))      # 8 ones in word 0: every in-block prefix is 8
+    mcl = lambda: q(8) + q(5) + b(5) + q(0) + q(0) + q(1) + b(1) + q(0)   # noqa: E731 -- 8 ones / 8 zeros
+    out = b"".join([
+        q(4), q(3),                                  # wt_int m_size, m_sigma
+        q(16), q(0x664B),                            # m_tree
+        q(128), q(0), q(rank_word),                  # m_tree_rank: m_basic_block
+        mcl(), mcl(),                                # m_tree_select1 / 0: superblock [0] w5, no mini_or_long, [0] w1
+        i32(4),                                      # m_max_level
+        q(3), b(3), q(3),                            # sa samples: [3]
+        q(3), b(3), q(2),                            # isa samples: [2]
+        q(13), b(2), q(6), b(2), q(0 | 3 << 2),      # m_char sd_vector: size, wl, m_low [0, 3, 0]
+        q(7), q(1 | 8 | 32),                         # m_high
+        q(3), q(3), b(1), q(0), q(0), q(1), b(1), q(0),   # high_1_select (3 ones at 0, 3, 5)
+        q(4), q(3), b(1), q(1), q(0), q(1), b(1), q(0),   # high_0_select (4 zeros from 1)
+        q(256), q(0), q(1), q(3), q(4),              # m_C
+        q(3),                                        # m_sigma
+    ])
+    return out
+
+
+def test_hand_assembled_fmi(tmp_path):
+    """A four-row file written byte by byte from the derivation: the reader
+    recovers n, the levels, the samples, the alphabet and the BWT; the test
+    writer produces the same bytes except the select structures it is free to
+    shape (the reader skips them)."""
+    import torch
+
+    from fmidx.sdsl_fmi import SdslCsaWtInt, decode_wt_int_device
+
+    p = str(tmp_path / "hand.fmi")
+    open(p, "wb").write(_hand_fmi_bytes())
+    f = SdslCsaWtInt(p)
+    assert (f.n, f.wt_sigma, f.max_level, f.sigma, f.alphabet_layout) == (4, 3, 4, 3, "sd_vector")
+    assert f.chars.tolist() == [0, 11, 12] and f.C.tolist() == [0, 1, 3, 4]
+    assert f.sa_samples.tolist() == [3] and f.isa_samples.tolist() == [2]
+    assert decode_wt_int_device(f.tree, 4, 4, torch.device("cpu")).tolist() == [11, 12, 0, 11]
+    w = str(tmp_path / "writer.fmi")
+    ref = write_csa_wt_int(w, np.array([11, 12, 11, 0]))
+    assert ref["sa"].tolist() == [3, 2, 0, 1] and ref["bwt"].tolist() == [11, 12, 0, 11]
+    g = SdslCsaWtInt(w)
+    assert g.tree.tolist() == f.tree.tolist() and g.chars.tolist() == f.chars.tolist()
+
+
+def test_wavelet_matrix_trailer_is_refused(tmp_path):
+    """wm_int's zero_cnt / rank_level after m_max_level (what round 3's reader
+    expected) are not part of wt_int: such a file does not parse."""
+    from fmidx.sdsl_fmi import SdslCsaWtInt, SdslFormatError
+
+    good = _hand_fmi_bytes()
+    cut = 8 + 8 + 16 + 24 + 2 * 53 + 4          # through m_max_level
+    trailer = (256).to_bytes(8, "little") + bytes(32) + (256).to_bytes(8, "little") + bytes(32)
+    p = str(tmp_path / "wm.fmi")
+    open(p, "wb").write(good[:cut] + trailer + good[cut:])
+    with pytest.raises(SdslFormatError):
+        SdslCsaWtInt(p)
 
 
 def test_contiguous_alphabet_and_corrupt_files(tmp_path):
@@ -60,7 +130,7 @@ def test_contiguous_alphabet_and_corrupt_files(tmp_path):
     p = str(tmp_path / "c.fmi")
     write_csa_wt_int(p, text)
     f = SdslCsaWtInt(p)
-    assert np.array_equal(f.comp2char, np.arange(5))
+    assert np.array_equal(f.comp2char, np.arange(5)) and f.alphabet_layout == "sd_vector"
     good = open(p, "rb").read()
     for name, bad in [("truncated", good[:-1]), ("trailing", good + b"\0"), ("header only", good[:16]),
                       ("empty", b""), ("n = 0", b"\0" * 8 + good[8:]),

@@ -67,6 +67,11 @@ class OracleShardFused(OracleShard):
             mask.copy_(torch.from_numpy(m))
         return mask
 
+    def shard_pack(self, lo, hi, bits, vocab, payload=None):
+        from fmidx.sharding import pack_payload_host
+
+        return pack_payload_host(lo.numpy(), hi.numpy(), self.ix._bwt, bits.numpy(), vocab)
+
 
 def make_case(seed=5):
     rng = np.random.default_rng(seed)
@@ -152,7 +157,7 @@ def _run(world, halo, reduce, fused=False):
 
 
 @pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("reduce", ["max_u8", "gather_bits"])
+@pytest.mark.parametrize("reduce", ["max_u8", "gather_bits", "sparse"])
 def test_sharded_or_equals_unsharded(reduce, fused):
     """fused: one decode_step per step (the packed all_gather ships int32 words)."""
     docs, patterns, steps = make_case()
