@@ -95,7 +95,10 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
                           uint64_t ld, const int64_t* fdf, uint64_t fdf_len, const float* pow_tab, uint64_t pow_len,
                           const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
                           fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
-                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s);
+                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s,
+                          int32_t* facts = nullptr, uint32_t* rowcase = nullptr);
+int launch_prep_finish(const fm_prep_config& cfg, uint64_t B, const int32_t* fsum, const uint32_t* rowcase,
+                       const float* pow_tab, uint64_t pow_len, fm_row_params* rows, uint32_t* status, hipStream_t s);
 }  // namespace fmidx
 
 using fmidx::set_error;
@@ -1178,6 +1181,49 @@ int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor
   // 3. scores + mask
   if (a->B && fmidx::launch_epilogue(a->dtype, a->scores, a->out, a->B, a->V, a->ld_scores, a->ld_out, a->bits,
                                      a->bits_ld, a->unigram_bits, a->rows, a->eos, s))
+    return -1;
+  return 0;
+  FM_API_END
+}
+
+int fm_processor_shard_prep(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* a, int32_t* d_facts,
+                            uint32_t* d_rowcase, void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  if (!cfg || !a || !d_facts || !d_rowcase) {
+    set_error("null config, arguments, facts or rowcase");
+    return -1;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // 1. row bookkeeping + this shard's ranges and facts
+  if (fmidx::launch_processor_step(h->idx.view, *cfg, a->ids, a->B, a->L, a->ld, a->fdf, a->fdf_len, a->pow_tab,
+                                   a->pow_len, a->prev_ids, a->prev_ld, a->prev_B, a->prev_state, a->rows, a->mask_lo,
+                                   a->mask_hi, a->state, a->status, a->ids_copy, a->copy_ld, true, s, d_facts,
+                                   d_rowcase))
+    return -1;
+  // 2. this shard's allowed bits of every searched row (to be ORed over the shards)
+  if (a->B && fmidx::launch_mask(h->idx.view, a->mask_lo, a->mask_hi, a->B, reinterpret_cast<uint8_t*>(a->bits),
+                                 a->bits_ld * 4, a->V, cfg->shift, 1, s))
+    return -1;
+  return 0;
+  FM_API_END
+}
+
+int fm_processor_shard_finish(const fm_prep_config* cfg, const fm_processor_args* a, const int32_t* d_facts_sum,
+                              const uint32_t* d_rowcase, const uint32_t* d_bits, uint64_t bits_ld, void* stream) {
+  FM_API_BEGIN
+  if (!cfg || !a) {
+    set_error("null config or arguments");
+    return -1;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (fmidx::launch_prep_finish(*cfg, a->B, d_facts_sum, d_rowcase, a->pow_tab, a->pow_len, a->rows, a->status, s))
+    return -1;
+  if (a->status_host) FM_HIP(hipMemcpyAsync(a->status_host, a->status, 16, hipMemcpyDeviceToHost, s));
+  if (a->status_event) FM_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(a->status_event), s));
+  if (a->B && fmidx::launch_epilogue(a->dtype, a->scores, a->out, a->B, a->V, a->ld_scores, a->ld_out, d_bits,
+                                     bits_ld, a->unigram_bits, a->rows, a->eos, s))
     return -1;
   return 0;
   FM_API_END

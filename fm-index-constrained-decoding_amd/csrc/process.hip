@@ -68,7 +68,8 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
                                              fm_row_params* __restrict__ rows, uint64_t* __restrict__ mlo,
                                              uint64_t* __restrict__ mhi, int64_t* __restrict__ state,
                                              uint32_t* __restrict__ status, int64_t* __restrict__ ids_copy,
-                                             uint64_t copy_ld) {
+                                             uint64_t copy_ld, int32_t* __restrict__ facts,
+                                             uint32_t* __restrict__ rowcase) {
   extern __shared__ int64_t srow[];   // STAGED: [npad] the row, then [4] its previous state
   const uint64_t row = blockIdx.x;
   const uint32_t lane = threadIdx.x;
@@ -105,6 +106,14 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
   uint32_t bad = 0;
   // remove_end_marker (causal_qwen.py:44-56): the tokens after the marker
   const bool hard = (cfg.flags & FM_PREP_HARD) != 0;
+  // FM_PREP_SHARD (a doc-range shard of the corpus): the index-dependent decisions of the soft
+  // variants -- count([last]) > 0, the pattern's range non-empty, its distinct set non-empty --
+  // are recorded as this shard's facts (facts [3][B]) with the row's case and pattern length
+  // (rowcase); fm_processor_shard_finish decides them from the facts summed over the shards
+  const bool shard = facts != nullptr;
+  uint32_t rcase = 0;          // 0: index-independent, 1: eos / pad last token, 2: pattern search
+  int64_t ls_case = 0;
+  int32_t f_cnt1 = 0, f_range = 0, f_dist = 0;
   const int64_t M = hard ? 0 : cfg.marker_len;
   int64_t first = -1;
   uint32_t hits = hard ? 1u : 0u;
@@ -192,6 +201,11 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
         // hard variants: no trailing n-gram rule, the eos / pad rule applies as is
         cnt1 = hard ? 1 : ((c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0);
         counted = true;
+        if (shard && !hard) {
+          rcase = 1;
+          ls_case = ls;
+          f_cnt1 = cnt1 > 0;
+        }
       }
       if (counted && cnt1 == 0) {
         ls = 0;
@@ -260,6 +274,13 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
         // a non-empty range implies count([last]) > 0; an empty one asks C
         // (the hard variants have no trailing n-gram rule)
         if (hi <= lo && !hard) cnt1 = (c >= 0 && (uint64_t)c <= v.max_sym) ? v.C[c + 1] - v.C[c] : 0;
+        if (shard && !hard) {   // this shard's facts; the decision below is provisional
+          rcase = 2;
+          ls_case = ls;
+          f_range = hi > lo;
+          f_cnt1 = hi > lo || cnt1 > 0;
+          f_dist = !(hi == lo || (hi - lo == 1 && v.bwt[lo] == 0));
+        }
         if (hi <= lo && !hard && cnt1 == 0) {
           ls = 0;
           lo = hi = 0;
@@ -280,7 +301,8 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
       p.flags = FM_ROW_UNIGRAM;
       p.v_uni = cfg.v_uni_full;
     } else if (kind == kSpecial || kind == kBits) {
-      p.v_dist = pow_at(pow_tab, pow_len, ls, bad);
+      // a shard's provisional decision must not flag a boost the summed facts may not need
+      p.v_dist = rcase ? 0.0f : pow_at(pow_tab, pow_len, ls, bad);
       bool empty = false;
       if (hard) {   // vllm.py:118-131: the distinct set only, on -inf
         p.flags = kind == kBits ? FM_ROW_BITS : FM_ROW_SPECIAL;
@@ -303,26 +325,91 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
   }
   if (lane == 0) {
     rows[row] = p;
-    const bool bits = kind == kBits && !forced;
+    // a shard's pattern rows keep their (possibly empty) local range: the bits of every shard
+    // are ORed, and an empty range stays empty under the next call's LF step
+    const bool searched = rcase == 2;
+    const bool bits = searched || (kind == kBits && !forced);
     mlo[row] = bits ? lo : 0;
     mhi[row] = bits ? hi : 0;
-    state[row] = pattern ? s0 : -1;
-    state[B + row] = pattern ? ls : -1;
+    state[row] = (pattern || searched) ? s0 : -1;
+    state[B + row] = searched ? ls_case : pattern ? ls : -1;
     state[2 * B + row] = (int64_t)lo;
     state[3 * B + row] = (int64_t)hi;
     if (bad) atomicOr(&status[0], bad);
+    if (shard) {
+      facts[row] = f_cnt1;
+      facts[B + row] = f_range;
+      facts[2 * B + row] = f_dist;
+      rowcase[row] = rcase | ((uint32_t)ls_case << 2);
+      // the longest searched pattern: the host checks it against the shards' halo
+      if (rcase == 2) atomicMax(&status[3], (uint32_t)(fdf_len + ls_case));
+    }
   }
 }
 
+// Phase 2 of a doc-sharded processor call: the rows whose decision depends on
+// the index (rowcase 1 / 2), decided from the shards' facts summed over the
+// ranks (> 0: some shard has it) exactly as k_prep decides them on one index.
+__global__ void __launch_bounds__(256) k_prep_finish(fm_prep_config cfg, uint64_t B, const int32_t* __restrict__ fsum,
+                                                     const uint32_t* __restrict__ rowcase,
+                                                     const float* __restrict__ pow_tab, uint64_t pow_len,
+                                                     fm_row_params* __restrict__ rows, uint32_t* __restrict__ status) {
+  const uint64_t row = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= B) return;
+  const uint32_t rc = rowcase[row];
+  const uint32_t c = rc & 3u;
+  if (!c) return;
+  const int64_t ls = (int64_t)(rc >> 2);
+  const bool g_cnt1 = fsum[row] > 0, g_range = fsum[B + row] > 0, g_dist = fsum[2 * B + row] > 0;
+  fm_row_params p = rows[row];
+  const uint32_t eosf = p.flags & FM_ROW_EOS;
+  uint32_t bad = 0;
+  p.special = 0;
+  p.v_dist = 0.0f;
+  if (c == 1 ? !g_cnt1 : (!g_range && !g_cnt1)) {   // count([last]) == 0: all unigrams
+    p.flags = FM_ROW_UNIGRAM | eosf;
+    p.v_uni = cfg.v_uni_full;
+  } else if (c == 1) {                               // eos / pad rule (stop_at_count is 0 here)
+    p.flags = FM_ROW_SPECIAL | FM_ROW_UNIGRAM | eosf;
+    p.special = cfg.pad;
+    p.v_dist = pow_at(pow_tab, pow_len, ls, bad);
+    p.v_uni = cfg.v_uni_half;
+  } else {
+    p.flags = FM_ROW_BITS | FM_ROW_UNIGRAM | eosf;
+    p.v_dist = pow_at(pow_tab, pow_len, ls, bad);
+    p.v_uni = (!g_dist && !(cfg.flags & FM_PREP_UNI_HALF)) ? cfg.v_uni_full : cfg.v_uni_half;
+  }
+  rows[row] = p;
+  if (bad) atomicOr(&status[0], bad);
+}
+
 }  // namespace
+
+int launch_prep_finish(const fm_prep_config& cfg, uint64_t B, const int32_t* fsum, const uint32_t* rowcase,
+                       const float* pow_tab, uint64_t pow_len, fm_row_params* rows, uint32_t* status, hipStream_t s) {
+  if (!B) return 0;
+  if (!fsum || !rowcase || !pow_tab || !rows || !status) {
+    set_error("processor shard finish: bad arguments");
+    return -1;
+  }
+  k_prep_finish<<<(unsigned)((B + 255) / 256), 256, 0, s>>>(cfg, B, fsum, rowcase, pow_tab, pow_len, rows, status);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
 
 int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int64_t* ids, uint64_t B, uint64_t L,
                           uint64_t ld, const int64_t* fdf, uint64_t fdf_len, const float* pow_tab, uint64_t pow_len,
                           const int64_t* prev_ids, uint64_t prev_ld, uint64_t prev_B, const int64_t* prev_state,
                           fm_row_params* rows, uint64_t* mlo, uint64_t* mhi, int64_t* state, uint32_t* status,
-                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s) {
+                          int64_t* ids_copy, uint64_t copy_ld, bool init_status, hipStream_t s, int32_t* facts,
+                          uint32_t* rowcase) {
   if (!(cfg.flags & FM_PREP_HARD) && (cfg.marker_len < 1 || cfg.marker_len > 8)) {
     set_error("processor step: marker length %d not in 1..8", cfg.marker_len);
+    return -1;
+  }
+  if (facts && (!rowcase || cfg.stop_at_count > 0)) {
+    // stop_at_count compares a count, and a shard's counts include its halo's duplicates
+    set_error("processor step over a shard: stop_at_count must be 0 (counts are not exact under sharding)");
     return -1;
   }
   if (ld < L || (fdf_len && !fdf) || !pow_tab || (prev_ids && !prev_state)) {
@@ -358,11 +445,11 @@ int launch_processor_step(const DevView& v, const fm_prep_config& cfg, const int
     const size_t lds = ((L + kStageBatch - 1) / kStageBatch * kStageBatch + 4) * sizeof(int64_t);
     k_prep<true><<<(unsigned)B, 64, lds, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
                                               prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status, ids_copy,
-                                              copy_ld);
+                                              copy_ld, facts, rowcase);
   } else {
     k_prep<false><<<(unsigned)B, 64, 0, s>>>(v, cfg, ids, B, L, ld, fdf, fdf_len, pow_tab, pow_len, prev_ids,
                                              prev_ld, prev_B, prev_state, rows, mlo, mhi, state, status, ids_copy,
-                                             copy_ld);
+                                             copy_ld, facts, rowcase);
   }
   FM_HIP(hipGetLastError());
   return 0;

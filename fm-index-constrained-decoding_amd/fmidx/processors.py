@@ -238,6 +238,114 @@ class _DeviceStep:
         return out if out.device == scores.device else out.to(scores.device)
 
 
+class _ShardedDeviceStep(_DeviceStep):
+    """A processor call over a doc-range shard (``fmidx.sharding.ShardedIndex``):
+    fm_processor_shard_prep on this rank's shard (the row bookkeeping, the
+    shard's ranges, the index-dependent facts and the shard's allowed bits),
+    the exchange (facts summed over the ranks, bits ORed -- the sparse or the
+    dense exchange), then fm_processor_shard_finish (the decisions from the
+    summed facts, the epilogue with the ORed bits).  Every rank returns the
+    same output, equal bit for bit to the unsharded processor's (SURVEY §8e:
+    masks, emptiness and count([last]) > 0 are exact under an OR).  ``prep`` /
+    ``finish`` are separate so that one process can drive several shards
+    (tests, the one-GPU rehearsal)."""
+
+    def __init__(self, core: "_BatchedCore", boost: float, lrf: float, fdf: Optional[List[int]]):
+        super().__init__(core, boost, lrf, fdf)
+        self.sidx = core.index
+        self.index = core.index.shard
+
+    def prep(self, input_ids, scores, cfg: _PrepConfig):
+        dev = self.dev
+        ids = input_ids if (input_ids.device == dev and input_ids.dtype == torch.int64
+                            and input_ids.is_contiguous()) else input_ids.to(dev, torch.int64).contiguous()
+        if ids.dim() != 2:
+            return None
+        B, Lt = ids.shape
+        if B != scores.shape[0] or B % max(1, cfg.num_beams):
+            return None
+        dtype = scores.dtype
+        if dtype not in _DTYPE_CODE:
+            raise TypeError(f"unsupported scores dtype {dtype}")
+        V = scores.shape[1]
+        src = scores if (scores.device == dev and scores.is_contiguous()) else scores.to(dev).contiguous()
+        out = torch.empty_like(src)
+        pow_t = self._pow_table(dtype, Lt + 1)
+        bufs = self._buffers(B, V)
+        if "facts" not in bufs or bufs["facts"].shape[1] != B:
+            bufs["facts"] = torch.empty((3, B), dtype=torch.int32, device=dev)
+            bufs["rowcase"] = torch.empty(B, dtype=torch.int32, device=dev)
+        cur, oth = self._cur, 1 - self._cur
+        keep = self._ids[cur]
+        if keep is None or keep.shape[0] != B or keep.shape[1] < Lt:
+            keep = torch.empty((B, max(Lt + 64, 2 * (keep.shape[1] if keep is not None else 0))), dtype=torch.int64,
+                               device=dev)
+            self._ids[cur] = keep
+        prev = self._ids[oth] if self._prev_ok else None
+        a = self._args
+        a.ids, a.B, a.L, a.ld = ids.data_ptr(), B, Lt, Lt
+        a.fdf, a.fdf_len = self.fdf.data_ptr(), self.fdf_len
+        a.pow_tab, a.pow_len = pow_t.data_ptr(), pow_t.numel()
+        if prev is not None:
+            a.prev_ids, a.prev_ld, a.prev_B, a.prev_state = prev.data_ptr(), prev.stride(0), prev.shape[0], \
+                self._state[oth].data_ptr()
+        else:
+            a.prev_ids, a.prev_ld, a.prev_B, a.prev_state = None, 0, 0, None
+        a.rows, a.mask_lo, a.mask_hi = bufs["rows"].data_ptr(), bufs["mlo"].data_ptr(), bufs["mhi"].data_ptr()
+        a.state, a.status = self._state[cur].data_ptr(), self.status.data_ptr()
+        a.bits, a.bits_ld = bufs["bits"].data_ptr(), bufs["words"]
+        a.dtype = _DTYPE_CODE[dtype]
+        a.scores, a.out, a.V, a.ld_scores, a.ld_out = src.data_ptr(), out.data_ptr(), V, src.stride(0), out.stride(0)
+        a.unigram_bits = self.core.unigram_bits(V, dev).data_ptr()
+        a.eos = int(cfg.eos)
+        a.ids_copy, a.copy_ld = keep.data_ptr(), keep.stride(0)
+        stream = torch.cuda.current_stream(dev)
+        check(lib().fm_processor_shard_prep(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
+                                            c_void_p(bufs["facts"].data_ptr()), c_void_p(bufs["rowcase"].data_ptr()),
+                                            c_void_p(stream.cuda_stream)), "processor_shard_prep")
+        return {"out": out, "B": B, "V": V, "facts": bufs["facts"], "rowcase": bufs["rowcase"], "bits": bufs["bits"],
+                "mlo": bufs["mlo"], "mhi": bufs["mhi"], "cfg": cfg, "scores_device": scores.device}
+
+    def finish(self, h, facts_sum, bits_or):
+        """The decisions from the summed facts and the epilogue with the ORed
+        bits (int32 [B, >= ceil(V/32)]); None when the call needs the host
+        path (end markers, boost overflow) -- not available over a shard."""
+        from .sharding import HaloExceeded
+
+        a = self._args
+        stream = torch.cuda.current_stream(self.dev)
+        a.status_host = self.status_h.data_ptr()
+        if not self._ev_ready:
+            self._ev.record(stream)
+            self._ev_ready = True
+        a.status_event = self._ev.cuda_event
+        check(lib().fm_processor_shard_finish(ctypes.byref(h["cfg"]), ctypes.byref(a),
+                                              c_void_p(facts_sum.data_ptr()), c_void_p(h["rowcase"].data_ptr()),
+                                              c_void_p(bits_or.data_ptr()), bits_or.stride(0),
+                                              c_void_p(stream.cuda_stream)), "processor_shard_finish")
+        self._ev.synchronize()
+        st = self._status_np
+        if st[0] != 0 or st[1] != st[2]:
+            self._prev_ok = False
+            return None
+        halo = self.sidx.halo
+        if halo is not None and int(st[3]) > halo - 1:
+            self._prev_ok = False
+            raise HaloExceeded(f"a pattern of {int(st[3])} tokens (force_decoding_from included) needs a halo of "
+                               f">= {int(st[3]) + 1}; the shards were built with {halo}")
+        self._cur, self._prev_ok = 1 - self._cur, True
+        out = h["out"]
+        return out if out.device == h["scores_device"] else out.to(h["scores_device"])
+
+    def __call__(self, input_ids, scores, cfg: _PrepConfig, wait: bool = True):
+        h = self.prep(input_ids, scores, cfg)
+        if h is None:
+            return None
+        facts = self.sidx.sum_facts(h["facts"])
+        bits = self.sidx.or_bits(h["mlo"], h["mhi"], h["bits"], h["V"])
+        return self.finish(h, facts, bits)
+
+
 class _BatchedCore:
     """Shared machinery: batched ranges, packed allowed bits, fused epilogue."""
 
@@ -339,9 +447,13 @@ class _BatchedCore:
 
 def _device_step(core, boost, lrf, fdf):
     """The device path when the index is this engine's GPU index (its
-    handle), else None (e.g. an oracle index in the CPU tests)."""
+    handle) or a doc-range shard of one (sharding.ShardedIndex), else None
+    (e.g. an oracle index in the CPU tests)."""
     from .fm_index import FMIndex as _Engine
+    from .sharding import ShardedIndex
 
+    if isinstance(core.index, ShardedIndex):
+        return _ShardedDeviceStep(core, boost, lrf, fdf)
     if not isinstance(core.index, _Engine) or not torch.cuda.is_available():
         return None
     return _DeviceStep(core, boost, lrf, fdf)

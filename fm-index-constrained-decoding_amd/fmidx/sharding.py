@@ -252,6 +252,82 @@ class ShardedDecoder:
         return unpack_bits(acc, self.vocab)
 
 
+class ShardedIndex:
+    """This rank's doc-range shard as the ``index`` of the logits processors
+    (fmidx.processors), so the reference's processors run over a corpus
+    sharded across GPUs: each call runs the row bookkeeping and
+    the pattern search on the shard, sums the shards' facts (count([last]) >
+    0, range and distinct set non-empty) and ORs their allowed bits over
+    ``group`` (RCCL), then decides and applies the boosts -- the same output
+    on every rank, bit for bit the unsharded processor's.
+
+    ``shard``: this rank's engine FMIndex (built from ``shard_text_device`` /
+    ``shard_corpus`` with ``halo``).  ``occurring_distinct``: the WHOLE
+    corpus's all-unigram list (index.py:67 -- it excludes BWT row n - 1 of
+    the unsharded index, so it is not the union of the shards' lists; take it
+    from the corpus's index metadata).  ``exchange``: "sparse" (per row the
+    shard's BWT slice or bitmap) or "dense" (every row's bitmap).  A pattern
+    longer than ``halo`` - 1 tokens raises HaloExceeded; stop_at_count must
+    be 0 (counts include halo duplicates), and inputs that need the host path
+    (rows without exactly one end marker, boost overflow) raise.  The
+    ``index.py`` query surface (get_range, distinct, ...) is the unsharded
+    index's business and is not offered here."""
+
+    def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "sparse",
+                 shift: int = 10):
+        if exchange not in ("sparse", "dense"):
+            raise ValueError(exchange)
+        self.shard = shard
+        self.occurring_distinct = list(occurring_distinct)
+        self.group = group
+        self.halo = halo
+        self.exchange = exchange
+        self.shift = shift
+        self._payload = None
+        self._parts = None
+
+    @property
+    def device(self) -> int:
+        return self.shard.device
+
+    def sum_facts(self, facts):
+        """SUM of every rank's int32 facts (in place)."""
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(facts, op=dist.ReduceOp.SUM, group=self.group)
+        return facts
+
+    def or_bits(self, lo, hi, bits, vocab: int):
+        """OR of every rank's packed allowed bits (int32 [B, W]) -> int32 [B, W]."""
+        if self.group is None:
+            return bits
+        import torch
+        import torch.distributed as dist
+
+        B, W = lo.numel(), (vocab + 31) // 32
+        if self.exchange == "sparse":
+            self._payload = self.shard.shard_pack(lo, hi, bits, vocab, payload=self._payload)
+            parts, _ = gather_payloads(self._payload, self.group)
+            return or_payloads(parts, B, vocab, self.shift, unpack=False)
+        world = dist.get_world_size(self.group)
+        mine = bits[:, :W].contiguous()
+        if self._parts is None or self._parts.shape != (world, B, W):
+            self._parts = torch.empty((world, B, W), dtype=torch.int32, device=bits.device)
+        dist.all_gather_into_tensor(self._parts, mine, group=self.group)
+        return or_bits(self._parts, vocab, unpack=False)
+
+    def _no_host_path(self, *a, **k):
+        raise NotImplementedError("this call needs the processors' host path (a row without exactly one end "
+                                  "marker, or a boost outside the float range), which a doc-sharded index cannot run")
+
+    get_range_batch = _no_host_path
+    allowed_mask = _no_host_path
+
+    def size(self) -> int:
+        return self.shard.size()
+
+
 def payload_capacity(B: int, vocab: int) -> int:
     """Worst-case uint32 words of a sparse-exchange payload of B rows."""
     from .fm_index import payload_capacity as _cap
@@ -409,5 +485,6 @@ def unpack_bits(packed, vocab: int):
 
 
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
+           "ShardedIndex",
            "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "gather_payloads", "or_payloads",
            "pack_payload_host", "or_payloads_host"]

@@ -379,6 +379,31 @@ typedef struct fm_processor_args {
 
 int fm_processor_call(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* args, void* stream);
 
+/* A processor call over a doc-range SHARD of the corpus (masks,
+ * emptiness and count([last]) > 0 are exact under an OR over the shards), in
+ * two phases around the caller's exchange:
+ *   fm_processor_shard_prep (every rank, on its shard): fm_processor_step with
+ *   the index-dependent decisions recorded instead of taken -- d_facts int32
+ *   [3][B] = this shard's (count([last]) > 0, pattern range non-empty, distinct
+ *   set non-empty) as 0/1, d_rowcase [B] = the row's case (0: decided without
+ *   the index, 1: eos / pad last token, 2: pattern searched) | pattern length
+ *   << 2 -- then the shard's packed allowed bits of every searched row into
+ *   args->bits.  args->status [3] receives the longest searched pattern
+ *   (force_decoding_from included), to be checked against the shards' halo.
+ *   The caller sums d_facts over the ranks (all_reduce SUM) and ORs the bits
+ *   (fm_or_bits / the sparse exchange).
+ *   fm_processor_shard_finish: decides those rows from the sums exactly as
+ *   fm_processor_step decides them on one index, copies the status (+ event,
+ *   as fm_processor_call), and runs the epilogue with the ORed bits (d_bits,
+ *   bits_ld words per row).
+ * stop_at_count must be 0 (a shard's counts include its halo's duplicates;
+ * every reference call site passes 0).  No index is needed for the finish. */
+#define FM_PREP_BAD_HALO 4u    /* status (host side): a pattern longer than the shards' halo allows */
+int fm_processor_shard_prep(fm_index* h, const fm_prep_config* cfg, const fm_processor_args* args, int32_t* d_facts,
+                            uint32_t* d_rowcase, void* stream);
+int fm_processor_shard_finish(const fm_prep_config* cfg, const fm_processor_args* args, const int32_t* d_facts_sum,
+                              const uint32_t* d_rowcase, const uint32_t* d_bits, uint64_t bits_ld, void* stream);
+
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
 /* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip

@@ -1,0 +1,174 @@
+"""The logits processors over a doc-range sharded corpus (BASELINE
+configs[3]) on ONE GPU: the 8 shards of a corpus (halo 64) are built side by
+side, one processor per shard (fmidx.sharding.ShardedIndex, no process
+group), and every call is driven as the 8 ranks would run it -- each shard's
+fm_processor_shard_prep, the facts summed and the allowed bits ORed (the dense
+exchange and the sparse one, which must agree), each shard's
+fm_processor_shard_finish -- against the unsharded processor of the same class
+(device path) and its host path, bit for bit, over generations with beam
+reordering, eos / pad rows, think / system tokens, force_decoding_from and
+always_allow_eos.  Every shard must return the same output."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+WORLD, HALO, V = 8, 64, 128256
+
+
+def _corpus(seed):
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(600):
+        ln = int(rng.integers(20, 400))
+        tok = int(rng.integers(0, 2000))
+        d = []
+        for _ in range(ln):
+            d.append(tok)
+            tok = (tok * 31 + 7) % 2000 if rng.random() < 0.6 else int(rng.integers(0, 2000))
+        docs.append(d)
+    for d in docs[::5]:                 # a phrase shared by many docs: wide ranges on every shard
+        d[:5] = [3, 4, 5, 6, 7]
+    return docs
+
+
+@pytest.fixture(scope="module")
+def indexes():
+    import os
+
+    from fmidx.index import FMIndex
+    from fmidx.sharding import shard_corpus
+
+    docs = _corpus(3)
+    old = {k: os.environ.get(k) for k in ("FMIDX_CACHE_MIN", "FMIDX_BM_LOG2")}
+    os.environ.update({"FMIDX_CACHE_MIN": "8", "FMIDX_BM_LOG2": "6"})   # cache / transitions / hierarchy exist
+    try:
+        full = FMIndex()
+        full.initialize(docs, in_memory=True)
+        shards = []
+        for r in range(WORLD):
+            sd, _ = shard_corpus(docs, WORLD, r, HALO)
+            ix = FMIndex()
+            ix.initialize(sd, in_memory=True)
+            shards.append(ix)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert full.stats()["cache_nodes"] > 1
+    return docs, full, shards
+
+
+def _drive(procs, ids, scores):
+    """One call of the sharded processors as WORLD ranks would run it."""
+    from fmidx.sharding import or_bits, or_payloads
+
+    cfgs = [p._prep_config(scores.dtype) for p in procs]
+    hs = [p._dev.prep(ids, scores, c) for p, c in zip(procs, cfgs)]
+    facts = torch.stack([h["facts"] for h in hs]).sum(0).to(torch.int32).contiguous()
+    B, Vs = hs[0]["B"], hs[0]["V"]
+    W = (Vs + 31) // 32
+    dense = or_bits(torch.stack([h["bits"][:, :W] for h in hs]).contiguous(), Vs, unpack=False)
+    pays = [p._dev.index.shard_pack(h["mlo"], h["mhi"], h["bits"], Vs) for p, h in zip(procs, hs)]
+    pays = [q[:int(q[0].item())] for q in pays]
+    m = max(q.numel() for q in pays)
+    parts = torch.zeros((len(pays), m), dtype=torch.int32, device=ids.device)
+    for r, q in enumerate(pays):
+        parts[r, :q.numel()] = q
+    sparse = or_payloads(parts, B, Vs, 10, unpack=False)
+    assert torch.equal(dense, sparse)
+    outs = [p._dev.finish(h, facts.clone(), sparse) for p, h in zip(procs, hs)]
+    for o in outs[1:]:
+        assert torch.equal(o.view(torch.int16 if o.dtype != torch.float32 else torch.int32),
+                           outs[0].view(torch.int16 if o.dtype != torch.float32 else torch.int32))
+    return outs[0]
+
+
+@pytest.mark.parametrize("variant", ["qwen", "causal", "seq"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sharded_processors_equal_unsharded(indexes, variant, dtype):
+    import fmidx.processors as P
+    from fmidx.sharding import ShardedIndex
+
+    docs, full, shards = indexes
+    occ = full.occurring_distinct
+    rng = np.random.default_rng(101)
+    F = [t for d in reversed(docs) for t in d]
+    beams, groups = 4, 8
+    B = beams * groups
+    iv = torch.int32 if dtype == torch.float32 else torch.int16
+    marker = [151645, 198, 151644, 77091, 198] if variant == "qwen" else [78191, 128007, 271]
+    think = [151667, 271, 151668, 271]
+    for cfg in range(2):
+        kw = dict(num_beams=beams, pad_token_id=0, eos_token_id=2,
+                  force_decoding_from=[F[11], F[12]] if cfg == 1 else None,
+                  always_allow_eos=cfg == 1)
+        if variant == "qwen":
+            mk = lambda index: P.QwenIndexBasedLogitsProcessor(index=index, min_new_tokens=3,  # noqa: E731
+                                                               length_reward_factor=1.5, **kw)
+        elif variant == "causal":
+            mk = lambda index: P.CausalIndexBasedLogitsProcessor(index=index, model_name="llama-3",  # noqa: E731
+                                                                 length_reward_factor=1.5, **kw)
+        else:
+            mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, **kw)  # noqa: E731
+        ref_p, host_p = mk(full), mk(full)
+        host_p._dev = None
+        procs = [mk(ShardedIndex(s, occ, halo=HALO)) for s in shards]
+        assert all(type(p._dev).__name__ == "_ShardedDeviceStep" for p in procs)
+        starts = rng.integers(0, len(F) - 80, size=B)
+        if variant == "seq":
+            prompt, sents = [], [[1] for _ in range(B)]           # the decoder start token
+        else:
+            prompt = [int(x) for x in rng.integers(100, 200, size=4)] + marker
+            sents = [[] for _ in range(B)]
+            if variant == "qwen":
+                for b in range(B):
+                    sents[b] = [list(think), [5, 6, 151668, 271], [5, 6, 7, 8]][b % 3]
+        for step in range(8):
+            perm = np.concatenate([g * beams + rng.permutation(beams) for g in range(groups)])
+            sents = [list(sents[i]) for i in perm]
+            starts = starts[perm]
+            for b in range(B):
+                r = rng.random()
+                if r < 0.78:
+                    sents[b].append(F[(int(starts[b]) + len(sents[b])) % len(F)])
+                elif r < 0.86:
+                    sents[b].append(int(rng.integers(0, 2000)))
+                elif r < 0.9:
+                    sents[b].append(2)
+                elif r < 0.93:
+                    sents[b].append(0)
+                else:
+                    sents[b].append(int(rng.integers(5000, 6000)))      # never in the corpus
+            ids = torch.tensor([prompt + s for s in sents], dtype=torch.int64).cuda()
+            scores = torch.from_numpy(rng.standard_normal((B, V)).astype(np.float32)).to(dtype).cuda()
+            want = ref_p(ids, scores.clone())
+            host = host_p(ids, scores.clone())
+            got = _drive(procs, ids, scores.clone())
+            assert torch.equal(want.view(iv), host.view(iv)), (variant, cfg, step, "device vs host")
+            assert torch.equal(got.view(iv), want.view(iv)), (variant, cfg, step)
+        assert all(p._dev.prev_ids is not None for p in procs)     # the incremental state was kept
+
+
+def test_sharded_processor_guards(indexes):
+    """A pattern longer than the halo allows raises HaloExceeded; stop_at_count
+    (a count, inflated by halo duplicates) is refused."""
+    import fmidx.processors as P
+    from fmidx import FMIndexError
+    from fmidx.sharding import HaloExceeded, ShardedIndex
+
+    docs, full, shards = indexes
+    occ = full.occurring_distinct
+    F = [t for d in reversed(docs) for t in d]
+    ids = torch.tensor([[1] + F[100:100 + HALO + 2]], dtype=torch.int64).cuda()
+    scores = torch.zeros((1, V), dtype=torch.float32).cuda()
+    procs = [P.SeqIndexBasedLogitsProcessor(index=ShardedIndex(s, occ, halo=HALO), num_beams=1) for s in shards]
+    with pytest.raises(HaloExceeded):
+        _drive(procs, ids, scores)
+    procs = [P.SeqIndexBasedLogitsProcessor(index=ShardedIndex(s, occ, halo=HALO), num_beams=1, stop_at_count=2)
+             for s in shards]
+    with pytest.raises(FMIndexError):
+        _drive(procs, ids[:, :5], scores)
