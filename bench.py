@@ -368,6 +368,12 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
         hi = hi_all[warmup - 1].copy()
         one_step(mode, warmup, lo, hi, mask, threads)          # untimed warm-up step
         state[(mode, threads)] = (lo, hi, mask, lo.copy(), hi.copy(), [])
+    # the part of a single-thread step that is distinct_count (fm_index.cpp:119-144: three
+    # sigma-sized zeroed vectors + the interval_symbols DFS): the same window's ranges -- the ones
+    # each step's LF produced, which the incremental leg enumerates -- timed as a fifth leg in the
+    # same interleaving, so it is a part of the same work as the whole steps it is compared with
+    ref.distinct_only(lo_all[warmup], hi_all[warmup], 1)       # untimed warm-up, like the legs
+    dts = []
     for _ in range(reps):
         for key in names:
             lo, hi, mask, lo_w, hi_w, rates = state[key]
@@ -377,6 +383,10 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
             for s in range(first, last + 1):
                 one_step(key[0], s, lo, hi, mask, key[1])
             rates.append(window * B / (time.perf_counter() - a))
+        a = time.perf_counter()
+        for s in range(first, last + 1):
+            ref.distinct_only(lo_all[s], hi_all[s], 1)
+        dts.append((time.perf_counter() - a) / window)
     legs = {}
     for (mode, threads), (lo, hi, mask, _, _, rates) in state.items():
         ok = bool(np.array_equal(lo, lo_all[last]) and np.array_equal(hi, hi_all[last]))
@@ -389,14 +399,6 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
             "steps": window, "ranges_match_gpu": ok, "masks_match_gpu": mok}
         log(f"cpu {mode} x{threads}: median {med:.0f} masks/s ({min(rates):.0f}-{max(rates):.0f}) over "
             f"{reps} x {window} steps; ranges ok {ok}, masks ok {mok}")
-    # where a single-thread step goes: distinct_count (fm_index.cpp:119-144: three sigma-sized
-    # zeroed vectors + the interval_symbols DFS) of the window's last ranges alone, vs the legs'
-    # whole steps -- the searches of either mode are a small part of a step
-    dts = []
-    for _ in range(3):
-        a = time.perf_counter()
-        ref.distinct_only(lo_all[last], hi_all[last], 1)
-        dts.append(time.perf_counter() - a)
     per_step = {"distinct_count_only": float(np.median(dts)),
                 "incremental": B / legs["incremental_1"]["value"],
                 "full_research": B / legs["full_research_1"]["value"]}
@@ -806,6 +808,7 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=5, help="CPU baseline: repetitions per leg (median reported)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the gather-ceiling probe")
+    ap.add_argument("--no-rank21", action="store_true", help="skip the 2^21-pair rank leg")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the doc-range sharded leg")
     ap.add_argument("--sharded-at-1", action="store_true",
                     help="run the sharded leg at N = 1 too (one shard; exercises the path on a one-GPU box)")
@@ -872,6 +875,9 @@ def main():
     # rank throughput at scale: RS_ROWS x (RS_STEPS - 1) independent (state,
     # token) pairs of a wider trace, for one k_lf launch (the grouped kernel)
     rs_tok, rs_lo, rs_hi, rs_ref = rank_pairs(fm, text, bwt, V, args.seed + 17 + rank, dev)
+    # ... and 2^21 pairs (4 x the rows), where the library picks the in-wave sweep (query.hip LfTuning)
+    r2_tok, r2_lo, r2_hi, r2_ref = (rank_pairs(fm, text, bwt, V, args.seed + 19 + rank, dev, rows=4 * 65536)
+                                    if not args.no_rank21 else (None, None, None, None))
     want_sharded = (world > 1 and not args.no_sharded) or args.sharded_at_1
     want_c4 = world == 1 and not args.no_c4 and not args.sharded_at_1 and n > 2e9 and args.corpus == "markov"
     sh = shard_trace(fm, text, bwt, B, V, S, dev) if (want_sharded or want_c4) else None
@@ -978,6 +984,18 @@ def main():
         fm.lf_step_batch(rs_tok, rs_lo, rs_hi, SHIFT, lo_out=rs_olo, hi_out=rs_ohi, reset_below=0)
     rs_cold = timed(g_rs, 3, cold=True)
     rs_ok = bool(torch.equal(rs_olo, rs_ref[0]) and torch.equal(rs_ohi, rs_ref[1]))
+    r2 = None
+    if r2_tok is not None:
+        r2_olo, r2_ohi = torch.empty_like(r2_lo), torch.empty_like(r2_hi)
+        g_r2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_r2):
+            fm.lf_step_batch(r2_tok, r2_lo, r2_hi, SHIFT, lo_out=r2_olo, hi_out=r2_ohi, reset_below=0)
+        r2_cold = timed(g_r2, 3, cold=True)
+        r2_warm = timed(g_r2, 3)
+        r2 = {"rows": int(r2_tok.numel()), "avg_launch_us_cold": float(np.median(r2_cold)) * 1e3,
+              "avg_launch_us_warm": float(np.median(r2_warm)) * 1e3,
+              "matches_decode_kernel": bool(torch.equal(r2_olo, r2_ref[0]) and torch.equal(r2_ohi, r2_ref[1]))}
+        del g_r2, r2_olo, r2_ohi
     mask_ms = [t / K for t in timed(g_mask, 5)]
     packed_cold = None
     if g_packed is not None:
@@ -1067,6 +1085,16 @@ def main():
                                    "lf").sum())
     rs_us = float(np.median(rs_cold)) * 1e3
     rank_gbs_scale = rs_bytes / (rs_us * 1e-6) / 1e9
+    if r2 is not None:
+        r2_pc = fm.cache_contains(r2_lo, r2_hi).cpu().numpy()
+        r2["alg_bytes_per_launch"] = float(lf_plan_bytes(r2_lo.cpu().numpy(), r2_hi.cpu().numpy(),
+                                                         r2_tok.cpu().numpy(), n, r2_pc, st, "lf").sum())
+        r2["rank_GBps"] = r2["alg_bytes_per_launch"] / (r2["avg_launch_us_cold"] * 1e-6) / 1e9
+        r2["frac_of_peak"] = r2["rank_GBps"] / HBM_PEAK_GBS
+        r2["lf_steps_per_s"] = r2["rows"] / (r2["avg_launch_us_cold"] * 1e-6)
+        r2["kernel"] = "k_lf_sweep<true> (in-wave tail rows), chosen by the library from 2^20 rows"
+        log(f"rank at 2^21 pairs: {r2['avg_launch_us_cold']:.1f}us cold ({r2['avg_launch_us_warm']:.1f} warm), "
+            f"{r2['rank_GBps']:.0f} GB/s, {r2['lf_steps_per_s'] / 1e9:.1f} G steps/s, exact {r2['matches_decode_kernel']}")
     gather_gbs, chase_ns, gather_modes = (None, None, None)
     if not args.no_gather:
         gather_gbs, chase_ns, gather_modes = gather_ceiling(dev)
@@ -1177,7 +1205,8 @@ def main():
                  "gather_ceiling_by_shape_GBps": gather_modes,
                  "frac_of_gather_ceiling": (rank_gbs_scale / gather_gbs) if gather_gbs else None,
                  "lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6),
-                 "b256_GBps": rank_gbs, "b256_avg_launch_us_cold": lf_us_cold},
+                 "b256_GBps": rank_gbs, "b256_avg_launch_us_cold": lf_us_cold,
+                 "pairs_2_21": r2},
     }
     # PMC traffic (tools/pmc_traffic.sh) is collected in a separate rocprofv3 run and committed;
     # it is used only when it was counted on this very library build, config and mask layout

@@ -114,6 +114,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
   uint32_t rcase = 0;          // 0: index-independent, 1: eos / pad last token, 2: pattern search
   int64_t ls_case = 0;
   int32_t f_cnt1 = 0, f_range = 0, f_dist = 0;
+  int64_t searched_len = 0;    // force_decoding_from + sent of a searched row (the halo check)
   const int64_t M = hard ? 0 : cfg.marker_len;
   int64_t first = -1;
   uint32_t hits = hard ? 1u : 0u;
@@ -216,6 +217,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
         // the range of force_decoding_from + sent: one LF step from the previous
         // call's range of a row (same beam group) whose pattern is this one's
         // pattern without its last token, else a full search
+        searched_len = (int64_t)fdf_len + ls;
         bool found = false;
         uint64_t pw = 0;   // count of the pattern without its last token (the hard variants' stop rule)
         if (prev_ids && ls >= 2) {
@@ -342,7 +344,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
       facts[2 * B + row] = f_dist;
       rowcase[row] = rcase | ((uint32_t)ls_case << 2);
       // the longest searched pattern: the host checks it against the shards' halo
-      if (rcase == 2) atomicMax(&status[3], (uint32_t)(fdf_len + ls_case));
+      if (searched_len) atomicMax(&status[3], (uint32_t)searched_len);
     }
   }
 }

@@ -1338,8 +1338,13 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 //    k_lf_cheap (every row but the wide ones: 36 VGPRs, 8 waves per SIMD) then
 //    k_lf_wide (the wide rows only).  Exact, but slower at C3: 2^19 cold pairs
 //    98.4 vs 76.0 us (the second pass still steps wide rows a few per wave).
-//  * FMIDX_LF_WORK (default 0): 1 / 2 = the worklist sweeps above (k_lf_sweep
-//    + k_lf_tail, or tail rows in-wave); exact, not faster cold.
+//  * FMIDX_LF_WORK: 0 = the grouped kernel only, 1 / 2 = the worklist sweeps
+//    above (k_lf_sweep + k_lf_tail, or tail rows in-wave); unset = chosen by
+//    the launch's row count: the in-wave sweep from FMIDX_LF_SWEEP_MIN rows
+//    (default 2^20), the grouped kernel below.  Measured on the C3 index, cold
+//    / warm us (profiles/r03_rank/worklist/): 2^19 pairs 71.8 / 60.9 grouped vs
+//    76.6 / 47.7 in-wave; 2^20 126.6 / 109.5 vs 123.0 / 77.6; 2^21 216.4 / 202.4
+//    vs 177.6 / 140.2 -- the in-wave sweep wins cold from 2^20 rows on.
 struct LfTuning {
   uint32_t G;
   uint32_t Gs;   // get_range
@@ -1349,6 +1354,7 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
+  uint64_t sweep_min; // work_inline from this many rows (FMIDX_LF_WORK unset: 2^20; set: min_rows)
   bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
 
@@ -1362,8 +1368,11 @@ LfTuning load_lf_tuning() {
   t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
   t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
   t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
-  t.work = env_u32("FMIDX_LF_WORK", 0) == 1;
-  t.work_inline = env_u32("FMIDX_LF_WORK", 0) == 2;
+  const char* w = std::getenv("FMIDX_LF_WORK");
+  const bool autow = !w || !*w;
+  t.work = !autow && env_u32("FMIDX_LF_WORK", 0) == 1;
+  t.work_inline = autow || env_u32("FMIDX_LF_WORK", 0) == 2;
+  t.sweep_min = autow ? env_u32("FMIDX_LF_SWEEP_MIN", 1u << 20) : 0;
   t.search_p8 = env_u32("FMIDX_SEARCH_P8", 1) != 0;
   return t;
 }
@@ -1398,7 +1407,8 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s, void* ws) {
   if (m == 0) return 0;
-  if (m > lf_tuning().min_rows && lf_tuning().work_inline) {   // one launch, tail rows stepped in-wave
+  if (m > lf_tuning().min_rows && m >= lf_tuning().sweep_min && lf_tuning().work_inline) {
+    // one launch, tail rows stepped in-wave
     const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
     k_lf_sweep<true><<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, nullptr,
                                                nullptr, 0);

@@ -338,28 +338,38 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   }
   __syncthreads();
   const uint32_t nd = s_nd;
+  const uint32_t total = s_pre[nparts];
+  // the first batch of sparse symbols (4 per thread) is loaded together with the dense words:
+  // both depend only on the staged (desc, off), so the row costs one data round trip
+  auto sym_at = [&](uint32_t i) -> uint32_t {
+    uint32_t p = 0;                                     // the part whose list holds flat index i
+    for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
+      if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
+    return parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
+  };
+  uint32_t sym0[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrRowThreads + t, total - 1)) : 0u;
   constexpr int kSlots = kOrRowMaxWords / kOrRowThreads;
   uint32_t acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0u;
-  if (nd) {
-    for (uint32_t j0 = 0; j0 < nd; j0 += 4) {
-      const uint32_t* src[4];
+  for (uint32_t j0 = 0; j0 < nd; j0 += 4) {
+    const uint32_t* src[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
-        src[q] = parts + (uint64_t)p * stride + s_off[p];
-      }
-      uint32_t x[4][kSlots];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < kSlots; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W - 1)];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < kSlots; ++k) acc[k] |= x[q][k];
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
+      src[q] = parts + (uint64_t)p * stride + s_off[p];
     }
+    uint32_t x[4][kSlots];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W - 1)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] |= x[q][k];
   }
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) {
@@ -367,18 +377,16 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     if (w < W) s_bits[w] = acc[k];
   }
   __syncthreads();
-  const uint32_t total = s_pre[nparts];
-  for (uint32_t i0 = 0; i0 < total; i0 += 4 * kOrRowThreads) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t tok = (int64_t)sym0[u] - shift;
+    if (u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+      atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+  }
+  for (uint32_t i0 = 4 * kOrRowThreads; i0 < total; i0 += 4 * kOrRowThreads) {   // long lists (rare)
     uint32_t sym[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t i = min(i0 + u * kOrRowThreads + t, total - 1);
-      uint32_t p = 0;                                   // the part whose list holds flat index i
-      for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
-        if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
-      while (p + 1 < nparts && s_pre[p + 1] <= i) ++p;    // parts with empty lists
-      sym[u] = parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
-    }
+    for (int u = 0; u < 4; ++u) sym[u] = sym_at(min(i0 + u * kOrRowThreads + t, total - 1));
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t tok = (int64_t)sym[u] - shift;
