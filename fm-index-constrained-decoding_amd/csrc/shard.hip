@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
                                                             int unpack) {
-  extern __shared__ uint32_t s_bits[];   // [W]
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
   __shared__ uint32_t s_desc[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
   __shared__ uint32_t s_nd;
   const uint64_t b = blockIdx.x;
@@ -350,31 +350,39 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   uint32_t sym0[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrRowThreads + t, total - 1)) : 0u;
-  constexpr int kSlots = kOrRowMaxWords / kOrRowThreads;
-  uint32_t acc[kSlots];
+  // dense parts: thread t owns words [4 (t + 1024 k), + 4) -- 16-B loads (a dense row's data
+  // starts on a 4-word boundary and is zero-padded to 4 words), four parts in flight at a time
+  constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);
+  const uint32_t W4 = (W + 3) / 4;
+  uint4 acc[kSlots4];
 #pragma unroll
-  for (int k = 0; k < kSlots; ++k) acc[k] = 0u;
+  for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
   for (uint32_t j0 = 0; j0 < nd; j0 += 4) {
-    const uint32_t* src[4];
+    const uint4* src[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
-      src[q] = parts + (uint64_t)p * stride + s_off[p];
+      src[q] = reinterpret_cast<const uint4*>(parts + (uint64_t)p * stride + s_off[p]);
     }
-    uint32_t x[4][kSlots];
+    uint4 x[4][kSlots4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int k = 0; k < kSlots; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W - 1)];
+      for (int k = 0; k < kSlots4; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W4 - 1)];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int k = 0; k < kSlots; ++k) acc[k] |= x[q][k];
+      for (int k = 0; k < kSlots4; ++k) {
+        acc[k].x |= x[q][k].x;
+        acc[k].y |= x[q][k].y;
+        acc[k].z |= x[q][k].z;
+        acc[k].w |= x[q][k].w;
+      }
   }
 #pragma unroll
-  for (int k = 0; k < kSlots; ++k) {
-    const uint32_t w = t + k * kOrRowThreads;
-    if (w < W) s_bits[w] = acc[k];
+  for (int k = 0; k < kSlots4; ++k) {
+    const uint32_t w4 = t + k * kOrRowThreads;
+    if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
   }
   __syncthreads();
 #pragma unroll
@@ -456,7 +464,12 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
     return -1;
   }
   if (B == 0) return 0;
-  k_or_rows<<<(unsigned)B, kOrRowThreads, W * 4, s>>>(parts, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift,
+  const bool aligned = (reinterpret_cast<uintptr_t>(parts) & 15) == 0 && stride % 4 == 0;
+  if (!aligned) {
+    set_error("shard_or_rows: the payloads must start on 16-B boundaries (stride a multiple of 4 words)");
+    return -1;
+  }
+  k_or_rows<<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift,
                                                       out, ld, unpack);
   FM_HIP(hipGetLastError());
   return 0;

@@ -80,6 +80,35 @@ def _boost_table(boost: float, lrf: float, dtype, n: int) -> List[float]:
     return out
 
 
+_CFG_ATTRS = ("eos_token_id", "pad_token_id", "stop_at_count", "min_new_tokens", "always_allow_eos",
+              "forced_bos_token_id", "length_reward_factor", "BOOST", "_num_beams", "model_name")
+
+
+def _config(proc, dtype) -> "_PrepConfig":
+    """proc._prep_config(dtype), built once per dtype and attribute values
+    (a call would otherwise rebuild the ctypes struct and round its boosts:
+    ~10 us of a vLLM per-sequence call's host time)."""
+    sig = (dtype, tuple(getattr(proc, "end_marker", ())), tuple(proc.force_decoding_from or ())) + \
+        tuple(getattr(proc, a, None) for a in _CFG_ATTRS)
+    cache = proc.__dict__.setdefault("_cfg_cache", {})
+    c = cache.get(sig)
+    if c is None:
+        c = cache[sig] = proc._prep_config(dtype)
+    return c
+
+
+def _raw_stream(dev_index: int) -> int:
+    """torch's current stream on the device as a raw hipStream_t (the C call
+    behind torch.cuda.current_stream(...).cuda_stream, without building the
+    Stream object)."""
+    return torch._C._cuda_getCurrentRawStream(dev_index)
+
+
+class SpeculativeCallError(RuntimeError):
+    """FMIDX_PROC_STATUS=deferred: an earlier call returned the device path's
+    output for an input whose reference result needs the host path."""
+
+
 class _ProcessorArgs(ctypes.Structure):
     """fm_processor_args (include/fmidx.h)."""
     _fields_ = [("ids", c_void_p), ("B", c_uint64), ("L", c_uint64), ("ld", c_uint64), ("fdf", c_void_p),
@@ -135,6 +164,26 @@ class _DeviceStep:
         self._ev_ready = False
         self._wait_stream = os.environ.get("FMIDX_PROC_WAIT", "event") == "stream"
         self._verify = os.environ.get("FMIDX_PROC_VERIFY", "0") != "0"    # hard calls: read the status anyway
+        # FMIDX_PROC_STATUS=deferred (opt-in, measurement of the wait's cost): a soft call returns
+        # without waiting for its status; the status is checked at the next call (or check_pending())
+        # and a call that needed the host path raises SpeculativeCallError there -- its output was
+        # the device path's, not the reference's.  Default: every soft call waits (exact).
+        self._deferred = os.environ.get("FMIDX_PROC_STATUS", "wait") == "deferred"
+        self._pend = None
+        self._pend_bufs = None
+
+    def check_pending(self):
+        """Deferred-status mode: raise if the last call needed the host path."""
+        pend, self._pend = self._pend, None
+        if pend is None:
+            return
+        ev, st = pend
+        ev.synchronize()
+        if st[0] != 0 or st[1] != st[2]:
+            self._prev_ok = False
+            raise SpeculativeCallError("a previous processor call's input needed the host path (end markers / "
+                                       "boost overflow); with FMIDX_PROC_STATUS=deferred its output was the "
+                                       "device path's")
 
     @property
     def prev_ids(self):
@@ -211,23 +260,36 @@ class _DeviceStep:
         a.unigram_bits = self.core.unigram_bits(V, dev).data_ptr()
         a.eos = int(cfg.eos)
         a.ids_copy, a.copy_ld = keep.data_ptr(), keep.stride(0)
-        stream = torch.cuda.current_stream(dev)
+        if self._deferred:
+            self.check_pending()
         wait = wait or self._verify or B == 0
+        if wait and self._deferred and B and not (cfg.flags & PREP_HARD):
+            if self._pend_bufs is None:
+                self._pend_bufs = [(torch.cuda.Event(), torch.zeros(4, dtype=torch.int32).pin_memory())
+                                   for _ in range(2)]
+            ev, st = self._pend_bufs[self._cur]
+            ev.record(torch.cuda.current_stream(dev))      # creates the event; re-recorded by the call
+            a.status_host, a.status_event = st.data_ptr(), ev.cuda_event
+            check(lib().fm_processor_call(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
+                                          c_void_p(_raw_stream(dev.index))), "processor_call")
+            self._pend = (ev, st.numpy())
+            self._cur, self._prev_ok = oth, True
+            return out if out.device == scores.device else out.to(scores.device)
         if wait:
             a.status_host = self.status_h.data_ptr()
             if not self._ev_ready:          # torch creates the event at its first record
-                self._ev.record(stream)
+                self._ev.record(torch.cuda.current_stream(dev))
                 self._ev_ready = True
             a.status_event = self._ev.cuda_event
         else:
             a.status_host = a.status_event = None
         check(lib().fm_processor_call(self.index._h, ctypes.byref(cfg), ctypes.byref(a),
-                                      c_void_p(stream.cuda_stream)), "processor_call")
+                                      c_void_p(_raw_stream(dev.index))), "processor_call")
         if not wait:
             self._cur, self._prev_ok = oth, True
             return out if out.device == scores.device else out.to(scores.device)
         if self._wait_stream:
-            stream.synchronize()
+            torch.cuda.current_stream(dev).synchronize()
         else:
             self._ev.synchronize()
         st = self._status_np
@@ -394,7 +456,7 @@ class _BatchedCore:
         return self.index.allowed_mask(lo_t, hi_t, vocab, SHIFT, packed=True)
 
     def unigram_bits(self, vocab: int, device):
-        key = (str(device), vocab)
+        key = (device.index if isinstance(device, torch.device) else device, vocab)
         if key not in self._uni_cache:
             words = (vocab + 31) // 32
             bits = np.zeros(words * 32, dtype=np.uint8)
@@ -548,7 +610,7 @@ class QwenIndexBasedLogitsProcessor:
 
     def _process(self, input_ids: torch.LongTensor, scores: torch.FloatTensor) -> torch.Tensor:
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            out = self._dev(input_ids, scores, _config(self, scores.dtype))
             if out is not None:
                 return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
@@ -676,7 +738,7 @@ class CausalIndexBasedLogitsProcessor:
         if self._dev is not None:
             # a soft variant: its status (end markers, boost overflow) depends on the
             # input, so the call waits for it (wait=False is for PREP_HARD only)
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype))
+            out = self._dev(input_ids, scores, _config(self, scores.dtype))
             if out is not None:
                 return out
         input_ids = torch.stack(_find_marker_rows(input_ids, self.end_marker))
@@ -859,7 +921,7 @@ class VllmIndexBasedLogitsProcessor(_HardMaskBase):
     def __call__(self, input_ids, scores):
         scores = scores.unsqueeze(0)
         if self._dev is not None:
-            out = self._dev(self._device_ids(tuple(input_ids)), scores, self._prep_config(scores.dtype), wait=False)
+            out = self._dev(self._device_ids(tuple(input_ids)), scores, _config(self, scores.dtype), wait=False)
             if out is not None:
                 return out
         input_ids = torch.tensor([list(input_ids)], dtype=torch.long)
@@ -916,7 +978,7 @@ class SeqIndexBasedLogitsProcessor(_HardMaskBase):
 
     def _process(self, input_ids, scores):
         if self._dev is not None:
-            out = self._dev(input_ids, scores, self._prep_config(scores.dtype), wait=False)
+            out = self._dev(input_ids, scores, _config(self, scores.dtype), wait=False)
             if out is not None:
                 return out
         B, V = scores.shape

@@ -125,19 +125,21 @@ def hf_leg(kind, fm, text, B, beams, new, dev, rng, reps=3):
     res = {"model": f"{kind} random weights ({sum(p.numel() for p in model.parameters()) / 1e9:.2f} B params, bf16)",
            "vocab": V, "rows": B, "prompts": prompts, "beams": beams, "new_tokens": new, "reps": reps}
     procs = {}
-    for mode in ("event", "stream", "host"):
+    for mode in ("event", "stream", "deferred", "host"):
         proc = mk()
         if mode == "host":
             proc._dev = None
         elif mode == "stream":
             proc._dev._wait_stream = True
+        elif mode == "deferred":          # no wait for the status (checked at the next call)
+            proc._dev._deferred = True
         procs[mode] = Timed(proc)
         gen(LogitsProcessorList([procs[mode]]), 2)                     # first calls: fresh searches, buffers
     # the modes interleaved, `reps` rounds (clock and allocator drift land on every mode alike)
-    times = {m: [] for m in ("none", "event", "stream", "host")}
-    calls = {m: [] for m in ("event", "stream", "host")}
+    times = {m: [] for m in ("none", "event", "stream", "deferred", "host")}
+    calls = {m: [] for m in ("event", "stream", "deferred", "host")}
     for _ in range(reps):
-        for mode in ("none", "event", "stream", "host"):
+        for mode in ("none", "event", "stream", "deferred", "host"):
             n_new = new
             if mode == "none":
                 t, _ = gen(LogitsProcessorList([]), n_new)
@@ -147,16 +149,18 @@ def hf_leg(kind, fm, text, B, beams, new, dev, rng, reps=3):
                 t, _ = gen(LogitsProcessorList([w]), n_new)
                 calls[mode].append(float(np.median(w.times)))
                 if mode != "host":
+                    w.proc._dev.check_pending()
                     assert w.proc._dev.prev_ids is not None, "device path fell back"
             times[mode].append(t / n_new)
     res["no_processor_ms_per_step"] = float(np.median(times["none"])) * 1e3
-    for mode in ("event", "stream", "host"):
+    for mode in ("event", "stream", "deferred", "host"):
         res[f"{mode}_ms_per_step"] = float(np.median(times[mode])) * 1e3
         res[f"{mode}_ms_per_step_all"] = [x * 1e3 for x in times[mode]]
         res[f"{mode}_processor_ms_per_call"] = float(np.median(calls[mode])) * 1e3
         log(f"{kind} {mode}: {res[f'{mode}_ms_per_step']:.2f} ms/step (no processor "
             f"{res['no_processor_ms_per_step']:.2f}), processor {res[f'{mode}_processor_ms_per_call']:.3f} ms/call")
     res["event_overhead_ms_per_step"] = res["event_ms_per_step"] - res["no_processor_ms_per_step"]
+    res["deferred_overhead_ms_per_step"] = res["deferred_ms_per_step"] - res["no_processor_ms_per_step"]
     res["host_overhead_ms_per_step"] = res["host_ms_per_step"] - res["no_processor_ms_per_step"]
     del model
     torch.cuda.empty_cache()
