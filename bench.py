@@ -1210,25 +1210,29 @@ def main():
     }
     # PMC traffic (tools/pmc_traffic.sh) is collected in a separate rocprofv3 run and committed;
     # it is used only when it was counted on this very library build, config and mask layout
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    # one committed file per config: profiles/pmc_traffic.json (C3), pmc_traffic_c2.json, pmc_traffic_c5.json
+    import glob
+
     lib_hash = lib_sha16()
     result["roofline"]["lib_sha16"] = lib_hash
-    if os.path.exists(pmc):
+    seen = []
+    for pmc in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_traffic*.json"))):
         try:
             with open(pmc) as f:
                 t = json.load(f)
-            same = t.get("lib_sha16") == lib_hash and t.get("corpus_tokens") == n and t.get("batch") == B and not PK
-            if same:
-                result["roofline"]["traffic"] = t.get("k_decode_bytes_per_launch")
-                result["roofline"]["traffic_source"] = "profiles/pmc_traffic.json (same lib_sha16, n, B)"
-                if t.get("k_lf_bytes_per_launch") is not None:
-                    result["standalone_kernels"]["k_lf"]["pmc_bytes_per_launch"] = t["k_lf_bytes_per_launch"]
-            else:
-                result["roofline"]["traffic_source"] = (f"none: profiles/pmc_traffic.json was counted on lib "
-                                                        f"{t.get('lib_sha16')} / n={t.get('corpus_tokens')}, "
-                                                        f"this run is lib {lib_hash} / n={n}")
-        except Exception:
-            pass
+        except (OSError, ValueError):
+            continue
+        name = os.path.relpath(pmc, REPO)
+        seen.append(f"{name}: lib {t.get('lib_sha16')} n={t.get('corpus_tokens')} B={t.get('batch')}")
+        if t.get("lib_sha16") == lib_hash and t.get("corpus_tokens") == n and t.get("batch") == B and not PK:
+            result["roofline"]["traffic"] = t.get("k_decode_bytes_per_launch")
+            result["roofline"]["traffic_source"] = f"{name} (same lib_sha16, n, B)"
+            if t.get("k_lf_bytes_per_launch") is not None:
+                result["standalone_kernels"]["k_lf"]["pmc_bytes_per_launch"] = t["k_lf_bytes_per_launch"]
+            break
+    else:
+        result["roofline"]["traffic_source"] = (f"none counted for this run (lib {lib_hash}, n={n}, B={B}); "
+                                                f"committed: {'; '.join(seen) or 'none'}")
     pr = os.path.join(REPO, "profiles", "pmc_rank.json")
     if os.path.exists(pr) and n > 4e9:
         try:   # tools/pmc_rank.sh: the 2^19-row grouped launches of tools/probe_rank.py on a C3 index

@@ -300,16 +300,26 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   }
 }
 
-// One workgroup (1024 threads) per row.  Every part's (desc, off) for the row
-// is staged in LDS first (one round trip); then the dense parts' words are
-// loaded four parts at a time for all of a thread's words (thread t owns
-// words t + 1024 k) and ORed in registers; then every sparse symbol of every
-// part -- one flat index space over the parts' lists, so a thread's loads do
-// not wait part by part -- is set with an LDS atomic; then the row is emitted
-// as uint8 (16 tokens per lane-chunk, 16-B write-through stores) or as words.
+// One workgroup (1024 threads) per row.  Two roles, as in k_decode (loads and
+// stores share vmcnt in issue order, so a wave with stores in flight cannot
+// wait on a load without waiting for them too):
+//   waves 4..15 (uint8 output)  zero-fill the row's 128 KB at once, overlapping
+//               the loads, and later store only the 16-token chunks that hold
+//               an allowed token (the same thread wrote the zeros of that
+//               chunk: program order on one address, no wait);
+//   waves 0..3  stage every part's (desc, off) for the row in LDS (one round
+//               trip), then load the dense parts' words (16-B loads, two parts
+//               per round) and the first 1024 sparse symbols (one flat index
+//               space over the parts' lists) together, OR the words into the
+//               LDS bitmap and set the symbols' bits with LDS atomics.
+// Barriers are LDS-only (s_waitcnt lgkmcnt(0); s_barrier): nothing that
+// crosses them is global data, so the zero stores need not drain.
 constexpr int kOrRowThreads = 1024;
+constexpr int kOrLoadThreads = 256;                 // waves 0..3
 constexpr int kOrRowMaxWords = 8 * kOrRowThreads;   // V <= 262144
 constexpr int kOrMaxParts = 64;
+
+__device__ __forceinline__ void or_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts, uint32_t nparts,
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
@@ -320,12 +330,31 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   __shared__ uint32_t s_nd;
   const uint64_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
+  const bool loader = t < kOrLoadThreads;
+  uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
+  const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+  const uint32_t nch = (uint32_t)((vocab + 15) / 16);
+  constexpr uint32_t kZ = kOrRowThreads - kOrLoadThreads;   // store-only threads
+  if (unpack && !loader) {
+    for (uint32_t c = t - kOrLoadThreads; c < nch; c += kZ) {
+      const uint64_t t0 = 16ull * c;
+      if (t0 + 16 <= vocab && aligned) {
+        or_v4u z = {0u, 0u, 0u, 0u};
+        __builtin_amdgcn_raw_buffer_store_b128(z, r, (uint32_t)t0, 0, kOrStoreAux);
+      } else {
+        for (uint64_t i = 0; i < 16 && t0 + i < vocab; ++i) row[t0 + i] = 0;
+      }
+    }
+  }
+  const uint32_t W4 = (W + 3) / 4;
+  for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
   if (t < nparts) {
     const uint32_t* pp = parts + (uint64_t)t * stride;
     s_desc[t] = pp[4 + b];
     s_off[t] = pp[4 + B + b];
   }
-  __syncthreads();
+  or_lds_barrier();
   if (t == 0) {
     uint32_t nd = 0, run = 0;
     for (uint32_t p = 0; p < nparts; ++p) {
@@ -336,84 +365,91 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     s_pre[nparts] = run;
     s_nd = nd;
   }
-  __syncthreads();
+  or_lds_barrier();
   const uint32_t nd = s_nd;
   const uint32_t total = s_pre[nparts];
-  // the first batch of sparse symbols (4 per thread) is loaded together with the dense words:
-  // both depend only on the staged (desc, off), so the row costs one data round trip
-  auto sym_at = [&](uint32_t i) -> uint32_t {
-    uint32_t p = 0;                                     // the part whose list holds flat index i
-    for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
-      if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
-    return parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
-  };
-  uint32_t sym0[4];
+  if (loader) {
+    auto sym_at = [&](uint32_t i) -> uint32_t {
+      uint32_t p = 0;                                     // the part whose list holds flat index i
+      for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
+        if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
+      return parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
+    };
+    // the first 1024 sparse symbols, loaded with the first dense round
+    uint32_t sym0[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrRowThreads + t, total - 1)) : 0u;
-  // dense parts: thread t owns words [4 (t + 1024 k), + 4) -- 16-B loads (a dense row's data
-  // starts on a 4-word boundary and is zero-padded to 4 words), four parts in flight at a time
-  constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);
-  const uint32_t W4 = (W + 3) / 4;
-  uint4 acc[kSlots4];
+    for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrLoadThreads + t, total - 1)) : 0u;
+    constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrLoadThreads);   // 8: W <= 8192 words
+    const uint32_t slots = (W4 + kOrLoadThreads - 1) / kOrLoadThreads;
+    uint4 acc[kSlots4];
 #pragma unroll
-  for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
-  for (uint32_t j0 = 0; j0 < nd; j0 += 4) {
-    const uint4* src[4];
+    for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t j0 = 0; j0 < nd; j0 += 2) {
+      const uint4* src[2];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
-      src[q] = reinterpret_cast<const uint4*>(parts + (uint64_t)p * stride + s_off[p]);
+      for (int q = 0; q < 2; ++q) {
+        const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
+        src[q] = reinterpret_cast<const uint4*>(parts + (uint64_t)p * stride + s_off[p]);
+      }
+      uint4 x[2][kSlots4];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int k = 0; k < kSlots4; ++k)
+          x[q][k] = (uint32_t)k < slots ? src[q][min(t + k * kOrLoadThreads, W4 - 1)] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int k = 0; k < kSlots4; ++k) {
+          acc[k].x |= x[q][k].x;
+          acc[k].y |= x[q][k].y;
+          acc[k].z |= x[q][k].z;
+          acc[k].w |= x[q][k].w;
+        }
     }
-    uint4 x[4][kSlots4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int k = 0; k < kSlots4; ++k) x[q][k] = src[q][min(t + k * kOrRowThreads, W4 - 1)];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
+    if (nd) {
 #pragma unroll
       for (int k = 0; k < kSlots4; ++k) {
-        acc[k].x |= x[q][k].x;
-        acc[k].y |= x[q][k].y;
-        acc[k].z |= x[q][k].z;
-        acc[k].w |= x[q][k].w;
+        const uint32_t w4 = t + k * kOrLoadThreads;
+        if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
       }
-  }
-#pragma unroll
-  for (int k = 0; k < kSlots4; ++k) {
-    const uint32_t w4 = t + k * kOrRowThreads;
-    if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t tok = (int64_t)sym0[u] - shift;
-    if (u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
-      atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
-  }
-  for (uint32_t i0 = 4 * kOrRowThreads; i0 < total; i0 += 4 * kOrRowThreads) {   // long lists (rare)
-    uint32_t sym[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) sym[u] = sym_at(min(i0 + u * kOrRowThreads + t, total - 1));
+    }
+    // the dense words are in place before any symbol's bit is ORed in (same threads, then a
+    // wave-level LDS fence: other loader waves' words may share a symbol's word)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t tok = (int64_t)sym[u] - shift;
-      if (i0 + u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+      const int64_t tok = (int64_t)sym0[u] - shift;
+      if (u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
         atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
     }
+    for (uint32_t i0 = 4 * kOrLoadThreads; i0 < total; i0 += 4 * kOrLoadThreads) {   // long lists
+      uint32_t sym[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sym[u] = sym_at(min(i0 + u * kOrLoadThreads + t, total - 1));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t tok = (int64_t)sym[u] - shift;
+        if (i0 + u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+          atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+      }
+    }
+  } else {
+    __builtin_amdgcn_s_barrier();    // the loaders' mid-phase barrier (every wave takes part)
   }
-  __syncthreads();
+  or_lds_barrier();
   if (!unpack) {
     uint32_t* o = static_cast<uint32_t*>(out) + b * (ld / 4);
     for (uint32_t w = t; w < W; w += kOrRowThreads) o[w] = s_bits[w];
     return;
   }
-  uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
-  __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
-  const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-  for (uint64_t c = t; 16 * c < vocab; c += kOrRowThreads) {   // 16-token chunk c
-    const uint64_t t0 = 16 * c;
+  if (loader) return;
+  // the non-zero chunks, by the threads that zero-filled them
+  for (uint32_t c = t - kOrLoadThreads; c < nch; c += kZ) {
+    const uint64_t t0 = 16ull * c;
     const uint32_t bits16 = (s_bits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+    if (!bits16) continue;
     uint32_t q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = (((bits16 >> (4 * i)) & 0xFu) * 0x204081u) & 0x01010101u;
