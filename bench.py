@@ -537,7 +537,7 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     per_step = [sum(w) for w in words_seen]
     return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": B / (ms / 1e3),
             "unit": "masks/s", "ms_per_step": ms, "scaling": "strong", "shards": world, "halo": halo,
-            "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": st["bwt_bytes"] // 4,
+            "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": ix.size(),
             "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
             "masks_equal_unsharded": exact,
             "exchange": "sparse: per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",

@@ -36,7 +36,7 @@ void Index::release() {
   // no kernel on any stream may still read what is freed here (the callers
   // hold the handle's device)
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {wm, sb, Z, D, C, bwt, bm, bm_full, bm_follow, sa, text, ws};
+  void* ptrs[] = {wm, sb, Z, D, C, bwt, bwt_view, bm, bm_full, bm_follow, sa, text, ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int l = 0; l < kW2MaxLevels; ++l) {
@@ -78,6 +78,7 @@ void Index::release() {
   D = nullptr;
   C = nullptr;
   bwt = nullptr;
+  bwt_view = nullptr;
   bm = nullptr;
   sa = nullptr;
   text = nullptr;
@@ -896,7 +897,17 @@ int fm_save(fm_index* h, const char* path) {
   fmidx::IndexFile f;
   f.n = n;
   f.bwt.resize(n);
-  FM_HIP(hipMemcpy(f.bwt.data(), x.bwt, n * 4, hipMemcpyDeviceToHost));
+  {
+    const bool made = !x.bwt && !x.bwt_view;   // materialised for this save only
+    const uint32_t* src = nullptr;
+    if (fmidx::device_bwt_view(&x, &src)) return -1;
+    const hipError_t e = hipMemcpy(f.bwt.data(), src, n * 4, hipMemcpyDeviceToHost);
+    if (made) {
+      (void)hipFree(x.bwt_view);
+      x.bwt_view = nullptr;
+    }
+    FM_HIP(e);
+  }
   if (x.mark) {
     f.mark.resize(fmidx::file_mark_words(n));
     f.samp.resize(fmidx::file_samp_count(n));
@@ -1080,9 +1091,10 @@ int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, u
   if (e_bytes) *e_bytes = e;
   if (sample_bytes) *sample_bytes = x.samp_bytes;
   if (total_bytes)
-    *total_bytes = x.wm_bytes + x.n * 4 + x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0) +
-                   x.w2_bytes + e + x.cache_bytes + x.trans_bytes + x.samp_bytes + (x.sa ? x.n * 8 : 0) +
-                   (x.text ? x.n * 4 : 0) + 3 * K * 8;
+    // (cache_bytes already holds the transition table: build_transitions adds it there)
+    *total_bytes = x.wm_bytes + (x.bwt ? x.n * 4 : 0) + x.bm_bytes + x.follow_bytes +
+                   (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0) + x.w2_bytes + e + x.cache_bytes + x.samp_bytes +
+                   (x.sa ? x.n * 8 : 0) + (x.text ? x.n * 4 : 0) + 3 * K * 8;
   return 0;
   FM_API_END
 }
@@ -1094,7 +1106,7 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
   const auto& x = h->idx;
   if (levels) *levels = x.NL;
   if (wm_bytes) *wm_bytes = x.wm_bytes;
-  if (bwt_bytes) *bwt_bytes = x.n * 4;
+  if (bwt_bytes) *bwt_bytes = x.bwt ? x.n * 4 : 0;
   if (bitmap_bytes) *bitmap_bytes = x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0);
   if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;
   return 0;
@@ -1277,8 +1289,10 @@ int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads
 int fm_device_bwt(const fm_index* h, const uint32_t** out) {
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
-  *out = h->idx.bwt;
-  return 0;
+  // the kept BWT, or a copy materialised from E (held by the handle; not a query structure)
+  auto* hm = const_cast<fm_index*>(h);
+  std::lock_guard<std::mutex> lk(hm->mu);
+  return fmidx::device_bwt_view(&hm->idx, out);
   FM_API_END
 }
 
@@ -1289,7 +1303,7 @@ int fm_device_struct(const fm_index* h, int which, const void** out, uint64_t* b
   const void* p = nullptr;
   uint64_t b = 0;
   switch (which) {
-    case 0: p = x.bwt; b = x.n * 4; break;
+    case 0: p = x.bwt; b = x.bwt ? x.n * 4 : 0; break;   // null once freed (E holds the symbols)
     case 1: p = x.E; b = x.E ? x.n * 8 : 0; break;
     case 2: p = x.trans_tab; b = x.trans_bytes; break;
     case 3: p = x.cache_bm; b = x.cache_bm ? x.cache_nodes * (uint64_t)x.view.bm_words * 4 : 0; break;

@@ -430,6 +430,33 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
   return (uint32_t)std::strtoul(v, nullptr, 10);
 }
 
+__global__ void __launch_bounds__(kThreads) k_e_symbols(const uint64_t* __restrict__ E, uint64_t n,
+                                                        uint32_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads)
+    out[i] = (uint32_t)(E[i] >> kESymShift);
+}
+
+// The BWT as plain uint32 symbols: the kept copy, or one materialised from E
+// (owned by h, freed with it) -- for fm_device_bwt / fm_save, not the query path.
+int device_bwt_view(Index* h, const uint32_t** out) {
+  if (h->bwt) {
+    *out = h->bwt;
+    return 0;
+  }
+  if (!h->bwt_view) {
+    if (!h->E) {
+      set_error("index has neither a BWT nor E");
+      return -1;
+    }
+    if (dmalloc(&h->bwt_view, h->n)) return -1;
+    k_e_symbols<<<2048, kThreads, 0, h->stream>>>(h->E, h->n, h->bwt_view);
+    FM_HIP(hipGetLastError());
+    FM_HIP(hipStreamSynchronize(h->stream));
+  }
+  *out = h->bwt_view;
+  return 0;
+}
+
 // h->bwt must already hold the BWT (device, owned by h).
 int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
   if (n == 0) {
@@ -634,6 +661,15 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   t = build_clock();
   if (device_build_cache(h, s)) return -1;
   build_phase("range cache + transitions", t, s);
+  // The plain BWT duplicates E's symbol field (4 bytes per row: 16.8 GiB at C3).  Once E is
+  // built every kernel reads symbols through bwt_sym() / stream_symbols_e(), so the copy is
+  // freed; fm_device_bwt materialises one on request (FMIDX_KEEP_BWT=1 keeps it).
+  if (h->E && d_bwt == h->bwt && env_u32("FMIDX_KEEP_BWT", 0) == 0) {
+    FM_HIP(hipStreamSynchronize(s));
+    FM_HIP(hipFree(h->bwt));
+    h->bwt = nullptr;
+    v.bwt = nullptr;
+  }
   h->built = true;
   return 0;
 }

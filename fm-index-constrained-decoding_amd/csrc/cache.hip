@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
     if (cw >= v.cache_min) {
       aux = cache_id_thread(v, clo, clo + cw);
     } else if (cw == 1) {
-      const uint64_t sym = v.bwt[clo];
+      const uint64_t sym = bwt_sym(v, clo);
       if (sym < kTransOne) aux = kTransOne | sym;
     }
     const uint64_t w0 = lo | (c << kTransSymShift);

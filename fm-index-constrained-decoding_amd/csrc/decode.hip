@@ -237,6 +237,58 @@ __device__ __forceinline__ void stream_symbols(const uint32_t* __restrict__ bwt,
   if (hsym != ~0u) set_bit(win, hsym, base_bit, lim);
 }
 
+// The same from E (the plain BWT freed): 16-B loads hold two entries, whose
+// symbols are bits 36.. of each; the aligned middle is in entry pairs, the
+// head / tail pieces one entry each (threads 0..3).  Same round-trip structure.
+__device__ __forceinline__ void stream_symbols_e(const uint64_t* __restrict__ E, uint64_t a0, uint64_t b0,
+                                                 uint64_t a1, uint64_t b1, int64_t base_bit, int64_t lim,
+                                                 uint32_t* win, uint32_t nthr) {
+  auto pairs = [](uint64_t a, uint64_t b, uint64_t& q, uint64_t& nq) {
+    const uint64_t a2 = (a + 1) & ~1ull, b2 = b & ~1ull;
+    const bool has = a < b && a2 < b2;
+    q = has ? a2 / 2 : 0;
+    nq = has ? (b2 - a2) / 2 : 0;
+  };
+  uint64_t q0, n0, q1, n1;
+  pairs(a0, b0, q0, n0);
+  pairs(a1, b1, q1, n1);
+  const uint64_t ntot = n0 + n1;
+  const uint4* src = reinterpret_cast<const uint4*>(E);
+  uint32_t hsym = ~0u;          // head / tail entries: threads 0..3, loaded with the first round
+  if (threadIdx.x < 4) {
+    const bool p1 = threadIdx.x >= 2, tail = (threadIdx.x & 1u) != 0;
+    const uint64_t a = p1 ? a1 : a0, b = p1 ? b1 : b0;
+    uint64_t q, nq;
+    pairs(a, b, q, nq);
+    uint64_t pos = ~0ull;
+    if (a < b) {
+      if (nq) pos = tail ? ((b & 1ull) ? b - 1 : ~0ull) : ((a & 1ull) ? a : ~0ull);
+      else pos = tail ? (a + 1 < b ? a + 1 : ~0ull) : a;   // no whole pair inside: at most two entries
+    }
+    if (pos != ~0ull) hsym = (uint32_t)(E[pos] >> kESymShift);
+  }
+  for (uint64_t base = threadIdx.x; base < ntot; base += (uint64_t)nthr * kUnroll) {
+    uint32_t s[kUnroll][2];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      // unconditional load (see stream_symbols): surplus lanes re-read pair 0 and are padded out
+      const uint64_t j = base + (uint64_t)u * nthr;
+      const uint64_t jj = j < ntot ? j : 0;
+      const uint4 x = src[jj < n0 ? q0 + jj : q1 + (jj - n0)];
+      const uint32_t pad = j < ntot ? 0u : ~0u;
+      s[u][0] = (x.y >> (kESymShift - 32)) | pad;
+      s[u][1] = (x.w >> (kESymShift - 32)) | pad;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (s[u][0] != ~0u) {
+        set_bit(win, s[u][0], base_bit, lim);
+        set_bit(win, s[u][1], base_bit, lim);
+      }
+  }
+  if (hsym != ~0u) set_bit(win, hsym, base_bit, lim);
+}
+
 // blockIdx -> (row, slice).  Blocks b and b+8 share an XCD under round-robin
 // dispatch, so the S slices of a row are given blockIdx values congruent mod 8:
 // their redundant reads of the row's rank blocks / BWT / bitmaps share one L2.
@@ -554,8 +606,12 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     if (nb == 0) {
       // streamed only
       const uint32_t nthr = early_zero ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
-      if (threadIdx.x < nthr)
-        stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
+      if (threadIdx.x < nthr) {
+        if (v.bwt)
+          stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
+        else
+          stream_symbols_e(v.E, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
+      }
       if (threadIdx.x == 0 && (int64_t)s_lohi[2] >= 0) set_bit(win, (uint32_t)s_lohi[2], base_bit, lim);   // one-row range
       if (cmask & kContentPath) {   // wave 0: the content read with the E scan
 #pragma unroll
@@ -583,7 +639,10 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         const uint32_t m = ok ? ~0u : 0u;
         x[u] = make_uint4(y.x & m, y.y & m, y.z & m, y.w & m);
       }
-      stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
+      if (v.bwt)
+        stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
+      else
+        stream_symbols_e(v.E, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, kDecThreads);
       FM_STAMP(v, 4);
       // G groups split the bitmaps, each thread owns one uint4 of the window
       // (several when the window is wider than the workgroup); partial ORs

@@ -76,7 +76,7 @@ struct DevView {
   const uint64_t* Z;          // NL * 16
   const int64_t* D;           // [2^L]
   const uint64_t* C;          // [2^L + 1]
-  const uint32_t* bwt;        // [n]
+  const uint32_t* bwt;        // [n], or null once E holds the symbols (bwt_sym)
   const uint32_t* bm;         // bitmap hierarchy
   const uint32_t* bm_full;    // bitmap of BWT[0, n) (all symbols), bm_words words
   const uint32_t* bm_follow;  // per symbol c: bitmap of BWT[C[c], C[c+1]) (follow set), or null
@@ -112,6 +112,13 @@ struct DevView {
   uint64_t* stamps;           // diagnostic build only: per-workgroup phase timestamps
 #endif
 };
+
+// BWT symbol i.  The plain BWT is freed once E exists (E's symbol field holds
+// the same symbols; device_build_from_bwt, FMIDX_KEEP_BWT=1 keeps it), so
+// every kernel reads single symbols through here.
+__device__ __forceinline__ uint32_t bwt_sym(const DevView& v, uint64_t i) {
+  return v.bwt ? v.bwt[i] : (uint32_t)(v.E[i] >> kESymShift);
+}
 
 // Diagnostic phase stamps (s_memrealtime, 100 MHz), compiled only with
 // -DFMIDX_STAMPS.  They are kept in LDS and written out once at the end of the
@@ -637,7 +644,8 @@ struct Index {
   uint64_t* Z = nullptr;
   int64_t* D = nullptr;
   uint64_t* C = nullptr;
-  uint32_t* bwt = nullptr;
+  uint32_t* bwt = nullptr;        // freed after the build when E holds the symbols
+  uint32_t* bwt_view = nullptr;   // materialised on request (fm_device_bwt) when bwt is freed
   uint32_t* bm = nullptr;
   uint32_t* bm_full = nullptr;
   uint32_t* bm_follow = nullptr;
@@ -670,6 +678,7 @@ struct Index {
 
 // build.hip
 int device_build_from_bwt(Index* h, const uint32_t* d_bwt_owned, uint64_t n, hipStream_t s);
+int device_bwt_view(Index* h, const uint32_t** out);
 int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);
 int device_build_cache(Index* h, hipStream_t s);   // cache.hip
 int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s);

@@ -96,7 +96,7 @@ __device__ __forceinline__ void lf_row(const DevView& v, uint64_t i, uint64_t& l
     c = (uint32_t)(e >> kESymShift);
     return;
   }
-  c = v.bwt[i];
+  c = bwt_sym(v, i);
   uint64_t l = i, h = i + 1;
   const uint32_t* cbm;
   int64_t one;

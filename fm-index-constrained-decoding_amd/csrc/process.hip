@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
           ls_case = ls;
           f_range = hi > lo;
           f_cnt1 = hi > lo || cnt1 > 0;
-          f_dist = !(hi == lo || (hi - lo == 1 && v.bwt[lo] == 0));
+          f_dist = !(hi == lo || (hi - lo == 1 && bwt_sym(v, lo) == 0));
         }
         if (hi <= lo && !hard && cnt1 == 0) {
           ls = 0;
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(64) k_prep(DevView v, fm_prep_config cfg, cons
       } else if (kind == kBits) {
         // distinct (sentinel dropped, index.py:170) is empty iff the range is
         // empty or its one row holds the sentinel
-        empty = hi == lo || (hi - lo == 1 && v.bwt[lo] == 0);
+        empty = hi == lo || (hi - lo == 1 && bwt_sym(v, lo) == 0);
         p.flags = FM_ROW_BITS | FM_ROW_UNIGRAM;
       } else {
         p.flags = FM_ROW_SPECIAL | FM_ROW_UNIGRAM;

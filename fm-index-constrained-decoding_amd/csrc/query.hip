@@ -818,7 +818,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_
       tb &= tb - 1;
       uint64_t tl = __shfl(l, src, 64), th = __shfl(h, src, 64);
       const uint64_t tc = __shfl(c, src, 64), tp = __shfl(pid1, src, 64);
-      const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5) : v.bwt;
+      const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5)
+                                : reinterpret_cast<const uint32_t*>(v.C);
       const uint32_t pword = tp ? *pw : ~0u;
       lf_step_tail(v, tc, pword, tl, th);
       if ((int)lane == src) {
@@ -876,8 +877,9 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_tail(DevView v, const LfWork*
     uint64_t l = it.l, h = it.h;
     const uint32_t c32 = (uint32_t)it.sym;
     const uint64_t pid1 = it.sym >> 32;
-    // a probe miss: the range's bitmap word for c (unconditional: bwt[0] as a dummy)
-    const uint32_t* pw = pid1 ? v.cache_bm + (pid1 - 1) * v.bm_words + (c32 >> 5) : v.bwt;
+    // a probe miss: the range's bitmap word for c (unconditional: C[0] as a dummy)
+    const uint32_t* pw = pid1 ? v.cache_bm + (pid1 - 1) * v.bm_words + (c32 >> 5)
+                              : reinterpret_cast<const uint32_t*>(v.C);
     const uint32_t pword = pid1 ? *pw : ~0u;
     lf_step_tail(v, c32, pword, l, h);
     if (lane == 0) {

@@ -282,15 +282,17 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   if (b == 0)
     for (uint64_t i = 4 + 2 * B + t; i < H; i += kPackRowThreads) pay[i] = 0u;
   const uint32_t count = desc & 0x7FFFFFFFu;
-  const uint32_t* src = (desc >> 31) ? bits + b * ldw : v.bwt + min(l0, v.n - 1);
+  const bool dense = (desc >> 31) != 0;
+  const uint64_t s0 = min(l0, v.n - 1);
   uint32_t* dst = pay + off;
-  // up to 8 loads per thread in flight before the stores (W <= 8192 words: one pass)
+  // up to 8 loads per thread in flight before the stores (W <= 8192 words: one pass); a slice's
+  // symbols come from the plain BWT when it is kept, else from E's symbol field
   for (uint32_t i0 = 0; i0 < (uint32_t)words; i0 += 8 * kPackRowThreads) {
     uint32_t x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const uint32_t i = i0 + u * kPackRowThreads + t;
-      x[u] = src[min(i, count ? count - 1 : 0u)];
+      const uint32_t i = min(i0 + u * kPackRowThreads + t, count ? count - 1 : 0u);
+      x[u] = dense ? bits[b * ldw + i] : bwt_sym(v, s0 + i);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
