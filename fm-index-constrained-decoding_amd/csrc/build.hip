@@ -564,7 +564,9 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   // 2^14-row blocks instead of 2^12 free 16.5 GiB (200.4 -> 183.9) with the
   // same step (13.4 us cold) and build time (profiles/r03_memory/bm_log2/);
   // small indexes keep 2^12 so that they still get a hierarchy and a cache.
-  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", n >= (1ull << 26) ? 14 : 12);
+  // From 2^31 rows 2^16 (round 4, with the plain BWT freed: C3 122.0 -> 117.9 GiB,
+  // 13.72 vs 13.86 us cold, build 12.0 -> 14.6 s; profiles/r04_memory/).
+  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", n >= (1ull << 31) ? 16 : n >= (1ull << 26) ? 14 : 12);
   const uint32_t words = (uint32_t)(((uint64_t)max_sym + 1 + 127) / 128 * 4);
   const uint64_t nb0 = n >> log2b0;
   uint32_t bm_levels = 0;

@@ -11,6 +11,8 @@
 //           of the words; 1: out = uint8 [B, vocab] 0/1 (ld_out bytes per row).
 #include "fmidx_internal.h"
 
+#include <cstdlib>
+
 namespace fmidx {
 
 namespace {
@@ -286,13 +288,19 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   const uint64_t s0 = min(l0, v.n - 1);
   uint32_t* dst = pay + off;
   // up to 8 loads per thread in flight before the stores (W <= 8192 words: one pass); a slice's
-  // symbols come from the plain BWT when it is kept, else from E's symbol field
+  // symbols come from the plain BWT when it is kept, else from E's symbol field -- one source per
+  // row (workgroup-uniform), chosen outside the loads so none sits under a branch
+  const uint32_t* src32 = dense ? bits + b * ldw : (v.bwt ? v.bwt + s0 : nullptr);
+  const uint64_t* srcE = v.E + (dense ? 0 : s0);
   for (uint32_t i0 = 0; i0 < (uint32_t)words; i0 += 8 * kPackRowThreads) {
     uint32_t x[8];
+    if (src32) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t i = min(i0 + u * kPackRowThreads + t, count ? count - 1 : 0u);
-      x[u] = dense ? bits[b * ldw + i] : bwt_sym(v, s0 + i);
+      for (int u = 0; u < 8; ++u) x[u] = src32[min(i0 + u * kPackRowThreads + t, count ? count - 1 : 0u)];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        x[u] = (uint32_t)(srcE[min(i0 + u * kPackRowThreads + t, count ? count - 1 : 0u)] >> kESymShift);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -317,12 +325,13 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
 // Barriers are LDS-only (s_waitcnt lgkmcnt(0); s_barrier): nothing that
 // crosses them is global data, so the zero stores need not drain.
 constexpr int kOrRowThreads = 1024;
-constexpr int kOrLoadThreads = 256;                 // waves 0..3
 constexpr int kOrRowMaxWords = 8 * kOrRowThreads;   // V <= 262144
 constexpr int kOrMaxParts = 64;
 
 __device__ __forceinline__ void or_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// EARLY = false: no zero-fill -- every thread loads, and every chunk is stored once at the end.
+template <bool EARLY>
 __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts, uint32_t nparts,
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
@@ -330,15 +339,16 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
   __shared__ uint32_t s_desc[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
   __shared__ uint32_t s_nd;
+  constexpr int kOrLoadThreads = EARLY ? 256 : kOrRowThreads;   // EARLY: waves 0..3
   const uint64_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
-  const bool loader = t < kOrLoadThreads;
+  const bool loader = t < (uint32_t)kOrLoadThreads;
   uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
   const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
   const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
   const uint32_t nch = (uint32_t)((vocab + 15) / 16);
-  constexpr uint32_t kZ = kOrRowThreads - kOrLoadThreads;   // store-only threads
-  if (unpack && !loader) {
+  constexpr uint32_t kZ = EARLY ? kOrRowThreads - kOrLoadThreads : 1;   // store-only threads
+  if (EARLY && unpack && !loader) {
     for (uint32_t c = t - kOrLoadThreads; c < nch; c += kZ) {
       const uint64_t t0 = 16ull * c;
       if (t0 + 16 <= vocab && aligned) {
@@ -381,7 +391,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     uint32_t sym0[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrLoadThreads + t, total - 1)) : 0u;
-    constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrLoadThreads);   // 8: W <= 8192 words
+    constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrLoadThreads);   // W <= 8192 words
     const uint32_t slots = (W4 + kOrLoadThreads - 1) / kOrLoadThreads;
     uint4 acc[kSlots4];
 #pragma unroll
@@ -446,12 +456,13 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     for (uint32_t w = t; w < W; w += kOrRowThreads) o[w] = s_bits[w];
     return;
   }
-  if (loader) return;
-  // the non-zero chunks, by the threads that zero-filled them
-  for (uint32_t c = t - kOrLoadThreads; c < nch; c += kZ) {
+  if (EARLY && loader) return;
+  // EARLY: the non-zero chunks, by the threads that zero-filled them; else every chunk
+  const uint32_t c0 = EARLY ? t - kOrLoadThreads : t, cstep = EARLY ? kZ : kOrRowThreads;
+  for (uint32_t c = c0; c < nch; c += cstep) {
     const uint64_t t0 = 16ull * c;
     const uint32_t bits16 = (s_bits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-    if (!bits16) continue;
+    if (EARLY && !bits16) continue;
     uint32_t q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = (((bits16 >> (4 * i)) & 0xFu) * 0x204081u) & 0x01010101u;
@@ -507,8 +518,16 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
     set_error("shard_or_rows: the payloads must start on 16-B boundaries (stride a multiple of 4 words)");
     return -1;
   }
-  k_or_rows<<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift,
-                                                      out, ld, unpack);
+  static const bool early = [] {
+    const char* e = std::getenv("FMIDX_OR_ROWS_EARLY");
+    return e && *e && std::atoi(e) != 0;
+  }();
+  if (early)
+    k_or_rows<true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B,
+                                                                         (uint32_t)W, vocab, shift, out, ld, unpack);
+  else
+    k_or_rows<false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B,
+                                                                          (uint32_t)W, vocab, shift, out, ld, unpack);
   FM_HIP(hipGetLastError());
   return 0;
 }
