@@ -387,6 +387,9 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
         for s in range(first, last + 1):
             ref.distinct_only(lo_all[s], hi_all[s], 1)
         dts.append((time.perf_counter() - a) / window)
+        # one line per repetition: a long CPU leg must not look like a hung run
+        log(f"cpu repetition {len(dts)}/{reps}: " +
+            ", ".join(f"{m}x{t} {state[(m, t)][5][-1]:.0f}" for m, t in names) + " masks/s")
     legs = {}
     for (mode, threads), (lo, hi, mask, _, _, rates) in state.items():
         ok = bool(np.array_equal(lo, lo_all[last]) and np.array_equal(hi, hi_all[last]))

@@ -396,21 +396,24 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     uint4 acc[kSlots4];
 #pragma unroll
     for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t j0 = 0; j0 < nd; j0 += 2) {
-      const uint4* src[2];
+    // parts per round: all 8 shards of a wide row are dense, so a round covers 8 (2 slots per
+    // thread) -- 4 when the loaders are 256 threads (8 slots each)
+    constexpr int kPB = EARLY ? 2 : 8;
+    for (uint32_t j0 = 0; j0 < nd; j0 += kPB) {
+      const uint4* src[kPB];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < kPB; ++q) {
         const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
         src[q] = reinterpret_cast<const uint4*>(parts + (uint64_t)p * stride + s_off[p]);
       }
-      uint4 x[2][kSlots4];
+      uint4 x[kPB][kSlots4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < kPB; ++q)
 #pragma unroll
         for (int k = 0; k < kSlots4; ++k)
           x[q][k] = (uint32_t)k < slots ? src[q][min(t + k * kOrLoadThreads, W4 - 1)] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < kPB; ++q)
 #pragma unroll
         for (int k = 0; k < kSlots4; ++k) {
           acc[k].x |= x[q][k].x;
@@ -436,12 +439,12 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
       if (u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
         atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
     }
-    for (uint32_t i0 = 4 * kOrLoadThreads; i0 < total; i0 += 4 * kOrLoadThreads) {   // long lists
-      uint32_t sym[4];
+    for (uint32_t i0 = 4 * kOrLoadThreads; i0 < total; i0 += 8 * kOrLoadThreads) {   // long lists: 8 per round
+      uint32_t sym[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sym[u] = sym_at(min(i0 + u * kOrLoadThreads + t, total - 1));
+      for (int u = 0; u < 8; ++u) sym[u] = sym_at(min(i0 + u * kOrLoadThreads + t, total - 1));
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int64_t tok = (int64_t)sym[u] - shift;
         if (i0 + u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
           atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));

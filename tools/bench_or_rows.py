@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=128256)
     ap.add_argument("--dense", type=float, default=0.15)
     ap.add_argument("--mean", type=float, default=6.0)
+    ap.add_argument("--wide", type=float, default=0.0, help="fraction of rows dense on EVERY part (wide rows)")
     ap.add_argument("-K", type=int, default=20)
     args = ap.parse_args()
     from fmidx.sharding import or_bits, or_payloads
@@ -41,13 +42,14 @@ def main():
     H = 4 + ((2 * B + 3) & ~3)
     dense_rows = np.zeros((P, B, W), dtype=np.uint32)
     pays = []
+    wide = rng.random(B) < args.wide
     for p in range(P):
         desc = np.zeros(B, dtype=np.uint32)
         off = np.zeros(B, dtype=np.uint32)
         data = []
         at = H
         for b in range(B):
-            if rng.random() < args.dense:
+            if wide[b] or rng.random() < args.dense:
                 bits = (rng.random(W * 32) < 0.1).astype(np.uint8)
                 bits[V:] = 0
                 row = np.packbits(bits, bitorder="little").view(np.uint32)
