@@ -454,7 +454,7 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     steps; the last step's mask of each must equal the replica's."""
     import torch.distributed as dist
 
-    from fmidx.sharding import gather_payloads, or_bits, or_payloads, shard_text_device
+    from fmidx.sharding import SparseExchange, or_bits, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
     S = W + K
@@ -493,6 +493,7 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     out = torch.empty((B, V), dtype=torch.uint8, device=dev)
     payload = None
     words_seen = []
+    xchg = SparseExchange(None)
 
     def run(mode):
         nonlocal payload
@@ -509,10 +510,9 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
                 or_bits(parts, V, out=out)
             else:
                 payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
-                pp, words = gather_payloads(payload, None)
+                xchg(payload, B, V, SHIFT, out=out)
                 if i >= W:
-                    words_seen.append(words)
-                or_payloads(pp, B, V, SHIFT, out=out)
+                    words_seen.append(xchg.words[-1])
 
         for i in range(W):
             step(i)
@@ -545,6 +545,7 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
             "masks_equal_unsharded": exact,
             "exchange": "sparse: per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",
             "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
+            "speculative_gathers_respecified": xchg.respecified,
             "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
                                                 if words_seen else None),
             "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
@@ -837,6 +838,12 @@ def main():
             sys.exit(2)
         rc = spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
         sys.exit(rc if rc >= 0 else 128 - rc)
+    # the JSON line must be the only thing on stdout, and libraries write there too (RCCL prints its
+    # version banner on fd 1 when a communicator comes up): fd 1 now goes to stderr, and the line is
+    # written to a duplicate of the original stdout
+    line_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1340,7 +1347,8 @@ def main():
         except Exception as e:  # the replica line must still print
             result["c4_one_gpu"] = {"error": repr(e)}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        line_out.write(json.dumps(result) + "\n")
+        line_out.flush()
     if world > 1:
         import torch.distributed as dist
 

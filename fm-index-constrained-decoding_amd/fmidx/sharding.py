@@ -135,6 +135,7 @@ class ShardedDecoder:
         self._parts = None     # gathered packed rows of every rank (device path)
         self._out = None
         self._payload = None   # this rank's sparse-exchange payload
+        self._xchg = None      # its SparseExchange
         self.exchange_words = []   # sparse: words every rank shipped, per step (host ints)
 
     def _check_halo(self):
@@ -204,12 +205,13 @@ class ShardedDecoder:
         import torch
 
         self._payload = self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=self._payload)
-        parts, words = gather_payloads(self._payload, self.group)
-        self.exchange_words.append(words)
         B = self.lo.numel()
-        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != parts.device:
-            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=parts.device)
-        return or_payloads(parts, B, self.vocab, self.shift, out=self._out)
+        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != self._payload.device:
+            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=self._payload.device)
+        if self._xchg is None:
+            self._xchg = SparseExchange(self.group)
+            self.exchange_words = self._xchg.words
+        return self._xchg(self._payload, B, self.vocab, self.shift, out=self._out)
 
     def local_mask(self):
         return self.index.allowed_mask(self.lo, self.hi, self.vocab, self.shift)
@@ -285,6 +287,7 @@ class ShardedIndex:
         self.shift = shift
         self._payload = None
         self._parts = None
+        self._xchg = None
 
     @property
     def device(self) -> int:
@@ -308,8 +311,9 @@ class ShardedIndex:
         B, W = lo.numel(), (vocab + 31) // 32
         if self.exchange == "sparse":
             self._payload = self.shard.shard_pack(lo, hi, bits, vocab, payload=self._payload)
-            parts, _ = gather_payloads(self._payload, self.group)
-            return or_payloads(parts, B, vocab, self.shift, unpack=False)
+            if self._xchg is None:
+                self._xchg = SparseExchange(self.group)
+            return self._xchg(self._payload, B, vocab, self.shift, unpack=False)
         world = dist.get_world_size(self.group)
         mine = bits[:, :W].contiguous()
         if self._parts is None or self._parts.shape != (world, B, W):
@@ -354,6 +358,62 @@ def gather_payloads(payload, group):
     parts = torch.empty(world * m, dtype=torch.int32, device=payload.device)
     dist.all_gather_into_tensor(parts, mine.contiguous(), group=group)
     return parts.view(world, m), words
+
+
+class SparseExchange:
+    """The sparse exchange of one rank, per step: all_gather of the payload
+    sizes, all_gather of the payloads, the OR pass.  The payload all_gather
+    needs its size on the host, and reading the sizes there stalls the stream
+    (the GPU then idles while the host enqueues the rest of the step).  So the
+    payload gather and the OR pass are issued speculatively, BEFORE the sizes
+    are read, with ``slack`` x the largest size of the last ``history`` steps;
+    only when a rank's payload turns out larger (every rank sees the same
+    sizes, so every rank takes the same decision) are they issued again with
+    the real size.  Exact either way: a payload is read only up to its own
+    header's size, and a gather at least that large holds all of it."""
+
+    def __init__(self, group=None, slack: float = 1.25, history: int = 8):
+        self.group = group
+        self.slack = slack
+        self.history = history
+        self._max = []          # largest payload (words) of the recent steps
+        self.words = []         # words every rank shipped, per step
+        self.respecified = 0    # steps whose speculative size was too small
+
+    def _gather(self, payload, m: int):
+        import torch
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
+        mine = payload[:m]
+        if mine.numel() < m:                  # a host payload is exactly its size
+            mine = torch.cat([mine, torch.zeros(m - mine.numel(), dtype=mine.dtype, device=mine.device)])
+        parts = torch.empty(world * m, dtype=torch.int32, device=payload.device)
+        dist.all_gather_into_tensor(parts, mine.contiguous(), group=self.group)
+        return parts.view(world, m)
+
+    def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+        import torch
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
+        used = payload[:1].to(torch.int64)
+        sizes = torch.empty(world, dtype=torch.int64, device=payload.device)
+        dist.all_gather_into_tensor(sizes, used, group=self.group)
+        guess = 0
+        if self._max:
+            # the same value on every rank (the sizes were gathered), never above a payload's capacity
+            guess = min(payload_capacity(B, vocab), (int(max(self._max) * self.slack) + 3) & ~3)
+            res = or_payloads(self._gather(payload, guess), B, vocab, shift, out=out, unpack=unpack)
+        words = [int(x) for x in sizes.tolist()]
+        m = max(words)
+        self.words.append(words)
+        self._max = (self._max + [m])[-self.history:]
+        if guess and m <= guess:
+            return res
+        if guess:
+            self.respecified += 1
+        return or_payloads(self._gather(payload, m), B, vocab, shift, out=out, unpack=unpack)
 
 
 def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
@@ -486,5 +546,5 @@ def unpack_bits(packed, vocab: int):
 
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
            "ShardedIndex",
-           "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "gather_payloads", "or_payloads",
+           "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "gather_payloads", "or_payloads", "SparseExchange",
            "pack_payload_host", "or_payloads_host"]
