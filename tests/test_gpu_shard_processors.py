@@ -172,3 +172,52 @@ def test_sharded_processor_guards(indexes):
              for s in shards]
     with pytest.raises(FMIndexError):
         _drive(procs, ids[:, :5], scores)
+
+
+def test_sparse_exchange_over_rccl_world_one(indexes):
+    """The RCCL code path of the sparse exchange (SparseExchange: the sizes
+    all_gather, the speculative payload gather + OR, the re-issue when a
+    payload outgrows the guess) and of ShardedIndex.or_bits, on a world of
+    one rank: ShardedDecoder(reduce="sparse") over the whole corpus as its
+    only shard == the unsharded masks, and the sharded processor == the
+    unsharded one."""
+    import socket
+
+    import torch.distributed as dist
+
+    import fmidx.processors as P
+    from fmidx.sharding import ShardedDecoder, ShardedIndex
+
+    docs, full, shards = indexes
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", world_size=1, rank=0,
+                            device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(7)
+        F = [t for d in reversed(docs) for t in d]
+        B = 64
+        starts = rng.integers(0, len(F) - 40, size=B)
+        pats = [F[a:a + 3] for a in starts]
+        dec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="sparse", halo=None)
+        dec.start(pats, "cuda")
+        for step in range(12):
+            tok = [F[a + 3 + step] if rng.random() < 0.8 else int(rng.integers(0, 2000)) for a in starts]
+            if step == 6:          # every row restarts: wide ranges, a payload far above the guess
+                tok = [-1] * B
+            got = dec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
+            want = full.allowed_mask(dec.lo, dec.hi, V, 10)
+            assert torch.equal(got, want), step
+        assert dec._xchg.respecified >= 1          # the restart step outgrew the speculative size
+        occ = full.occurring_distinct
+        mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
+        ref = mk(full)
+        sp = mk(ShardedIndex(full, occ, group=dist.group.WORLD))
+        for step in range(4):
+            ids = torch.tensor([[1] + F[a:a + 2 + step] for a in starts[:8]], dtype=torch.int64).cuda()
+            scores = torch.from_numpy(rng.standard_normal((8, V)).astype(np.float32)).cuda()
+            assert torch.equal(sp(ids, scores.clone()).view(torch.int32), ref(ids, scores.clone()).view(torch.int32))
+    finally:
+        dist.destroy_process_group()
