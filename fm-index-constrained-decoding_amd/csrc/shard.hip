@@ -362,9 +362,15 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   const uint32_t W4 = (W + 3) / 4;
   for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
   if (t < nparts) {
+    // a row whose data lies past the part's end (a gather shorter than the payload: the
+    // speculative all_gather of SparseExchange, redone in full when it was too short) is read as
+    // empty -- never beyond the part
     const uint32_t* pp = parts + (uint64_t)t * stride;
-    s_desc[t] = pp[4 + b];
-    s_off[t] = pp[4 + B + b];
+    const uint32_t d = pp[4 + b], o = pp[4 + B + b];
+    const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
+    const bool inside = o >= 4 + 2 * B && end <= stride;
+    s_desc[t] = inside ? d : 0u;
+    s_off[t] = inside ? o : 0u;
   }
   or_lds_barrier();
   if (t == 0) {

@@ -485,6 +485,8 @@ def or_payloads_host(parts, B: int, vocab: int, shift: int, unpack: bool = True)
         for b in range(B):
             d, o = int(p[4 + b]), int(p[4 + B + b])
             cnt = d & 0x7FFFFFFF
+            if o + ((cnt + 3) & ~3) > p.size:   # past a short gather's end: read as empty (fm_shard_or_rows too)
+                continue
             if d >> 31:
                 bits[b] |= np.unpackbits(p[o:o + W].view(np.uint8), bitorder="little")
             else:

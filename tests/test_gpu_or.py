@@ -129,3 +129,36 @@ def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
                                                                            unpack=False))
     if V > 1000:   # most rows ship a slice, not a 16-KB bitmap
         assert sum(p.numel() for p in payloads) * 4 < world * B * W * 4 / 2
+
+
+def test_sparse_or_reads_nothing_past_a_short_gather(dev):
+    """A gather shorter than a payload (SparseExchange's speculative size,
+    redone in full afterwards) must not make fm_shard_or_rows read past the
+    part: rows whose data does not fit are read as empty -- the same rule as
+    the host reader."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from fmidx.sharding import or_payloads, or_payloads_host
+
+    rng = np.random.default_rng(3)
+    docs = [rng.integers(0, 300, size=int(rng.integers(5, 200))).tolist() for _ in range(200)]
+    ix = FMIndex()
+    ix.initialize(docs, in_memory=True)
+    V, B = 400, 48
+    F = [t for d in reversed(docs) for t in d]
+    pats = [[]] * 6 + [F[s:s + 1] for s in rng.integers(0, len(F) - 2, B - 6)]
+    lo, hi = ix.get_range_batch(pats, 10)
+    lo_t = torch.tensor(lo.astype(np.int64), device=dev)
+    hi_t = torch.tensor(hi.astype(np.int64), device=dev)
+    bits = ix.allowed_mask(lo_t, hi_t, V, 10, packed=True)
+    pay = ix.shard_pack(lo_t, hi_t, bits, V)
+    used = int(pay[0].item())
+    H = 4 + ((2 * B + 3) & ~3)
+    for m in (H, H + 8, (H + used) // 2 // 4 * 4, used):
+        parts = pay[:m].unsqueeze(0).contiguous()
+        got = or_payloads(parts, B, V, 10)
+        want = or_payloads_host(parts.cpu(), B, V, 10)
+        assert torch.equal(got.cpu(), want), m
+    full = or_payloads(pay[:used].unsqueeze(0).contiguous(), B, V, 10)
+    assert torch.equal(full, ix.allowed_mask(lo_t, hi_t, V, 10))
