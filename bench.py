@@ -446,15 +446,19 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     then every rank indexes its doc range + halo (one slice of T', built on the
     device) and decodes all B rows against it into bit-packed rows.  A step is
     the fused LF + packed mask (fm_decode_step_batch), then the exchange:
-    "sparse" (the default) -- fm_shard_pack (per row the shard's BWT slice when
-    smaller than the bitmap, else the bitmap), an all_gather of the payload
-    sizes (read on the host), an all_gather of the payloads and ONE fused OR /
-    scatter / unpack pass (fm_shard_or_rows); "dense" -- RCCL all_gather of
-    every row's packed bitmap and fm_or_bits.  Both are timed over the same K
-    steps; the last step's mask of each must equal the replica's."""
+    "dense" -- RCCL all_gather of every row's packed bitmap and fm_or_bits;
+    "sparse" -- fm_shard_pack (per row the shard's BWT slice when smaller than
+    the bitmap, else the bitmap), an all_gather of the payload sizes (read on
+    the host), an all_gather of the payloads and ONE fused OR / scatter /
+    unpack pass (fm_shard_or_rows); "peer" -- the same payloads packed into
+    IPC-mapped buffers, a one-element RCCL all_reduce as the stream-ordered
+    barrier, and the OR pass reading every rank's payload in place over xGMI
+    (fm_shard_or_rows_peers).  Each is timed over the same K steps and the
+    last step's mask of each must equal the replica's; ``value`` is the
+    fastest exact one.  FMIDX_BENCH_PEER=0 leaves the peer mode out."""
     import torch.distributed as dist
 
-    from fmidx.sharding import SparseExchange, or_bits, shard_text_device
+    from fmidx.sharding import PeerExchange, SparseExchange, or_bits, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
     S = W + K
@@ -494,6 +498,18 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     payload = None
     words_seen = []
     xchg = SparseExchange(None)
+    peer, peer_err = None, ""
+    if os.environ.get("FMIDX_BENCH_PEER", "1") != "0":
+        try:
+            peer = PeerExchange(None, B, V, dev)
+        except Exception as e:   # every rank learns of it below
+            peer_err = repr(e)
+        ok_all = torch.tensor([0 if peer_err else 1], device=dev)
+        dist.all_reduce(ok_all, op=dist.ReduceOp.MIN)
+        if not int(ok_all.item()):
+            if peer is not None:
+                peer.close()
+            peer, peer_err = None, peer_err or "the peer mapping failed on another rank"
 
     def run(mode):
         nonlocal payload
@@ -508,6 +524,10 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
             if mode == "dense":
                 dist.all_gather_into_tensor(parts, mine)
                 or_bits(parts, V, out=out)
+            elif mode == "peer":
+                pay = peer.payload()
+                ix.shard_pack(dst[0], dst[1], mine, V, payload=pay)
+                peer(pay, B, V, SHIFT, out=out)
             else:
                 payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
                 xchg(payload, B, V, SHIFT, out=out)
@@ -535,23 +555,40 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
         return float(t.item()), bool(ok.item())
 
     ms_dense, exact_dense = run("dense")
-    ms, exact = run("sparse")
-    st = ix.stats()
+    ms_sparse, exact_sparse = run("sparse")
     per_step = [sum(w) for w in words_seen]
-    return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": B / (ms / 1e3),
-            "unit": "masks/s", "ms_per_step": ms, "scaling": "strong", "shards": world, "halo": halo,
-            "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": ix.size(),
+    modes = {
+        "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
+                  "exchange_bytes_per_step": world * B * Wd * 4,
+                  "step": "RCCL all_gather of the packed rows + fm_or_bits"},
+        "sparse": {"ms_per_step": ms_sparse, "value": B / (ms_sparse / 1e3), "masks_equal_unsharded": exact_sparse,
+                   "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
+                   "speculative_gathers_respecified": xchg.respecified,
+                   "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
+                                                       if words_seen else None),
+                   "step": "fm_shard_pack, all_gather of sizes (host read) + payloads, fm_shard_or_rows"},
+    }
+    if peer is not None:
+        ms_peer, exact_peer = run("peer")
+        peer.close()
+        modes["peer"] = {"ms_per_step": ms_peer, "value": B / (ms_peer / 1e3), "masks_equal_unsharded": exact_peer,
+                         "exchange_bytes_per_step_median": modes["sparse"]["exchange_bytes_per_step_median"],
+                         "step": "fm_shard_pack into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
+                                 "fm_shard_or_rows_peers reading every rank's payload over xGMI"}
+    else:
+        modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
+    exact_modes = [m for m, r in modes.items() if r.get("masks_equal_unsharded")]
+    best = min(exact_modes, key=lambda m: modes[m]["ms_per_step"]) if exact_modes else "sparse"
+    st = ix.stats()
+    return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": modes[best]["value"],
+            "unit": "masks/s", "ms_per_step": modes[best]["ms_per_step"], "scaling": "strong", "shards": world,
+            "halo": halo, "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": ix.size(),
             "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
-            "masks_equal_unsharded": exact,
-            "exchange": "sparse: per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",
-            "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
-            "speculative_gathers_respecified": xchg.respecified,
-            "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
-                                                if words_seen else None),
-            "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
-                      "exchange_bytes_per_step": world * B * Wd * 4},
-            "step": "fused LF + packed mask; sparse payload (fm_shard_pack), all_gather of sizes (host read) + "
-                    "payloads, fused OR / scatter / unpack (fm_shard_or_rows) to uint8 [B, V]; eager launches"}
+            "masks_equal_unsharded": bool(exact_modes) and modes[best]["masks_equal_unsharded"],
+            "exchange": best, "modes": modes,
+            "payload": "per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",
+            "step": "fused LF + packed mask, then the exchange of 'exchange' (modes: each timed over the same K "
+                    "steps), uint8 [B, V] out; eager launches"}
 
 
 COMPACT_ENV = {"FMIDX_TRANS": "1", "FMIDX_LF_E": "0", "FMIDX_PROBE_FIRST": "0"}

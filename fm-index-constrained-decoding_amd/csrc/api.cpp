@@ -1278,6 +1278,56 @@ int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_str
   FM_API_END
 }
 
+int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                           uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
+  FM_API_BEGIN
+  return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
+                                           reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_ipc_handle(const void* d_ptr, uint8_t* handle, uint64_t* offset) {
+  FM_API_BEGIN
+  if (!d_ptr || !handle || !offset) {
+    set_error("ipc_handle: null argument");
+    return -1;
+  }
+  // the handle names the whole allocation (torch's caching allocator hands out pieces of
+  // larger blocks): the peer adds the offset to the base it maps
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  FM_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(d_ptr)));
+  hipIpcMemHandle_t hd;
+  FM_HIP(hipIpcGetMemHandle(&hd, base));
+  static_assert(sizeof(hd) == FM_IPC_HANDLE_BYTES, "hipIpcMemHandle_t size");
+  std::memcpy(handle, &hd, sizeof(hd));
+  *offset = (uint64_t)(static_cast<const char*>(d_ptr) - static_cast<const char*>(base));
+  return 0;
+  FM_API_END
+}
+
+int fm_ipc_open(const uint8_t* handle, void** d_base) {
+  FM_API_BEGIN
+  if (!handle || !d_base) {
+    set_error("ipc_open: null argument");
+    return -1;
+  }
+  hipIpcMemHandle_t hd;
+  std::memcpy(&hd, handle, sizeof(hd));
+  *d_base = nullptr;
+  FM_HIP(hipIpcOpenMemHandle(d_base, hd, hipIpcMemLazyEnablePeerAccess));
+  return 0;
+  FM_API_END
+}
+
+int fm_ipc_close(void* d_base) {
+  FM_API_BEGIN
+  if (!d_base) return 0;
+  FM_HIP(hipIpcCloseMemHandle(d_base));
+  return 0;
+  FM_API_END
+}
+
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream) {
   FM_API_BEGIN

@@ -310,67 +310,67 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   }
 }
 
-// One workgroup (1024 threads) per row.  Two roles, as in k_decode (loads and
-// stores share vmcnt in issue order, so a wave with stores in flight cannot
-// wait on a load without waiting for them too):
-//   waves 4..15 (uint8 output)  zero-fill the row's 128 KB at once, overlapping
-//               the loads, and later store only the 16-token chunks that hold
-//               an allowed token (the same thread wrote the zeros of that
-//               chunk: program order on one address, no wait);
-//   waves 0..3  stage every part's (desc, off) for the row in LDS (one round
-//               trip), then load the dense parts' words (16-B loads, two parts
-//               per round) and the first 1024 sparse symbols (one flat index
-//               space over the parts' lists) together, OR the words into the
-//               LDS bitmap and set the symbols' bits with LDS atomics.
-// Barriers are LDS-only (s_waitcnt lgkmcnt(0); s_barrier): nothing that
-// crosses them is global data, so the zero stores need not drain.
+// One workgroup (1024 threads) per row.  Every part's (desc, off) for the row
+// is staged in LDS (one round trip), then the dense parts' words (16-B loads,
+// eight parts per round: all 8 shards of a wide row are dense) and the first
+// 4096 sparse symbols (one flat index space over the parts' lists) load
+// together; the words are ORed into the LDS bitmap and the symbols' bits set
+// with LDS atomics; the row is stored once, each 16-token chunk by one thread.
+// Barriers are LDS-only (s_waitcnt lgkmcnt(0); s_barrier).  (A variant whose
+// store waves zero-filled the row while the loads were in flight measured
+// slower, 17-56 us against 11-31: profiles/r04_or/.)
+//
+// PEERS = false: part p is parts + p * stride (an all_gather's output).
+// PEERS = true:  part p is ptrs[p], a peer rank's payload buffer mapped over
+//                xGMI (fm_ipc_open), of cap words; every load of it is a
+//                system-scope (sc0 sc1) load, so no line of an earlier step's
+//                payload (double-buffered: the same buffer two steps ago) is
+//                served from this GPU's caches.
 constexpr int kOrRowThreads = 1024;
 constexpr int kOrRowMaxWords = 8 * kOrRowThreads;   // V <= 262144
 constexpr int kOrMaxParts = 64;
+constexpr int kSysLoadAux = 1 | 16;                 // sc0 sc1
+
+typedef const __attribute__((address_space(1))) uint32_t g32_t;
 
 __device__ __forceinline__ void or_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// EARLY = false: no zero-fill -- every thread loads, and every chunk is stored once at the end.
-template <bool EARLY>
-__global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts, uint32_t nparts,
+template <bool PEERS>
+__device__ __forceinline__ uint32_t part_word(const uint32_t* base, uint64_t i) {
+  g32_t* p = (g32_t*)(base + i);   // a global load, not a flat one (the base may come from LDS)
+  if constexpr (PEERS) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else return *p;
+}
+
+template <bool PEERS>
+__global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts,
+                                                            const uint64_t* __restrict__ ptrs, uint32_t nparts,
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
                                                             int unpack) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
   __shared__ uint32_t s_desc[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
+  __shared__ uint64_t s_base[PEERS ? kOrMaxParts : 1];
   __shared__ uint32_t s_nd;
-  constexpr int kOrLoadThreads = EARLY ? 256 : kOrRowThreads;   // EARLY: waves 0..3
   const uint64_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
-  const bool loader = t < (uint32_t)kOrLoadThreads;
-  uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
-  const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
-  const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-  const uint32_t nch = (uint32_t)((vocab + 15) / 16);
-  constexpr uint32_t kZ = EARLY ? kOrRowThreads - kOrLoadThreads : 1;   // store-only threads
-  if (EARLY && unpack && !loader) {
-    for (uint32_t c = t - kOrLoadThreads; c < nch; c += kZ) {
-      const uint64_t t0 = 16ull * c;
-      if (t0 + 16 <= vocab && aligned) {
-        or_v4u z = {0u, 0u, 0u, 0u};
-        __builtin_amdgcn_raw_buffer_store_b128(z, r, (uint32_t)t0, 0, kOrStoreAux);
-      } else {
-        for (uint64_t i = 0; i < 16 && t0 + i < vocab; ++i) row[t0 + i] = 0;
-      }
-    }
-  }
+  auto base_of = [&](uint32_t p) -> const uint32_t* {
+    if constexpr (PEERS) return reinterpret_cast<const uint32_t*>(s_base[p]);
+    else return parts + (uint64_t)p * stride;
+  };
   const uint32_t W4 = (W + 3) / 4;
   for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
   if (t < nparts) {
     // a row whose data lies past the part's end (a gather shorter than the payload: the
     // speculative all_gather of SparseExchange, redone in full when it was too short) is read as
     // empty -- never beyond the part
-    const uint32_t* pp = parts + (uint64_t)t * stride;
-    const uint32_t d = pp[4 + b], o = pp[4 + B + b];
+    const uint32_t* pp = PEERS ? reinterpret_cast<const uint32_t*>(ptrs[t]) : parts + (uint64_t)t * stride;
+    const uint32_t d = part_word<PEERS>(pp, 4 + b), o = part_word<PEERS>(pp, 4 + B + b);
     const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
     const bool inside = o >= 4 + 2 * B && end <= stride;
     s_desc[t] = inside ? d : 0u;
     s_off[t] = inside ? o : 0u;
+    if constexpr (PEERS) s_base[t] = reinterpret_cast<uint64_t>(pp);
   }
   or_lds_barrier();
   if (t == 0) {
@@ -386,78 +386,84 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   or_lds_barrier();
   const uint32_t nd = s_nd;
   const uint32_t total = s_pre[nparts];
-  if (loader) {
-    auto sym_at = [&](uint32_t i) -> uint32_t {
-      uint32_t p = 0;                                     // the part whose list holds flat index i
-      for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
-        if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
-      return parts[(uint64_t)p * stride + s_off[p] + (i - s_pre[p])];
-    };
-    // the first 1024 sparse symbols, loaded with the first dense round
-    uint32_t sym0[4];
+  auto sym_at = [&](uint32_t i) -> uint32_t {
+    uint32_t p = 0;                                     // the part whose list holds flat index i
+    for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
+      if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
+    return part_word<PEERS>(base_of(p), s_off[p] + (i - s_pre[p]));
+  };
+  // the first 4096 sparse symbols, loaded with the first dense round
+  uint32_t sym0[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrLoadThreads + t, total - 1)) : 0u;
-    constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrLoadThreads);   // W <= 8192 words
-    const uint32_t slots = (W4 + kOrLoadThreads - 1) / kOrLoadThreads;
-    uint4 acc[kSlots4];
+  for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrRowThreads + t, total - 1)) : 0u;
+  constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);   // W <= 8192 words
+  const uint32_t slots = (W4 + kOrRowThreads - 1) / kOrRowThreads;
+  uint4 acc[kSlots4];
 #pragma unroll
-    for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
-    // parts per round: all 8 shards of a wide row are dense, so a round covers 8 (2 slots per
-    // thread) -- 4 when the loaders are 256 threads (8 slots each)
-    constexpr int kPB = EARLY ? 2 : 8;
-    for (uint32_t j0 = 0; j0 < nd; j0 += kPB) {
-      const uint4* src[kPB];
+  for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
+  constexpr int kPB = 8;
+  for (uint32_t j0 = 0; j0 < nd; j0 += kPB) {
+    uint4 x[kPB][kSlots4];
 #pragma unroll
-      for (int q = 0; q < kPB; ++q) {
-        const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
-        src[q] = reinterpret_cast<const uint4*>(parts + (uint64_t)p * stride + s_off[p]);
-      }
-      uint4 x[kPB][kSlots4];
-#pragma unroll
-      for (int q = 0; q < kPB; ++q)
-#pragma unroll
-        for (int k = 0; k < kSlots4; ++k)
-          x[q][k] = (uint32_t)k < slots ? src[q][min(t + k * kOrLoadThreads, W4 - 1)] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < kPB; ++q)
+    for (int q = 0; q < kPB; ++q) {
+      const uint32_t p = s_dense[min(j0 + q, nd - 1)];   // past the last: the last again (harmless for an OR)
+      const uint32_t* src = base_of(p) + s_off[p];
+      if constexpr (PEERS) {
+        // workgroup-uniform part: one buffer resource over the row's W words
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, 16u * W4);
 #pragma unroll
         for (int k = 0; k < kSlots4; ++k) {
-          acc[k].x |= x[q][k].x;
-          acc[k].y |= x[q][k].y;
-          acc[k].z |= x[q][k].z;
-          acc[k].w |= x[q][k].w;
+          if ((uint32_t)k < slots) {
+            const or_v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * min(t + k * kOrRowThreads, W4 - 1), 0,
+                                                                   kSysLoadAux);
+            x[q][k] = make_uint4(v.x, v.y, v.z, v.w);
+          } else {
+            x[q][k] = make_uint4(0, 0, 0, 0);
+          }
         }
+      } else {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+        for (int k = 0; k < kSlots4; ++k)
+          x[q][k] = (uint32_t)k < slots ? s4[min(t + k * kOrRowThreads, W4 - 1)] : make_uint4(0, 0, 0, 0);
+      }
     }
-    if (nd) {
+#pragma unroll
+    for (int q = 0; q < kPB; ++q)
 #pragma unroll
       for (int k = 0; k < kSlots4; ++k) {
-        const uint32_t w4 = t + k * kOrLoadThreads;
-        if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
+        acc[k].x |= x[q][k].x;
+        acc[k].y |= x[q][k].y;
+        acc[k].z |= x[q][k].z;
+        acc[k].w |= x[q][k].w;
       }
-    }
-    // the dense words are in place before any symbol's bit is ORed in (same threads, then a
-    // wave-level LDS fence: other loader waves' words may share a symbol's word)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+  }
+  if (nd) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t tok = (int64_t)sym0[u] - shift;
-      if (u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+    for (int k = 0; k < kSlots4; ++k) {
+      const uint32_t w4 = t + k * kOrRowThreads;
+      if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
+    }
+  }
+  // the dense words are in place before any symbol's bit is ORed in (other waves' words may
+  // share a symbol's word)
+  or_lds_barrier();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t tok = (int64_t)sym0[u] - shift;
+    if (u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
+      atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+  }
+  for (uint32_t i0 = 4 * kOrRowThreads; i0 < total; i0 += 8 * kOrRowThreads) {   // long lists: 8 per round
+    uint32_t sym[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sym[u] = sym_at(min(i0 + u * kOrRowThreads + t, total - 1));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t tok = (int64_t)sym[u] - shift;
+      if (i0 + u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
         atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
     }
-    for (uint32_t i0 = 4 * kOrLoadThreads; i0 < total; i0 += 8 * kOrLoadThreads) {   // long lists: 8 per round
-      uint32_t sym[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sym[u] = sym_at(min(i0 + u * kOrLoadThreads + t, total - 1));
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t tok = (int64_t)sym[u] - shift;
-        if (i0 + u * kOrLoadThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
-          atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
-      }
-    }
-  } else {
-    __builtin_amdgcn_s_barrier();    // the loaders' mid-phase barrier (every wave takes part)
   }
   or_lds_barrier();
   if (!unpack) {
@@ -465,13 +471,13 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     for (uint32_t w = t; w < W; w += kOrRowThreads) o[w] = s_bits[w];
     return;
   }
-  if (EARLY && loader) return;
-  // EARLY: the non-zero chunks, by the threads that zero-filled them; else every chunk
-  const uint32_t c0 = EARLY ? t - kOrLoadThreads : t, cstep = EARLY ? kZ : kOrRowThreads;
-  for (uint32_t c = c0; c < nch; c += cstep) {
+  uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
+  const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+  const uint32_t nch = (uint32_t)((vocab + 15) / 16);
+  for (uint32_t c = t; c < nch; c += kOrRowThreads) {
     const uint64_t t0 = 16ull * c;
     const uint32_t bits16 = (s_bits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-    if (EARLY && !bits16) continue;
     uint32_t q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) q[i] = (((bits16 >> (4 * i)) & 0xFu) * 0x204081u) & 0x01010101u;
@@ -527,16 +533,26 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
     set_error("shard_or_rows: the payloads must start on 16-B boundaries (stride a multiple of 4 words)");
     return -1;
   }
-  static const bool early = [] {
-    const char* e = std::getenv("FMIDX_OR_ROWS_EARLY");
-    return e && *e && std::atoi(e) != 0;
-  }();
-  if (early)
-    k_or_rows<true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B,
-                                                                         (uint32_t)W, vocab, shift, out, ld, unpack);
-  else
-    k_or_rows<false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, (uint32_t)nparts, stride, B,
-                                                                          (uint32_t)W, vocab, shift, out, ld, unpack);
+  k_or_rows<false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, nullptr, (uint32_t)nparts, stride, B,
+                                                                        (uint32_t)W, vocab, shift, out, ld, unpack);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
+                               int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s) {
+  const uint64_t W = (vocab + 31) / 32;
+  if (!ptrs || !out || !nparts || nparts > (uint64_t)kOrMaxParts || W > (uint64_t)kOrRowMaxWords ||
+      cap < shard_payload_capacity(B, vocab) || cap >= (1ull << 30) ||
+      (unpack ? ld < vocab : (ld < 4 * W || ld % 4))) {
+    set_error("shard_or_rows_peers: bad arguments (parts %llu, cap %llu words, vocab %llu, ld %llu)",
+              (unsigned long long)nparts, (unsigned long long)cap, (unsigned long long)vocab,
+              (unsigned long long)ld);
+    return -1;
+  }
+  if (B == 0) return 0;
+  k_or_rows<true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(nullptr, ptrs, (uint32_t)nparts, cap, B,
+                                                                       (uint32_t)W, vocab, shift, out, ld, unpack);
   FM_HIP(hipGetLastError());
   return 0;
 }

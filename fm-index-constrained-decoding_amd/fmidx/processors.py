@@ -403,8 +403,10 @@ class _ShardedDeviceStep(_DeviceStep):
         h = self.prep(input_ids, scores, cfg)
         if h is None:
             return None
+        # the peer exchange packs first: the facts all_reduce is then its barrier
+        staged = self.sidx.stage(h["mlo"], h["mhi"], h["bits"], h["V"])
         facts = self.sidx.sum_facts(h["facts"])
-        bits = self.sidx.or_bits(h["mlo"], h["mhi"], h["bits"], h["V"])
+        bits = self.sidx.or_bits(h["mlo"], h["mhi"], h["bits"], h["V"], staged=staged)
         return self.finish(h, facts, bits)
 
 

@@ -25,7 +25,10 @@ GPU -- the sparse exchange: each rank ships, per row, its shard's BWT slice
 when that is smaller than the row's bitmap, else the bitmap (fm_shard_pack;
 most rows are a few rows wide on a shard), one tiny all_gather of the payload
 sizes, one all_gather of the payloads (the largest rank's prefix), then one
-fused OR / scatter / unpack pass (fm_shard_or_rows).
+fused OR / scatter / unpack pass (fm_shard_or_rows).  The peer exchange
+(PeerExchange) ships nothing: every rank maps the others' payload buffers once
+(hipIpc over xGMI) and, after one stream-ordered barrier, the OR pass reads
+them in place (fm_shard_or_rows_peers) -- no host read of sizes, no gather.
 """
 from __future__ import annotations
 
@@ -114,17 +117,21 @@ class ShardedDecoder:
     """
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8",
-                 halo: Optional[int] = None):
+                 halo: Optional[int] = None, peer_barrier: str = "collective"):
         """reduce: "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
-        (all_gather of the packed rows + fm_or_bits) or "sparse" (BWT slices /
-        bitmaps per row, fm_shard_pack + fm_shard_or_rows)."""
+        (all_gather of the packed rows + fm_or_bits), "sparse" (BWT slices /
+        bitmaps per row, fm_shard_pack + all_gather + fm_shard_or_rows) or
+        "peer" (the same payloads read in place over xGMI: PeerExchange, whose
+        ``barrier`` is ``peer_barrier``)."""
         self.index = index
         self.vocab = vocab
         self.shift = shift
         self.group = group
-        if reduce not in ("max_u8", "gather_bits", "sparse"):
+        if reduce not in ("max_u8", "gather_bits", "sparse", "peer"):
             raise ValueError(reduce)
         self.reduce = reduce
+        self.peer_barrier = peer_barrier
+        self._peer = None      # its PeerExchange (reduce="peer")
         self.halo = halo
         self.fused = hasattr(index, "decode_step")
         self.lo = None
@@ -182,7 +189,7 @@ class ShardedDecoder:
         if not self.fused:
             self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
             return self.mask()
-        packed = self.group is not None and self.reduce in ("gather_bits", "sparse")
+        packed = self.group is not None and self.reduce in ("gather_bits", "sparse", "peer")
         if self._buf is None:
             B = self.lo.numel()
             if packed:
@@ -197,7 +204,28 @@ class ShardedDecoder:
         self.hi, self._hi2 = self._hi2, self.hi
         if self.group is not None and self.reduce == "sparse":
             return self._combine_sparse(self._buf)
+        if self.group is not None and self.reduce == "peer":
+            return self._combine_peer(self._buf)
         return self._combine(self._buf, packed)
+
+    def _combine_peer(self, bits):
+        import torch
+
+        B = self.lo.numel()
+        if self._peer is None or self._peer.rows < B:
+            self.close()
+            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier)
+        pay = self._peer.payload()
+        self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=pay)
+        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
+            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=pay.device)
+        return self._peer(pay, B, self.vocab, self.shift, out=self._out)
+
+    def close(self):
+        """Release the peer exchange's mappings (collective: every rank calls it)."""
+        if self._peer is not None:
+            self._peer.close()
+            self._peer = None
 
     def _combine_sparse(self, bits):
         """The sparse exchange of this step's rows (new state self.lo/hi,
@@ -268,7 +296,9 @@ class ShardedIndex:
     corpus's all-unigram list (index.py:67 -- it excludes BWT row n - 1 of
     the unsharded index, so it is not the union of the shards' lists; take it
     from the corpus's index metadata).  ``exchange``: "sparse" (per row the
-    shard's BWT slice or bitmap) or "dense" (every row's bitmap).  A pattern
+    shard's BWT slice or bitmap, all_gathered), "peer" (the same payloads read
+    in place over xGMI, PeerExchange; the facts all_reduce, issued after the
+    pack, is its barrier) or "dense" (every row's bitmap).  A pattern
     longer than ``halo`` - 1 tokens raises HaloExceeded; stop_at_count must
     be 0 (counts include halo duplicates), and inputs that need the host path
     (rows without exactly one end marker, boost overflow) raise.  The
@@ -276,9 +306,12 @@ class ShardedIndex:
     index's business and is not offered here."""
 
     def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "sparse",
-                 shift: int = 10):
-        if exchange not in ("sparse", "dense"):
+                 shift: int = 10, peer_barrier: str = "collective"):
+        if exchange not in ("sparse", "dense", "peer"):
             raise ValueError(exchange)
+        self.peer_barrier = peer_barrier
+        self._peer = None
+        self._staged = False
         self.shard = shard
         self.occurring_distinct = list(occurring_distinct)
         self.group = group
@@ -301,14 +334,41 @@ class ShardedIndex:
             dist.all_reduce(facts, op=dist.ReduceOp.SUM, group=self.group)
         return facts
 
-    def or_bits(self, lo, hi, bits, vocab: int):
-        """OR of every rank's packed allowed bits (int32 [B, W]) -> int32 [B, W]."""
+    def stage(self, lo, hi, bits, vocab: int) -> bool:
+        """The peer exchange's pack, issued before the facts all_reduce so that
+        it is the exchange's barrier.  True when staged that way."""
+        if self.group is None or self.exchange != "peer":
+            return False
+        B = lo.numel()
+        if self._peer is None or self._peer.rows < B or self._peer.vocab != vocab:
+            self.close()
+            self._peer = PeerExchange(self.group, B, vocab, lo.device, barrier=self.peer_barrier)
+        self.shard.shard_pack(lo, hi, bits, vocab, payload=self._peer.payload())
+        self._staged = True
+        return self.peer_barrier == "collective"
+
+    def close(self):
+        """Release the peer exchange's mappings (collective: every rank calls it)."""
+        if self._peer is not None:
+            self._peer.close()
+            self._peer = None
+
+    def or_bits(self, lo, hi, bits, vocab: int, staged: bool = False):
+        """OR of every rank's packed allowed bits (int32 [B, W]) -> int32 [B, W].
+        ``staged``: stage() packed this step's payload before a collective
+        every rank issued after it (the peer exchange's barrier)."""
         if self.group is None:
             return bits
         import torch
         import torch.distributed as dist
 
         B, W = lo.numel(), (vocab + 31) // 32
+        if self.exchange == "peer":
+            if not self._staged:
+                self.stage(lo, hi, bits, vocab)
+                staged = False          # packed just now: no collective has run since
+            self._staged = False
+            return self._peer(self._peer.payload(), B, vocab, self.shift, unpack=False, barrier_done=staged)
         if self.exchange == "sparse":
             self._payload = self.shard.shard_pack(lo, hi, bits, vocab, payload=self._payload)
             if self._xchg is None:
@@ -414,6 +474,142 @@ class SparseExchange:
         if guess:
             self.respecified += 1
         return or_payloads(self._gather(payload, m), B, vocab, shift, out=out, unpack=unpack)
+
+
+class PeerExchange:
+    """The sparse exchange with no gather and no host read: every rank packs
+    into one of two payload buffers of its own (double-buffered by step
+    parity), whose IPC handles the ranks swapped once at construction
+    (fm_ipc_handle / fm_ipc_open: the peers' buffers mapped over xGMI); after
+    a stream-ordered barrier, ONE launch (fm_shard_or_rows_peers) reads every
+    rank's payload in place and ORs them.
+
+    ``barrier``: "collective" -- a one-element all_reduce issued after the
+    pack (RCCL runs it after the rank's pack and completes it only when every
+    rank's has run, so the OR that follows on the stream sees every payload;
+    the processors pass ``barrier_done`` when their facts all_reduce, issued
+    after the pack, already is one); "host" -- synchronize + group barrier
+    (gloo; ranks sharing a GPU, where RCCL refuses to run).  Two buffers are
+    enough: a rank packs buffer k again two steps later, after a barrier that
+    every rank entered only after its OR of buffer k had been issued before it
+    on its stream.  ``capacity_rows``: the largest batch the buffers hold
+    (payload_capacity words each)."""
+
+    def __init__(self, group, capacity_rows: int, vocab: int, device, barrier: str = "collective"):
+        import torch
+        import torch.distributed as dist
+        from ctypes import byref, c_uint8, c_uint64, c_void_p
+
+        from ._lib import check, lib
+
+        if barrier not in ("collective", "host"):
+            raise ValueError(barrier)
+        self.group, self.barrier_mode, self.vocab = group, barrier, vocab
+        self.device = torch.device(device)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.rows = capacity_rows
+        self.cap = payload_capacity(capacity_rows, vocab)
+        self.bufs = [torch.zeros(self.cap, dtype=torch.int32, device=self.device) for _ in range(2)]
+        torch.cuda.synchronize(self.device)
+        mine = []
+        for b in self.bufs:
+            hd = (c_uint8 * 64)()
+            off = c_uint64(0)
+            check(lib().fm_ipc_handle(c_void_p(b.data_ptr()), hd, byref(off)), "ipc_handle")
+            mine.append((bytes(hd), int(off.value)))
+        every = [None] * self.world
+        dist.all_gather_object(every, mine, group=group)
+        self._opened = []
+        table = [[0] * self.world for _ in range(2)]
+        try:
+            for r, hs in enumerate(every):
+                for k, (hd, off) in enumerate(hs):
+                    if r == self.rank:
+                        table[k][r] = self.bufs[k].data_ptr()
+                        continue
+                    base = c_void_p()
+                    check(lib().fm_ipc_open((c_uint8 * 64).from_buffer_copy(hd), byref(base)), f"ipc_open (rank {r})")
+                    self._opened.append(base.value)
+                    table[k][r] = base.value + off
+        except Exception:
+            self._unmap()
+            raise
+        self.ptab = torch.tensor(table, dtype=torch.int64, device=self.device)
+        self._tok = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.step = 0
+
+    def payload(self):
+        """This step's payload buffer (pack into it, then call)."""
+        return self.bufs[self.step % 2]
+
+    def barrier(self):
+        import torch
+        import torch.distributed as dist
+
+        if self.barrier_mode == "collective":
+            dist.all_reduce(self._tok, group=self.group)
+        else:
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+
+    def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True,
+                 barrier_done: bool = False):
+        k = self.step % 2
+        if payload.data_ptr() != self.bufs[k].data_ptr():
+            raise ValueError("PeerExchange: pack into payload() of this step")
+        if B > self.rows or vocab != self.vocab:
+            raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
+        if not barrier_done:
+            self.barrier()
+        out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack)
+        self.step += 1
+        return out
+
+    def _unmap(self):
+        from ctypes import c_void_p
+
+        from ._lib import lib
+
+        for base in self._opened:
+            lib().fm_ipc_close(c_void_p(base))
+        self._opened = []
+
+    def close(self):
+        """Unmap the peers' buffers once no rank reads any buffer (a
+        synchronize + group barrier: no rank frees its buffers while a peer
+        may still read them)."""
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        self._unmap()
+
+
+def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+    """OR of the payloads at the device addresses ``ptrs`` (int64 [P], on the
+    GPU that runs the pass; each payload ``cap`` words, in this process or a
+    peer's buffer mapped by fm_ipc_open) -> uint8 [B, vocab] (unpack) or int32
+    [B, ceil(vocab/32)] words (fm_shard_or_rows_peers)."""
+    import torch
+    from ctypes import c_void_p
+
+    from ._lib import check, lib
+
+    W = (vocab + 31) // 32
+    if not (ptrs.is_cuda and ptrs.dtype == torch.int64 and ptrs.dim() == 1 and ptrs.is_contiguous()):
+        raise ValueError("ptrs: a contiguous int64 device tensor [P]")
+    if out is None:
+        out = (torch.empty((B, vocab), dtype=torch.uint8, device=ptrs.device) if unpack
+               else torch.empty((B, W), dtype=torch.int32, device=ptrs.device))
+    assert out.stride(1) == 1 and out.device == ptrs.device
+    ld = out.stride(0) * out.element_size()
+    stream = torch.cuda.current_stream(ptrs.device).cuda_stream
+    check(lib().fm_shard_or_rows_peers(c_void_p(ptrs.data_ptr()), ptrs.numel(), int(cap), B, vocab, int(shift),
+                                       c_void_p(out.data_ptr()), ld, 1 if unpack else 0, c_void_p(stream)),
+          "shard_or_rows_peers")
+    return out
 
 
 def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = True):

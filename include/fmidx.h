@@ -282,6 +282,25 @@ int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint6
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
                      int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
 
+/* The peer exchange (no host read, no gather): every rank packs into one of
+ * two payload buffers of fm_shard_payload_capacity words (double-buffered by
+ * step parity), whose IPC handles the ranks swapped once (fm_ipc_handle /
+ * fm_ipc_open: hipIpc*, the peer mapping over xGMI); after a stream-ordered
+ * barrier (any collective every rank issues after its pack, e.g. the
+ * processors' facts all_reduce), fm_shard_or_rows_peers reads the nparts
+ * payloads in place through d_part_ptrs (a device array of nparts addresses,
+ * each payload cap_words words), with system-scope loads, and ORs them as
+ * fm_shard_or_rows does.  fm_ipc_handle returns the allocation's handle
+ * (FM_IPC_HANDLE_BYTES) and d_ptr's offset in it; fm_ipc_open maps a peer's
+ * allocation (its base: add the offset); fm_ipc_close unmaps it.  Not in the
+ * reference (its OR-exchange is an all_gather). */
+#define FM_IPC_HANDLE_BYTES 64
+int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                           uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
+int fm_ipc_handle(const void* d_ptr, uint8_t* handle, uint64_t* offset);
+int fm_ipc_open(const uint8_t* handle, void** d_base);
+int fm_ipc_close(void* d_base);
+
 /* ---- logits-processor step on the device --------------------------------- */
 
 /* The per-row bookkeeping of the soft processors' _process

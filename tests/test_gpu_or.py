@@ -81,7 +81,7 @@ def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
     import torch
 
     from fmidx.index import FMIndex
-    from fmidx.sharding import or_bits, or_payloads, shard_corpus
+    from fmidx.sharding import or_bits, or_payloads, or_peer_payloads, payload_capacity, shard_corpus
 
     rng = np.random.default_rng(V + world)
     vocab_used = min(V, 3000)
@@ -129,6 +129,15 @@ def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
                                                                            unpack=False))
     if V > 1000:   # most rows ship a slice, not a 16-KB bitmap
         assert sum(p.numel() for p in payloads) * 4 < world * B * W * 4 / 2
+    # the peer exchange's pass: the same payloads read in place through a table of addresses
+    cap = payload_capacity(B, V)
+    bufs = [torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(world)]
+    for bf, p in zip(bufs, payloads):
+        bf[:p.numel()] = p
+    ptrs = torch.tensor([bf.data_ptr() for bf in reversed(bufs)], dtype=torch.int64, device=dev)
+    assert torch.equal(or_peer_payloads(ptrs, cap, B, V, 10), want)       # the OR does not care for order
+    assert torch.equal(or_peer_payloads(ptrs, cap, B, V, 10, unpack=False),
+                       or_payloads(parts, B, V, 10, unpack=False))
 
 
 def test_sparse_or_reads_nothing_past_a_short_gather(dev):

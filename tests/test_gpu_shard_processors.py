@@ -211,13 +211,25 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
             want = full.allowed_mask(dec.lo, dec.hi, V, 10)
             assert torch.equal(got, want), step
         assert dec._xchg.respecified >= 1          # the restart step outgrew the speculative size
+        # the peer exchange, its stream-ordered RCCL barrier (a world of one: the own buffer only)
+        pdec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="peer", halo=None)
+        pdec.start(pats, "cuda")
+        for step in range(6):
+            tok = [F[a + 3 + step] if rng.random() < 0.8 else -1 for a in starts]
+            got = pdec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
+            assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), step
+        pdec.close()
         occ = full.occurring_distinct
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         ref = mk(full)
-        sp = mk(ShardedIndex(full, occ, group=dist.group.WORLD))
-        for step in range(4):
-            ids = torch.tensor([[1] + F[a:a + 2 + step] for a in starts[:8]], dtype=torch.int64).cuda()
-            scores = torch.from_numpy(rng.standard_normal((8, V)).astype(np.float32)).cuda()
-            assert torch.equal(sp(ids, scores.clone()).view(torch.int32), ref(ids, scores.clone()).view(torch.int32))
+        for exchange in ("sparse", "peer"):
+            sidx = ShardedIndex(full, occ, group=dist.group.WORLD, exchange=exchange)
+            sp = mk(sidx)
+            for step in range(4):
+                ids = torch.tensor([[1] + F[a:a + 2 + step] for a in starts[:8]], dtype=torch.int64).cuda()
+                scores = torch.from_numpy(rng.standard_normal((8, V)).astype(np.float32)).cuda()
+                assert torch.equal(sp(ids, scores.clone()).view(torch.int32),
+                                   ref(ids, scores.clone()).view(torch.int32)), (exchange, step)
+            sidx.close()
     finally:
         dist.destroy_process_group()
