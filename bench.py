@@ -613,7 +613,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
     the same way and checked against the replica's uint8 mask.  The exchange
     itself (all_gather of 8 x B x V/8 bytes over xGMI) cannot run on one GPU;
     ``predicted_step_us`` adds a stated model of it."""
-    from fmidx.sharding import or_bits, or_payloads, shard_text_device
+    from fmidx.sharding import or_bits, or_payloads, or_peer_payloads, payload_capacity, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()
     S = W + K
@@ -786,6 +786,25 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         sp_cold = replay(g_sp, True) / K * 1e3
         exact_sparse = exact_sparse and bool(torch.equal(out, ref))
         del spk, g_sp, sp
+        # the peer exchange's pass (fm_shard_or_rows_peers) over the same 8 payloads, each in a
+        # buffer of its own of the full capacity, as the ranks' IPC-mapped buffers are (here local)
+        cap = payload_capacity(B, V)
+        pb = torch.zeros((K, world, cap), dtype=torch.int32, device=dev)
+        for r, p in enumerate(last_pay):
+            pb[:, r, :p.numel()] = p
+        ptabs = torch.tensor([[pb[i, r].data_ptr() for r in range(world)] for i in range(K)], dtype=torch.int64,
+                             device=dev)
+        out.zero_()
+        or_peer_payloads(ptabs[0], cap, B, V, SHIFT, out=out)
+        exact_peer = bool(torch.equal(out, ref))
+        g_pp = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_pp):
+            for i in range(K):
+                or_peer_payloads(ptabs[i], cap, B, V, SHIFT, out=out)
+        pp_warm = float(np.median([replay(g_pp, False) for _ in range(3)])) / K * 1e3
+        pp_cold = replay(g_pp, True) / K * 1e3
+        exact_peer = exact_peer and bool(torch.equal(out, ref))
+        del pb, ptabs, g_pp
         step_words = [sum(w[i] for w in pay_words) for i in range(K)]
         step_max = [max(w[i] for w in pay_words) for i in range(K)]
         # exchange model: every rank receives (world - 1) packed slices of B x 4 ceil(V/32)
@@ -812,8 +831,19 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
                                         "ring": slow + pack + sizes_us + ag_sp_ring + sp_cold},
                   "note": "per row the shard's BWT slice when hi - lo < ceil(V/32), else its bitmap "
                           "(fm_shard_pack); OR / scatter / unpack of the 8 payloads (fm_shard_or_rows)"}
+        # peer model: the same pack; a one-element all_reduce as the barrier (assumed 15 us at 8
+        # ranks); the OR pass reads the 7 peers' payloads over the 7 links in parallel (the largest
+        # payload / 153 GB/s on top of the pass measured here over local buffers, + 2 us per remote
+        # round trip: the header, then the data)
+        remote_us = sp_slice / 153e9 * 1e6 + 2 * 2.0
+        peer = {"masks_equal_unsharded": exact_peer, "or_rows_peers_cold_us": pp_cold,
+                "or_rows_peers_warm_us": pp_warm, "pack_cold_us_slowest_shard": pack,
+                "barrier_us_assumed": 15.0, "remote_read_model_us": remote_us,
+                "predicted_step_us": slow + pack + 15.0 + remote_us + pp_cold,
+                "note": "payloads in IPC-mapped buffers read in place (fm_shard_or_rows_peers): no sizes "
+                        "exchange, no gather; here over local buffers"}
         return {"shards": world, "halo": halo, "global_batch": B, "steps": K, "per_shard": shards,
-                "sparse_exchange": sparse,
+                "sparse_exchange": sparse, "peer_exchange": peer,
                 "slowest_shard_cold_us": slow, "or_pass_cold_us": or_cold, "or_pass_warm_us": or_warm,
                 "or_pass_bytes": world * slice_b + B * V,
                 "or_pass_GBps_cold": (world * slice_b + B * V) / (or_cold * 1e-6) / 1e9,
@@ -1380,7 +1410,10 @@ def main():
             else:
                 log(f"c4 on one GPU: slowest shard {c4['slowest_shard_cold_us']:.1f}us cold, OR "
                     f"{c4['or_pass_cold_us']:.1f}us, exact {c4['masks_equal_unsharded']}, predicted 8-GPU step "
-                    f"{c4['predicted_step_us']['direct']:.0f}-{c4['predicted_step_us']['ring']:.0f}us")
+                    f"{c4['predicted_step_us']['direct']:.0f}-{c4['predicted_step_us']['ring']:.0f}us (dense), "
+                    f"{c4['peer_exchange']['predicted_step_us']:.0f}us (peer, OR pass "
+                    f"{c4['peer_exchange']['or_rows_peers_cold_us']:.1f}us, exact "
+                    f"{c4['peer_exchange']['masks_equal_unsharded']})")
         except Exception as e:  # the replica line must still print
             result["c4_one_gpu"] = {"error": repr(e)}
     if rank == 0:
