@@ -477,8 +477,16 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
   }
 }
 
+#ifndef FMIDX_GROUP_WPE
+#define FMIDX_GROUP_WPE 0
+#endif
+#if FMIDX_GROUP_WPE > 0
+#define FMIDX_GROUP_ATTR __attribute__((amdgpu_waves_per_eu(FMIDX_GROUP_WPE, FMIDX_GROUP_WPE)))
+#else
+#define FMIDX_GROUP_ATTR
+#endif
 template <int G, bool GP, bool Q>
-__global__ void __launch_bounds__(kLfThreads) k_lf_group(DevView v, const int64_t* __restrict__ tok,
+__global__ void __launch_bounds__(kLfThreads) FMIDX_GROUP_ATTR k_lf_group(DevView v, const int64_t* __restrict__ tok,
                                                         int64_t shift, int64_t reset_below,
                                                         const uint64_t* lo_in, const uint64_t* hi_in,
                                                         uint64_t* lo_out, uint64_t* hi_out, uint64_t m) {
@@ -681,8 +689,17 @@ __device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint3
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
+// occupancy experiments (make qvariant VFLAGS=-DFMIDX_SWEEP_WPE=6): waves per SIMD forced on the sweep
+#ifndef FMIDX_SWEEP_WPE
+#define FMIDX_SWEEP_WPE 0
+#endif
+#if FMIDX_SWEEP_WPE > 0
+#define FMIDX_SWEEP_ATTR __attribute__((amdgpu_waves_per_eu(FMIDX_SWEEP_WPE, FMIDX_SWEEP_WPE)))
+#else
+#define FMIDX_SWEEP_ATTR
+#endif
 template <bool INLINE>
-__global__ void __launch_bounds__(kLfThreads) k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
+__global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
                                                         int64_t reset_below, const uint64_t* lo_in,
                                                         const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                                                         uint64_t m, LfWork* lt, uint32_t* cnt, uint64_t cap) {
