@@ -645,7 +645,10 @@ struct LfWork {
 };
 constexpr uint32_t kWorkRegions = 64;
 constexpr uint64_t kSweepScan = 64;   // widest range k_lf_sweep scans in E
-constexpr int kSweepPass = 2;   // 64-entry passes per round trip of the packed scan (2: 92 VGPRs; 4: 100)
+#ifndef FMIDX_SWEEP_PASS
+#define FMIDX_SWEEP_PASS 2
+#endif
+constexpr int kSweepPass = FMIDX_SWEEP_PASS;   // 64-entry passes per round trip of the packed scan (2: 92 VGPRs; 4: 100)
 // The 2-level descent / wide E scan, by a whole wave (uniform inputs;
 // lo < hi <= n, not the full range, sym valid).  pword = the range's cached
 // bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
