@@ -385,7 +385,7 @@ int host_distinct(fm_index* h, const uint64_t* lows, const uint64_t* highs, uint
   std::memcpy(hstage_at<uint64_t>(h, o_hi), highs, m * 8);
   std::memcpy(hstage_at<uint64_t>(h, o_cap), cap_off.data(), (m + 1) * 8);
   if (stage_up(h, 0, o_k)) return -1;
-  if (ws_acquire(h, x.stream, fmidx::distinct_ws_bytes(total, m))) return -1;
+  if (ws_acquire(h, x.stream, fmidx::distinct_ws_bytes(total))) return -1;
   if (fmidx::launch_distinct(x.view, stage_at<uint64_t>(h, o_lo), stage_at<uint64_t>(h, o_hi), m,
                              stage_at<uint64_t>(h, o_cap), d_syms, d_cnt, stage_at<uint64_t>(h, o_k), x.ws, total,
                              x.stream))
@@ -1046,7 +1046,7 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (ws_acquire(h, s, fmidx::distinct_ws_bytes(total_cap, m))) return -1;
+  if (ws_acquire(h, s, fmidx::distinct_ws_bytes(total_cap))) return -1;
   if (fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k, h->idx.ws, total_cap, s))
     return -1;
   return ws_release(h, s);

@@ -143,7 +143,7 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   DBuf<uint8_t> d_ws;
   if (d_lo.alloc(kChunkRows) || d_hi.alloc(kChunkRows) || d_off.alloc(kChunkRows + 1) || d_syms.alloc(kChunkCap) ||
       d_cnt.alloc(kChunkCap) || d_child.alloc(kChunkCap) || d_k.alloc(kChunkRows) ||
-      d_ws.alloc(distinct_ws_bytes(kChunkCap, kChunkRows)))
+      d_ws.alloc(distinct_ws_bytes(kChunkCap)))
     return -1;
   std::vector<uint64_t> lo, hi, off, k;
   lo.reserve(kChunkRows);
@@ -278,7 +278,7 @@ int device_build_cache(Index* h, hipStream_t s) {
       DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_child, d_k;
       DBuf<uint8_t> d_ws;
       if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(total) || d_cnt.alloc(total) ||
-          d_child.alloc(total) || d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(total, m)))
+          d_child.alloc(total) || d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(total)))
         return -1;
       FM_HIP(hipMemcpyAsync(d_lo.p, lo.data(), m * 8, hipMemcpyHostToDevice, s));
       FM_HIP(hipMemcpyAsync(d_hi.p, hi.data(), m * 8, hipMemcpyHostToDevice, s));
@@ -345,7 +345,7 @@ int device_build_cache(Index* h, hipStream_t s) {
       DBuf<uint64_t> d_lo, d_hi, d_off, d_syms, d_cnt, d_k;
       DBuf<uint8_t> d_ws;
       if (d_lo.alloc(m) || d_hi.alloc(m) || d_off.alloc(m + 1) || d_syms.alloc(total) || d_cnt.alloc(total) ||
-          d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(total, m)))
+          d_k.alloc(m) || d_ws.alloc(distinct_ws_bytes(total)))
         return -1;
       FM_HIP(hipMemcpyAsync(d_lo.p, lo.data(), m * 8, hipMemcpyHostToDevice, s));
       FM_HIP(hipMemcpyAsync(d_hi.p, hi.data(), m * 8, hipMemcpyHostToDevice, s));

@@ -726,7 +726,7 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
                     void* ws, uint64_t total_cap, hipStream_t s, uint64_t min_count = 1,
                     uint64_t* child_lo = nullptr);
-size_t distinct_ws_bytes(uint64_t total_cap, uint64_t m);
+size_t distinct_ws_bytes(uint64_t total_cap);
 // dense CSR (off[m + 1], interleaved (symbol, count) pairs) of launch_distinct's output
 int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64_t* syms, const uint64_t* counts,
                         uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s);

@@ -984,15 +984,84 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[
   return base + x - v;
 }
 
-// Levels lev0 .. NL - 1 of the BFS over a frontier of fc nodes in (alo, ahi, apre): on
-// return the final frontier is in (alo, ahi, apre) (the pointers are swapped level by
-// level) and its node count is returned -- ~0 when a level outgrows cap.  Every thread
-// of the workgroup calls it (block scans inside).
-__device__ uint64_t distinct_levels(const DevView& v, uint32_t lev0, uint64_t fc, uint64_t cap, uint64_t min_count,
-                                    uint64_t*& alo, uint64_t*& ahi, uint32_t*& apre, uint64_t*& blo, uint64_t*& bhi,
-                                    uint32_t*& bpre, uint32_t* wave_tot) {
+// interval_symbols with counts: level-synchronous BFS over the 16-ary
+// wavelet matrix, one workgroup per row; children are appended in digit
+// order so the final frontier is in ascending symbol order.  Each frontier
+// node is expanded by 4 lanes, lane j ranking digits 4j..4j+3 at both
+// endpoints (the 4 lanes read the same two rank blocks: one coalesced
+// request), 64 nodes per workgroup round; a thread holds 8 ranks instead of
+// all 32 (no register spills), and a block-wide scan of the per-lane child
+// counts in (node, digit) order gives every child its output slot.
+// min_count > 1 prunes every prefix node holding fewer occurrences (so only
+// symbols occurring >= min_count times are reported, in O(width / min_count)
+// space); child_lo, when given, receives LF(lo, c) = C[c] + rank_c(lo) of
+// every reported symbol (the child range is [child_lo, child_lo + count)).
+__global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __restrict__ lo_a,
+                                                 const uint64_t* __restrict__ hi_a, uint64_t m,
+                                                 const uint64_t* __restrict__ cap_off,
+                                                 uint64_t* __restrict__ syms,
+                                                 uint64_t* __restrict__ counts,
+                                                 uint64_t* __restrict__ k_out, Frontier fr,
+                                                 uint64_t min_count, uint64_t* __restrict__ child_lo,
+                                                 bool cached_path) {
+  __shared__ uint32_t wave_tot[4];
+  const uint64_t row = blockIdx.x;
+  if (row >= m) return;
+  uint64_t lo = lo_a[row], hi = hi_a[row];
+  const uint64_t base = cap_off[row];
+  const uint64_t cap = cap_off[row + 1] - base;
+  // fm_index.cpp:127-133
+  bool empty = (lo == hi);
+  if (hi > v.n) hi = v.n;
+  if (lo >= hi) empty = true;
+  if (empty || cap == 0) {
+    if (threadIdx.x == 0) k_out[row] = empty ? 0 : ~0ull;
+    return;
+  }
+  if (cached_path && ((lo == 0 && hi == v.n) ? v.bm_full != nullptr : cache_find(v, lo, hi) != nullptr))
+    return;   // k_distinct_cached's row
+  if (lo == 0 && hi == v.n) {
+    // The full range: its symbols and counts are the C array itself (symbol c
+    // occurs C[c+1] - C[c] times, its child range starts at C[c]) -- one pass
+    // over sigma instead of a BFS whose last level holds every symbol.  Each
+    // thread takes a contiguous run of symbols; a block scan orders the output.
+    const uint64_t sigma = (uint64_t)v.max_sym + 1;
+    const uint64_t per = (sigma + 255) / 256;
+    const uint64_t c0 = min<uint64_t>(sigma, threadIdx.x * per), c1 = min<uint64_t>(sigma, c0 + per);
+    uint32_t mine = 0;
+    for (uint64_t c = c0; c < c1; ++c) mine += (v.C[c + 1] - v.C[c] >= min_count) ? 1u : 0u;
+    uint32_t tot;
+    uint64_t pos = block_scan_u32(mine, wave_tot, tot);
+    if (tot <= cap) {
+      for (uint64_t c = c0; c < c1; ++c) {
+        const uint64_t a = v.C[c], b = v.C[c + 1];
+        if (b - a >= min_count) {
+          syms[base + pos] = c;
+          counts[base + pos] = b - a;
+          if (child_lo) child_lo[base + pos] = a;
+          ++pos;
+        }
+      }
+    }
+    if (threadIdx.x == 0) k_out[row] = tot <= cap ? tot : ~0ull;
+    return;
+  }
+  uint64_t* alo = fr.lo[0] + base;
+  uint64_t* ahi = fr.hi[0] + base;
+  uint32_t* apre = fr.pre[0] + base;
+  uint64_t* blo = fr.lo[1] + base;
+  uint64_t* bhi = fr.hi[1] + base;
+  uint32_t* bpre = fr.pre[1] + base;
+  if (threadIdx.x == 0) {
+    alo[0] = lo;
+    ahi[0] = hi;
+    apre[0] = 0;
+  }
+  __syncthreads();
+  uint64_t fc = 1;
+  bool overflow = false;
   const uint32_t d0 = 4 * (threadIdx.x & 3u);   // this lane's digits d0 .. d0 + 3
-  for (uint32_t lev = lev0; lev < v.NL; ++lev) {
+  for (uint32_t lev = 0; lev < v.NL; ++lev) {
     uint64_t zd[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) zd[j] = v.Z[lev * kRadix + d0 + j];
@@ -1049,7 +1118,10 @@ __device__ uint64_t distinct_levels(const DevView& v, uint32_t lev0, uint64_t fc
       out += tot;
     }
     __syncthreads();
-    if (out > cap) return ~0ull;
+    if (out > cap) {
+      overflow = true;
+      break;
+    }
     fc = out;
     uint64_t* t;
     uint32_t* tp;
@@ -1057,96 +1129,7 @@ __device__ uint64_t distinct_levels(const DevView& v, uint32_t lev0, uint64_t fc
     t = ahi; ahi = bhi; bhi = t;
     tp = apre; apre = bpre; bpre = tp;
   }
-  return fc;
-}
-
-// A row the split BFS takes (k_distinct_split / k_distinct_join; k_distinct leaves it):
-// an uncached range of at least split_min rows (not the full range).  Its 16 top-level
-// digit subtrees are expanded by 16 workgroups at once instead of one.
-__device__ __forceinline__ bool distinct_split_row(const DevView& v, uint64_t lo, uint64_t hi, uint64_t cap,
-                                                   bool cached_path, uint64_t split_min) {
-  if (hi > v.n) hi = v.n;
-  if (lo >= hi || cap == 0 || hi - lo < split_min || (lo == 0 && hi == v.n) || v.NL < 2) return false;
-  return !(cached_path && cache_find(v, lo, hi) != nullptr);
-}
-
-// interval_symbols with counts: level-synchronous BFS over the 16-ary
-// wavelet matrix, one workgroup per row; children are appended in digit
-// order so the final frontier is in ascending symbol order.  Each frontier
-// node is expanded by 4 lanes, lane j ranking digits 4j..4j+3 at both
-// endpoints (the 4 lanes read the same two rank blocks: one coalesced
-// request), 64 nodes per workgroup round; a thread holds 8 ranks instead of
-// all 32 (no register spills), and a block-wide scan of the per-lane child
-// counts in (node, digit) order gives every child its output slot.
-// min_count > 1 prunes every prefix node holding fewer occurrences (so only
-// symbols occurring >= min_count times are reported, in O(width / min_count)
-// space); child_lo, when given, receives LF(lo, c) = C[c] + rank_c(lo) of
-// every reported symbol (the child range is [child_lo, child_lo + count)).
-__global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __restrict__ lo_a,
-                                                 const uint64_t* __restrict__ hi_a, uint64_t m,
-                                                 const uint64_t* __restrict__ cap_off,
-                                                 uint64_t* __restrict__ syms,
-                                                 uint64_t* __restrict__ counts,
-                                                 uint64_t* __restrict__ k_out, Frontier fr,
-                                                 uint64_t min_count, uint64_t* __restrict__ child_lo,
-                                                 bool cached_path, uint64_t split_min) {
-  __shared__ uint32_t wave_tot[4];
-  const uint64_t row = blockIdx.x;
-  if (row >= m) return;
-  uint64_t lo = lo_a[row], hi = hi_a[row];
-  const uint64_t base = cap_off[row];
-  const uint64_t cap = cap_off[row + 1] - base;
-  // fm_index.cpp:127-133
-  bool empty = (lo == hi);
-  if (hi > v.n) hi = v.n;
-  if (lo >= hi) empty = true;
-  if (empty || cap == 0) {
-    if (threadIdx.x == 0) k_out[row] = empty ? 0 : ~0ull;
-    return;
-  }
-  if (cached_path && ((lo == 0 && hi == v.n) ? v.bm_full != nullptr : cache_find(v, lo, hi) != nullptr))
-    return;   // k_distinct_cached's row
-  if (distinct_split_row(v, lo, hi, cap, cached_path, split_min)) return;   // k_distinct_split's row
-  if (lo == 0 && hi == v.n) {
-    // The full range: its symbols and counts are the C array itself (symbol c
-    // occurs C[c+1] - C[c] times, its child range starts at C[c]) -- one pass
-    // over sigma instead of a BFS whose last level holds every symbol.  Each
-    // thread takes a contiguous run of symbols; a block scan orders the output.
-    const uint64_t sigma = (uint64_t)v.max_sym + 1;
-    const uint64_t per = (sigma + 255) / 256;
-    const uint64_t c0 = min<uint64_t>(sigma, threadIdx.x * per), c1 = min<uint64_t>(sigma, c0 + per);
-    uint32_t mine = 0;
-    for (uint64_t c = c0; c < c1; ++c) mine += (v.C[c + 1] - v.C[c] >= min_count) ? 1u : 0u;
-    uint32_t tot;
-    uint64_t pos = block_scan_u32(mine, wave_tot, tot);
-    if (tot <= cap) {
-      for (uint64_t c = c0; c < c1; ++c) {
-        const uint64_t a = v.C[c], b = v.C[c + 1];
-        if (b - a >= min_count) {
-          syms[base + pos] = c;
-          counts[base + pos] = b - a;
-          if (child_lo) child_lo[base + pos] = a;
-          ++pos;
-        }
-      }
-    }
-    if (threadIdx.x == 0) k_out[row] = tot <= cap ? tot : ~0ull;
-    return;
-  }
-  uint64_t* alo = fr.lo[0] + base;
-  uint64_t* ahi = fr.hi[0] + base;
-  uint32_t* apre = fr.pre[0] + base;
-  uint64_t* blo = fr.lo[1] + base;
-  uint64_t* bhi = fr.hi[1] + base;
-  uint32_t* bpre = fr.pre[1] + base;
-  if (threadIdx.x == 0) {
-    alo[0] = lo;
-    ahi[0] = hi;
-    apre[0] = 0;
-  }
-  __syncthreads();
-  const uint64_t fc = distinct_levels(v, 0, 1, cap, min_count, alo, ahi, apre, blo, bhi, bpre, wave_tot);
-  if (fc == ~0ull) {
+  if (overflow) {
     if (threadIdx.x == 0) k_out[row] = ~0ull;
     return;
   }
@@ -1156,156 +1139,6 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
   }
   if (threadIdx.x == 0) k_out[row] = fc;
-}
-
-// A wide uncached row split over its 16 top-level digits: workgroup (row, d) ranks both
-// ends at level 0 (all 16 digits, one coalesced block each), derives every subtree's
-// capacity -- min(occurrences with digit d [/ min_count], symbols with top digit d), which
-// sum to at most the row's capacity -- and runs the BFS of subtree d from level 1 in its
-// own slice [off_d, off_d + cap_d) of the row's frontier and output; k_distinct_join then
-// closes the gaps.  When the capacities do not fit the row's (a caller-given smaller
-// cap), workgroup 0 runs the whole row's BFS alone, as k_distinct would.
-// sub[row][d] = {k_d, off_d}; sub[row][0].off = ~0: not split (k_out already written).
-__global__ void __launch_bounds__(256) k_distinct_split(DevView v, const uint64_t* __restrict__ lo_a,
-                                                       const uint64_t* __restrict__ hi_a, uint64_t m,
-                                                       const uint64_t* __restrict__ cap_off,
-                                                       uint64_t* __restrict__ syms, uint64_t* __restrict__ counts,
-                                                       uint64_t* __restrict__ k_out, Frontier fr, uint64_t min_count,
-                                                       uint64_t* __restrict__ child_lo, bool cached_path,
-                                                       uint64_t split_min, uint64_t* __restrict__ sub) {
-  __shared__ uint32_t wave_tot[4];
-  __shared__ uint64_t s_r[2][kRadix];
-  const uint64_t row = blockIdx.x / kRadix;
-  const uint32_t d = blockIdx.x % kRadix;
-  if (row >= m) return;
-  uint64_t lo = lo_a[row], hi = hi_a[row];
-  const uint64_t base = cap_off[row];
-  const uint64_t cap = cap_off[row + 1] - base;
-  if (!distinct_split_row(v, lo, hi, cap, cached_path, split_min)) return;
-  if (hi > v.n) hi = v.n;
-  if (threadIdx.x < 2 * kRadix) {
-    const uint32_t dd = threadIdx.x % kRadix;
-    s_r[threadIdx.x / kRadix][dd] = rank16(v, 0, threadIdx.x < kRadix ? lo : hi, dd);
-  }
-  __syncthreads();
-  const uint64_t span = 1ull << (4 * (v.NL - 1));   // symbols per top digit
-  const uint64_t sigma = (uint64_t)v.max_sym + 1;
-  uint64_t off = 0, total = 0, capd = 0;
-  for (uint32_t e = 0; e < (uint32_t)kRadix; ++e) {
-    const uint64_t cw = s_r[1][e] - s_r[0][e];
-    const uint64_t se = (uint64_t)e * span >= sigma ? 0 : min(span, sigma - (uint64_t)e * span);
-    const uint64_t ce = min(min_count > 1 ? cw / min_count : cw, se);
-    if (e < d) off += ce;
-    if (e == d) capd = ce;
-    total += ce;
-  }
-  uint64_t* alo = fr.lo[0] + base;
-  uint64_t* ahi = fr.hi[0] + base;
-  uint32_t* apre = fr.pre[0] + base;
-  uint64_t* blo = fr.lo[1] + base;
-  uint64_t* bhi = fr.hi[1] + base;
-  uint32_t* bpre = fr.pre[1] + base;
-  uint64_t* sr = sub + (row * kRadix + d) * 2;
-  if (total > cap) {
-    // the whole row by workgroup 0 (k_distinct's BFS)
-    if (d != 0) return;
-    if (threadIdx.x == 0) {
-      alo[0] = lo;
-      ahi[0] = hi;
-      apre[0] = 0;
-    }
-    __syncthreads();
-    const uint64_t fc = distinct_levels(v, 0, 1, cap, min_count, alo, ahi, apre, blo, bhi, bpre, wave_tot);
-    if (fc != ~0ull) {
-      for (uint64_t i = threadIdx.x; i < fc; i += 256) {
-        syms[base + i] = apre[i];
-        counts[base + i] = ahi[i] - alo[i];
-        if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
-      }
-    }
-    if (threadIdx.x == 0) {
-      k_out[row] = fc;
-      sr[1] = ~0ull;
-    }
-    return;
-  }
-  const uint64_t cl = s_r[0][d], ch = s_r[1][d];
-  uint64_t fc = 0;
-  if (ch >= cl + min_count && capd) {
-    alo += off;
-    ahi += off;
-    apre += off;
-    blo += off;
-    bhi += off;
-    bpre += off;
-    const uint64_t z = v.Z[d];
-    if (threadIdx.x == 0) {
-      alo[0] = z + cl;
-      ahi[0] = z + ch;
-      apre[0] = d;
-    }
-    __syncthreads();
-    fc = distinct_levels(v, 1, 1, capd, min_count, alo, ahi, apre, blo, bhi, bpre, wave_tot);
-    if (fc != ~0ull) {
-      for (uint64_t i = threadIdx.x; i < fc; i += 256) {
-        syms[base + off + i] = apre[i];
-        counts[base + off + i] = ahi[i] - alo[i];
-        if (child_lo) child_lo[base + off + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
-      }
-    }
-  }
-  if (threadIdx.x == 0) {
-    sr[0] = fc;
-    sr[1] = off;
-  }
-}
-
-// Closes the gaps between a split row's 16 subtree outputs (in digit order, so the
-// symbols stay ascending): each slice moves left by whole 256-entry chunks, every
-// chunk read before any of it is written (a destination never lies past its source).
-__global__ void __launch_bounds__(256) k_distinct_join(DevView v, const uint64_t* __restrict__ lo_a,
-                                                      const uint64_t* __restrict__ hi_a, uint64_t m,
-                                                      const uint64_t* __restrict__ cap_off,
-                                                      uint64_t* __restrict__ syms, uint64_t* __restrict__ counts,
-                                                      uint64_t* __restrict__ k_out, uint64_t* __restrict__ child_lo,
-                                                      bool cached_path, uint64_t split_min,
-                                                      const uint64_t* __restrict__ sub) {
-  const uint64_t row = blockIdx.x;
-  if (row >= m) return;
-  const uint64_t base = cap_off[row];
-  const uint64_t cap = cap_off[row + 1] - base;
-  if (!distinct_split_row(v, lo_a[row], hi_a[row], cap, cached_path, split_min)) return;
-  const uint64_t* sr = sub + row * kRadix * 2;
-  if (sr[1] == ~0ull) return;   // not split: k_distinct_split's workgroup 0 wrote the row
-  uint64_t pos = 0;
-  bool bad = false;
-  for (uint32_t e = 0; e < (uint32_t)kRadix; ++e) {
-    const uint64_t k = sr[2 * e], off = sr[2 * e + 1];
-    if (k == ~0ull) {
-      bad = true;
-      break;
-    }
-    if (off != pos) {
-      for (uint64_t c0 = 0; c0 < k; c0 += 256) {
-        const uint64_t i = c0 + threadIdx.x;
-        uint64_t a = 0, b = 0, c = 0;
-        if (i < k) {
-          a = syms[base + off + i];
-          b = counts[base + off + i];
-          if (child_lo) c = child_lo[base + off + i];
-        }
-        __syncthreads();
-        if (i < k) {
-          syms[base + pos + i] = a;
-          counts[base + pos + i] = b;
-          if (child_lo) child_lo[base + pos + i] = c;
-        }
-        __syncthreads();
-      }
-    }
-    pos += k;
-  }
-  if (threadIdx.x == 0) k_out[row] = bad ? ~0ull : pos;
 }
 
 // interval_symbols of a cached range or the full range (k_distinct leaves these rows to it):
@@ -1691,11 +1524,7 @@ int launch_raw_multi(const DevView& v, const uint64_t* q, uint64_t len, uint64_t
   return 0;
 }
 
-// the BFS frontiers (two buffers of (lo, hi, prefix) per capacity slot), then the split
-// rows' per-subtree {count, offset} pairs
-size_t distinct_ws_bytes(uint64_t total_cap, uint64_t m) {
-  return (size_t)total_cap * 40 + (size_t)m * kRadix * 16 + 256;
-}
+size_t distinct_ws_bytes(uint64_t total_cap) { return (size_t)total_cap * 40 + 256; }
 
 int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m,
                     const uint64_t* cap_off, uint64_t* syms, uint64_t* counts, uint64_t* k,
@@ -1712,21 +1541,9 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
   fr.pre[1] = fr.pre[0] + T;
   const bool cached_path = v.trans_cap && v.cache_mask && (min_count ? min_count : 1) == 1 &&
                            env_u32("FMIDX_DISTINCT_CACHED", 1) != 0;
-  // rows of >= FMIDX_DISTINCT_SPLIT_MIN occurrences outside the cache: 16 workgroups each
-  const uint64_t split_min = std::max<uint32_t>(1u, env_u32("FMIDX_DISTINCT_SPLIT_MIN", 1u << 15));
-  uint64_t* sub = reinterpret_cast<uint64_t*>(fr.pre[1] + T);
-  sub = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(sub) + 7) & ~uintptr_t(7));
-  const uint64_t mc = min_count ? min_count : 1;
-  k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr, mc, child_lo, cached_path,
-                                         split_min);
+  k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr,
+                                         min_count ? min_count : 1, child_lo, cached_path);
   FM_HIP(hipGetLastError());
-  if (m * kRadix < (1ull << 31)) {
-    k_distinct_split<<<(unsigned)(m * kRadix), 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr, mc, child_lo,
-                                                            cached_path, split_min, sub);
-    k_distinct_join<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, child_lo, cached_path,
-                                                split_min, sub);
-    FM_HIP(hipGetLastError());
-  }
   if (cached_path) {
     const uint32_t chunks = (v.bm_words + kDcWords - 1) / kDcWords;
     k_distinct_cached<<<(unsigned)(m * chunks), 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, child_lo,

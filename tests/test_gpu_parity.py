@@ -910,71 +910,3 @@ def test_device_structs(dev):
         assert p and b > 0
     with pytest.raises(Exception):
         ours.device_struct(9)
-
-
-@pytest.mark.parametrize("cached", [False, True])
-def test_distinct_split_rows(dev, monkeypatch, cached):
-    """Uncached wide rows split over their 16 top-level digit subtrees
-    (k_distinct_split + k_distinct_join; FMIDX_DISTINCT_SPLIT_MIN, read at every
-    launch, lowered so that most rows split): symbols ascending and counts equal
-    to the oracle's for arbitrary ranges of every width, the full range and
-    cached ranges beside them, capacity overflow (a too-small cap falls back to
-    one workgroup and reports k = UINT64_MAX); and an index whose construction
-    ran its min_count BFS (range cache, transition table) through the split
-    kernels equals one built without them."""
-    import torch
-
-    docs = markov_docs(5, 400, 3000, 200)
-    kw = dict(bm_log2=5, cache_min=8) if cached else dict(cache_min=1 << 40, trans=0)
-    ora = OracleIndex()
-    ora.initialize(docs, in_memory=True)
-    n = ora.size()
-    monkeypatch.setenv("FMIDX_DISTINCT_SPLIT_MIN", "2")
-    ours = ours_index(docs, **kw)
-    monkeypatch.delenv("FMIDX_DISTINCT_SPLIT_MIN")
-    ref = ours_index(docs, **kw)
-    so, sr = ours.stats(), ref.stats()
-    assert so["cache_nodes"] == sr["cache_nodes"]
-    # which keys a full probe run leaves out depends on the parallel insert's timing; the
-    # children the min_count BFS found (inserted + left out) may not
-    assert so["trans_entries"] + so["trans_dropped"] == sr["trans_entries"] + sr["trans_dropped"]
-    rng = np.random.default_rng(9)
-    rows = [(0, n), (1, n), (0, n - 1), (5, 5), (7, 3)]
-    for w in (1, 2, 3, 15, 16, 17, 100, 1000, 5000, 20000, n // 2):
-        for _ in range(3):
-            a = int(rng.integers(0, max(1, n - w)))
-            rows.append((a, min(n, a + w)))
-    F = [t for d in reversed(docs) for t in d]
-    rows += [ora.get_range(F[s:s + 1]) for s in range(0, 300, 37)]
-    lo = torch.tensor([r[0] for r in rows], dtype=torch.int64, device=dev)
-    hi = torch.tensor([r[1] for r in rows], dtype=torch.int64, device=dev)
-    monkeypatch.setenv("FMIDX_DISTINCT_SPLIT_MIN", "2")
-    syms, counts, k, cap_off = [x.cpu().numpy() for x in ours.distinct_count_batch(lo, hi)]
-    for i, (a, b) in enumerate(rows):
-        s0 = int(cap_off[i])
-        got = []
-        for j in range(int(k[i])):
-            got += [int(syms[s0 + j]), int(counts[s0 + j])]
-        assert tuple(got) == ora.distinct_count(a, b), (i, a, b)
-    assert ours.distinct_count_multi([r[0] for r in rows], [r[1] for r in rows]) == \
-        ora.distinct_count_multi([r[0] for r in rows], [r[1] for r in rows])
-    # a capacity below the subtrees' sum: one workgroup, overflow reported
-    wide = [r for r in rows if r[1] - r[0] >= 1000][:3]
-    ks = [len(ora.distinct_count(a, b)) // 2 for a, b in wide]
-    lo = torch.tensor([r[0] for r in wide], dtype=torch.int64, device=dev)
-    hi = torch.tensor([r[1] for r in wide], dtype=torch.int64, device=dev)
-    cap = torch.tensor([ks[0] - 1, ks[1], ks[2] + 1], dtype=torch.int64, device=dev)
-    syms, counts, k, cap_off = [x.cpu().numpy() for x in ours.distinct_count_batch(lo, hi, cap=cap)]
-    assert int(k[0]) == -1
-    for i in (1, 2):
-        a, b = wide[i]
-        s0 = int(cap_off[i])
-        got = []
-        for j in range(int(k[i])):
-            got += [int(syms[s0 + j]), int(counts[s0 + j])]
-        assert tuple(got) == ora.distinct_count(a, b), i
-    # the decode path over the split-built index
-    V = 3000
-    lo_t = torch.tensor([r[0] for r in rows], dtype=torch.int64, device=dev)
-    hi_t = torch.tensor([r[1] for r in rows], dtype=torch.int64, device=dev)
-    assert torch.equal(ours.allowed_mask(lo_t, hi_t, V, 10), ref.allowed_mask(lo_t, hi_t, V, 10))
