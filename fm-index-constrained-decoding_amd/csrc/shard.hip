@@ -342,6 +342,26 @@ __device__ __forceinline__ uint32_t part_word(const uint32_t* base, uint64_t i) 
   else return *p;
 }
 
+typedef const __attribute__((address_space(1))) or_v4u g128_t;
+typedef const __attribute__((address_space(1))) uint64_t g64_t;
+
+// four consecutive words at a 16-B aligned address (PEERS: two system-scope 8-B loads)
+template <bool PEERS>
+__device__ __forceinline__ uint4 part_quad(const uint32_t* base, uint64_t i) {
+  if constexpr (PEERS) {
+    g64_t* p = (g64_t*)(base + i);
+    const uint64_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+  } else {
+    const or_v4u v = *(g128_t*)(base + i);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
+constexpr int kOrSym0 = 4;   // 16-B symbol loads per thread issued with the dense words (16 K symbols)
+constexpr int kOrSymU = 8;   // per later round (32 K symbols)
+
 template <bool PEERS>
 __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts,
                                                             const uint64_t* __restrict__ ptrs, uint32_t nparts,
@@ -349,7 +369,9 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
                                                             int unpack) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
-  __shared__ uint32_t s_desc[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
+  // per part: its sparse count (0 for dense parts), data offset, and first 16-B slot in the
+  // flat space of every sparse list padded to a multiple of 4 words
+  __shared__ uint32_t s_cnt[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
   __shared__ uint64_t s_base[PEERS ? kOrMaxParts : 1];
   __shared__ uint32_t s_nd;
   const uint64_t b = blockIdx.x;
@@ -360,42 +382,70 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   };
   const uint32_t W4 = (W + 3) / 4;
   for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
-  if (t < nparts) {
-    // a row whose data lies past the part's end (a gather shorter than the payload: the
-    // speculative all_gather of SparseExchange, redone in full when it was too short) is read as
-    // empty -- never beyond the part
-    const uint32_t* pp = PEERS ? reinterpret_cast<const uint32_t*>(ptrs[t]) : parts + (uint64_t)t * stride;
-    const uint32_t d = part_word<PEERS>(pp, 4 + b), o = part_word<PEERS>(pp, 4 + B + b);
-    const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
-    const bool inside = o >= 4 + 2 * B && end <= stride;
-    s_desc[t] = inside ? d : 0u;
-    s_off[t] = inside ? o : 0u;
-    if constexpr (PEERS) s_base[t] = reinterpret_cast<uint64_t>(pp);
-  }
-  or_lds_barrier();
-  if (t == 0) {
-    uint32_t nd = 0, run = 0;
-    for (uint32_t p = 0; p < nparts; ++p) {
-      s_pre[p] = run;
-      if (s_desc[p] >> 31) s_dense[nd++] = p;
-      else run += s_desc[p];
+  if (t < 64) {
+    // wave 0 stages every part's (desc, off) and scans them in registers (nparts <= 64).  A row
+    // whose data lies past the part's end (a gather shorter than the payload: the speculative
+    // all_gather of SparseExchange, redone in full when it was too short) is read as empty --
+    // never beyond the part
+    uint32_t d = 0, o = 0;
+    const uint32_t* pp = nullptr;
+    if (t < nparts) {
+      pp = PEERS ? reinterpret_cast<const uint32_t*>(ptrs[t]) : parts + (uint64_t)t * stride;
+      d = part_word<PEERS>(pp, 4 + b);
+      o = part_word<PEERS>(pp, 4 + B + b);
+      const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
+      if (!(o >= 4 + 2 * B && end <= stride)) d = o = 0;
     }
-    s_pre[nparts] = run;
-    s_nd = nd;
+    const bool dense = (d >> 31) != 0;
+    const uint32_t q = dense ? 0u : (d + 3u) >> 2;
+    uint32_t inc = q;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const uint32_t y = __shfl_up(inc, k, 64);
+      if (t >= (uint32_t)k) inc += y;
+    }
+    const uint64_t dm = __ballot(dense);
+    if (t < nparts) {
+      s_cnt[t] = dense ? 0u : d;
+      s_off[t] = o;
+      s_pre[t] = inc - q;
+      if (dense) s_dense[__popcll(dm & ((1ull << t) - 1))] = t;
+      if constexpr (PEERS) s_base[t] = reinterpret_cast<uint64_t>(pp);
+    }
+    const uint32_t tot = __shfl(inc, (int)(nparts - 1), 64);
+    if (t == 0) {
+      s_pre[nparts] = tot;
+      s_nd = (uint32_t)__popcll(dm);
+    }
   }
   or_lds_barrier();
   const uint32_t nd = s_nd;
-  const uint32_t total = s_pre[nparts];
-  auto sym_at = [&](uint32_t i) -> uint32_t {
-    uint32_t p = 0;                                     // the part whose list holds flat index i
+  const uint32_t total4 = s_pre[nparts];   // 16-B slots of sparse symbols
+  // the 16-B slot j of the flat space: its part and its four symbols
+  auto quad_at = [&](uint32_t j, uint32_t& p) -> uint4 {
+    p = 0;                                              // the last part whose first slot is <= j
     for (uint32_t step = kOrMaxParts / 2; step; step >>= 1)
-      if (p + step <= nparts - 1 && s_pre[p + step] <= i) p += step;
-    return part_word<PEERS>(base_of(p), s_off[p] + (i - s_pre[p]));
+      if (p + step <= nparts - 1 && s_pre[p + step] <= j) p += step;
+    return part_quad<PEERS>(base_of(p), s_off[p] + 4ull * (j - s_pre[p]));
   };
-  // the first 4096 sparse symbols, loaded with the first dense round
-  uint32_t sym0[4];
+  auto set_quad = [&](uint32_t j, uint32_t p, const uint4& x) {
+    const uint32_t k0 = 4 * (j - s_pre[p]), cnt = s_cnt[p];
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-  for (int u = 0; u < 4; ++u) sym0[u] = total ? sym_at(min(u * kOrRowThreads + t, total - 1)) : 0u;
+    for (int e = 0; e < 4; ++e) {
+      const int64_t tok = (int64_t)xs[e] - shift;
+      if (j < total4 && k0 + e < cnt && tok >= 0 && (uint64_t)tok < vocab)
+        atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+    }
+  };
+  // the first 16 K sparse symbols, loaded with the first dense round
+  uint4 sq0[kOrSym0];
+  uint32_t sp0[kOrSym0];
+#pragma unroll
+  for (int u = 0; u < kOrSym0; ++u) {
+    sp0[u] = 0;
+    sq0[u] = total4 ? quad_at(min(u * kOrRowThreads + t, total4 - 1), sp0[u]) : make_uint4(0, 0, 0, 0);
+  }
   constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);   // W <= 8192 words
   const uint32_t slots = (W4 + kOrRowThreads - 1) / kOrRowThreads;
   uint4 acc[kSlots4];
@@ -449,21 +499,14 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   // share a symbol's word)
   or_lds_barrier();
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int64_t tok = (int64_t)sym0[u] - shift;
-    if (u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
-      atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
-  }
-  for (uint32_t i0 = 4 * kOrRowThreads; i0 < total; i0 += 8 * kOrRowThreads) {   // long lists: 8 per round
-    uint32_t sym[8];
+  for (int u = 0; u < kOrSym0; ++u) set_quad(u * kOrRowThreads + t, sp0[u], sq0[u]);
+  for (uint32_t j0 = kOrSym0 * kOrRowThreads; j0 < total4; j0 += kOrSymU * kOrRowThreads) {   // long lists
+    uint4 sq[kOrSymU];
+    uint32_t sp[kOrSymU];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) sym[u] = sym_at(min(i0 + u * kOrRowThreads + t, total - 1));
+    for (int u = 0; u < kOrSymU; ++u) sq[u] = quad_at(min(j0 + u * kOrRowThreads + t, total4 - 1), sp[u]);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t tok = (int64_t)sym[u] - shift;
-      if (i0 + u * kOrRowThreads + t < total && tok >= 0 && (uint64_t)tok < vocab)
-        atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
-    }
+    for (int u = 0; u < kOrSymU; ++u) set_quad(j0 + u * kOrRowThreads + t, sp[u], sq[u]);
   }
   or_lds_barrier();
   if (!unpack) {
