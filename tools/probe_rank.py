@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--patterns", type=int, default=1 << 18)
     ap.add_argument("--out", default="")
     ap.add_argument("--by-path", action="store_true", help="also one launch per LF path class (PMC breakdown)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="also each launch with its pairs ordered by lo (locality experiment, sort untimed)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     fm, text, bwt, _ = bench.build_index(int(args.tokens), args.vocab, 20250905, dev)
@@ -121,6 +123,18 @@ def main():
               f"{e['Msteps_per_s_cold']:7.0f} M steps/s, {e['frac_gather_bwt_cold']:.3f} of gather), warm "
               f"{warm * 1e3:8.1f} us ({e['GBps_warm']:6.0f} GB/s); {by.sum() / m:.0f} B/row, exact {ok}",
               flush=True)
+        if args.sorted:
+            order = torch.argsort(plo)
+            st_, sl_, sh_ = tok[order].contiguous(), plo[order].contiguous(), phi[order].contiguous()
+            fs = lambda: fm.lf_step_batch(st_, sl_, sh_, SHIFT, lo_out=olo, hi_out=ohi, reset_below=0)  # noqa: E731
+            fs()
+            torch.cuda.synchronize()
+            e["sorted_exact"] = bool(torch.equal(olo, lo_h[1:S].reshape(-1)[order]) and
+                                     torch.equal(ohi, hi_h[1:S].reshape(-1)[order]))
+            e["sorted_cold_us"] = timed(fs, True) * 1e3
+            e["sorted_warm_us"] = timed(fs, False) * 1e3
+            print(f"   sorted by lo: cold {e['sorted_cold_us']:.1f} us, warm {e['sorted_warm_us']:.1f} us, "
+                  f"exact {e['sorted_exact']}", flush=True)
         del tokens, lo_h, hi_h, tok, plo, phi, olo, ohi
         torch.cuda.empty_cache()
 
