@@ -7,7 +7,7 @@ Both are timed as the bench times its OR pass: K launches in one graph, each
 over its own copy of the gathered data, after a 1 GiB eviction (cold) and
 back to back (warm).  The outputs must agree.
 
-    FMIDX_OR_ROWS_EARLY=0|1 python tools/bench_or_rows.py
+    python tools/bench_or_rows.py [--wide 0.15]
 """
 from __future__ import annotations
 
@@ -110,7 +110,7 @@ def main():
 
     r_s = timed(lambda x: or_payloads(x, B, V, SH, out=out_s), sp_t)
     r_d = timed(lambda x: or_bits(x, V, out=out_d), dn_t)
-    print(json.dumps({"early": os.environ.get("FMIDX_OR_ROWS_EARLY", "0"), "exact": exact,
+    print(json.dumps({"exact": exact,
                       "payload_bytes": int(sum(x.size for x in pays) * 4), "dense_bytes": int(dense_rows.nbytes),
                       "or_rows_us": r_s, "or_bits_us": r_d}), flush=True)
 
