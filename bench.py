@@ -519,15 +519,16 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
         def step(i):
             nonlocal payload
             src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+            if mode == "peer":          # the decode kernel writes the payload itself (fixed slots, no pack)
+                pay = peer.payload()
+                ix.decode_step_payload(tokens[i], src[0], src[1], dst[0], dst[1], pay, V, SHIFT, reset_below=0)
+                peer(pay, B, V, SHIFT, out=out)
+                return
             ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1],
                            packed=True)
             if mode == "dense":
                 dist.all_gather_into_tensor(parts, mine)
                 or_bits(parts, V, out=out)
-            elif mode == "peer":
-                pay = peer.payload()
-                ix.shard_pack(dst[0], dst[1], mine, V, payload=pay)
-                peer(pay, B, V, SHIFT, out=out)
             else:
                 payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
                 xchg(payload, B, V, SHIFT, out=out)
@@ -573,7 +574,8 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
         peer.close()
         modes["peer"] = {"ms_per_step": ms_peer, "value": B / (ms_peer / 1e3), "masks_equal_unsharded": exact_peer,
                          "exchange_bytes_per_step_median": modes["sparse"]["exchange_bytes_per_step_median"],
-                         "step": "fm_shard_pack into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
+                         "step": "fm_decode_step_payload (the decode kernel writes the payload, fixed row slots) "
+                                 "into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
                                  "fm_shard_or_rows_peers reading every rank's payload over xGMI"}
     else:
         modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
@@ -692,7 +694,7 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
         Wd = (V + 31) // 32
         parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
-        shards, last_pay, pay_words = [], [], []
+        shards, last_pay, pay_words, fix_pay = [], [], [], []
         for r in range(world):
             t0 = time.time()
             t_r, (a, b) = shard_text_device(text, beg, world, r, halo)
@@ -744,11 +746,35 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
                 sizes.append(int(ix.shard_pack(dst[0], dst[1], scratch, V, payload=pay)[0].item()))
             pay_words.append(sizes)
             del g_pack, pay, scratch
+            # the peer exchange's decode: the kernel writes the payload itself (fixed row slots, no pack);
+            # the same K steps from the same state, graph-captured, cold like the packed steps
+            fpay = torch.zeros(payload_capacity(B, V), dtype=torch.int32, device=dev)
+            g_pd = torch.cuda.CUDAGraph()
+            lo.copy_(s_lo)
+            hi.copy_(s_hi)
+            with torch.cuda.graph(g_pd):
+                for i in range(K):
+                    src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+                    ix.decode_step_payload(tokens[W + i], src[0], src[1], dst[0], dst[1], fpay, V, SHIFT,
+                                           reset_below=0)
+            pd_warm = []
+            for _ in range(3):
+                lo.copy_(s_lo)
+                hi.copy_(s_hi)
+                pd_warm.append(replay(g_pd, False) / K * 1e3)
+            lo.copy_(s_lo)
+            hi.copy_(s_hi)
+            pd_cold = replay(g_pd, True) / K * 1e3
+            pd_same = bool(torch.equal(bufs[K % 2][0], fin_lo) and torch.equal(bufs[K % 2][1], fin_hi))
+            fix_pay.append(fpay)
+            del g_pd
             st = ix.stats()
             shards.append({"docs": [int(a), int(b)], "rows": int(rows), "device_bytes": int(st["device_bytes"]),
                            "build_s": round(build_s, 2), "cold_us_per_step": cold,
                            "warm_us_per_step": float(np.median(warm)), "pack_cold_us": pack_cold,
-                           "payload_bytes_per_step_median": 4.0 * float(np.median(sizes))})
+                           "payload_bytes_per_step_median": 4.0 * float(np.median(sizes)),
+                           "payload_decode_cold_us": pd_cold, "payload_decode_warm_us": float(np.median(pd_warm)),
+                           "payload_decode_states_equal": pd_same})
             mem_log(f"c4 shard {r} built", dev)
             log(f"c4 shard {r}: rows {rows}, build {build_s:.1f}s, step cold {cold:.1f}us warm {np.median(warm):.1f}us")
             del g, ix, bufs, lo, hi, s_lo, s_hi
@@ -786,11 +812,12 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         sp_cold = replay(g_sp, True) / K * 1e3
         exact_sparse = exact_sparse and bool(torch.equal(out, ref))
         del spk, g_sp, sp
-        # the peer exchange's pass (fm_shard_or_rows_peers) over the same 8 payloads, each in a
-        # buffer of its own of the full capacity, as the ranks' IPC-mapped buffers are (here local)
+        # the peer exchange's pass (fm_shard_or_rows_peers) over the 8 shards' last-step payloads as the
+        # payload decode wrote them (fixed row slots, each in a buffer of its own, as the ranks'
+        # IPC-mapped buffers are -- here local)
         cap = payload_capacity(B, V)
         pb = torch.zeros((K, world, cap), dtype=torch.int32, device=dev)
-        for r, p in enumerate(last_pay):
+        for r, p in enumerate(fix_pay):
             pb[:, r, :p.numel()] = p
         ptabs = torch.tensor([[pb[i, r].data_ptr() for r in range(world)] for i in range(K)], dtype=torch.int64,
                              device=dev)
@@ -836,12 +863,15 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         # payload / 153 GB/s on top of the pass measured here over local buffers, + 2 us per remote
         # round trip: the header, then the data)
         remote_us = sp_slice / 153e9 * 1e6 + 2 * 2.0
+        slow_pd = max(s["payload_decode_cold_us"] for s in shards)
         peer = {"masks_equal_unsharded": exact_peer, "or_rows_peers_cold_us": pp_cold,
-                "or_rows_peers_warm_us": pp_warm, "pack_cold_us_slowest_shard": pack,
+                "or_rows_peers_warm_us": pp_warm, "payload_decode_cold_us_slowest_shard": slow_pd,
+                "payload_decode_states_equal": all(s["payload_decode_states_equal"] for s in shards),
                 "barrier_us_assumed": 15.0, "remote_read_model_us": remote_us,
-                "predicted_step_us": slow + pack + 15.0 + remote_us + pp_cold,
-                "note": "payloads in IPC-mapped buffers read in place (fm_shard_or_rows_peers): no sizes "
-                        "exchange, no gather; here over local buffers"}
+                "predicted_step_us": slow_pd + 15.0 + remote_us + pp_cold,
+                "note": "the decode kernel writes each shard's payload (fixed row slots, no pack pass) into "
+                        "IPC-mapped buffers read in place (fm_shard_or_rows_peers): no sizes exchange, no "
+                        "gather; here over local buffers"}
         return {"shards": world, "halo": halo, "global_batch": B, "steps": K, "per_shard": shards,
                 "sparse_exchange": sparse, "peer_exchange": peer,
                 "slowest_shard_cold_us": slow, "or_pass_cold_us": or_cold, "or_pass_warm_us": or_warm,

@@ -57,7 +57,9 @@ constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
 // symbols before the slice (128-bit aligned) and ends 64 after it
 __host__ __device__ constexpr uint32_t win_words(uint64_t sw) { return (uint32_t)(sw / 32 + 16); }
 constexpr uint64_t kEarlyZeroWidth = 64;      // rows this narrow get their zeros written up front
-constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
+constexpr int kUnroll = 4;
+constexpr uint32_t kPayMagic = 0x58534D46u;    // the shard payload's magic (csrc/shard.hip)
+constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144                    // uint4 loads in flight per thread while streaming
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release/acquire, which on gfx950 also drains every wave's outstanding
@@ -357,7 +359,16 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // the compiler's own allocation (92 VGPRs, 5 waves) is kept
 #define FMIDX_SMALL_WG_WAVES 1
 #endif
-template <bool PACKED, bool DO_LF, int kDecThreads>
+// PAY (with PACKED and DO_LF, one slice per row): the output is the doc-range
+// shards' exchange payload (csrc/shard.hip's layout) with FIXED row slots --
+// row b's data at H + b * round4(W) words, W = ceil(vocab / 32) -- so no pack
+// pass is needed when the payload is read in place (PeerExchange): a row whose
+// new range is streamed whole and narrower than W (every row narrower than W
+// when the bitmap blocks and the cache start above W) writes its BWT slice
+// (the symbols) and nothing else -- no zero-fill, no bitmap; every other row
+// writes its packed bitmap into its slot exactly as PACKED does; the row's
+// workgroup writes its desc / off words, row 0's the header.
+template <bool PACKED, bool DO_LF, int kDecThreads, bool PAY = false>
 // Argument order: the per-row state pointers and the slice geometry come first
 // so that, with kernel-argument preloading (Makefile: -amdgpu-kernarg-preload-
 // count), they arrive in SGPRs at dispatch and the row-state loads issue
@@ -370,7 +381,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        uint64_t* __restrict__ hi_out,
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
-                                                       uint64_t early_width, DevView v) {
+                                                       uint64_t early_width, DevView v,
+                                                       uint32_t* __restrict__ pay) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
   // zero-filling waves -- from thread 256, 512 or 768 -- measured the same)
@@ -417,7 +429,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // chunks holding an allowed token.
   const bool reset = DO_LF && st_tok < reset_below;
   const uint64_t in_lo = st_lo, in_hi = min(st_hi, v.n);
-  const bool early_zero = !reset && (in_lo >= in_hi || in_hi - in_lo <= early_width);
+  const bool early_zero = !PAY && !reset && (in_lo >= in_hi || in_hi - in_lo <= early_width);
   // Incoming ranges of kENarrow+1 .. kEWide rows that the transition table does
   // not serve take their LF step as ONE scan of E[lo, hi) by the whole
   // workgroup (<= kEWide / kDecThreads entries per thread, one round trip)
@@ -552,6 +564,47 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   lds_barrier();
   const uint64_t lo = s_lohi[0], hi = s_lohi[1];
   FM_STAMP(v, 3);
+  if constexpr (PAY) {
+    const uint32_t Wd = (uint32_t)((vocab + 31) / 32);
+    const uint64_t W4 = ((uint64_t)Wd + 3) & ~3ull;
+    const bool sparse = lo >= hi || (hi - lo < Wd && plan.nb == 0);   // workgroup-uniform
+    if (threadIdx.x == 0) {
+      const uint64_t H = 4 + ((2 * m + 3) & ~3ull);
+      pay[4 + row] = sparse ? (uint32_t)(lo < hi ? hi - lo : 0) : (Wd | 0x80000000u);
+      pay[4 + m + row] = (uint32_t)(H + row * W4);
+      if (row == 0) {
+        pay[0] = (uint32_t)(H + m * W4);
+        pay[1] = (uint32_t)m;
+        pay[2] = Wd;
+        pay[3] = kPayMagic;
+      }
+    }
+    if (sparse) {
+      // the slice BWT[lo, hi): every load of the thread in flight together (clamped, masked after)
+      const uint32_t w = lo < hi ? (uint32_t)(hi - lo) : 0u;
+      for (uint32_t i0 = 0; i0 < w; i0 += 8 * kDecThreads) {
+        uint32_t sy[8];
+        if (v.bwt) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sy[u] = v.bwt[lo + min(i0 + threadIdx.x + (uint32_t)u * kDecThreads, w - 1)];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            sy[u] = (uint32_t)(v.E[lo + min(i0 + threadIdx.x + (uint32_t)u * kDecThreads, w - 1)] >> kESymShift);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t i = i0 + threadIdx.x + (uint32_t)u * kDecThreads;
+          if (i < w) store4(orsrc, i * 4, sy[u]);
+        }
+      }
+      if (DO_LF && threadIdx.x == 0) {
+        lo_out[row] = lo;
+        hi_out[row] = hi;
+      }
+      return;
+    }
+  }
   // Roles.  A wave with stores in flight cannot wait on a load without
   // waiting for its stores too (shared vmcnt), so loads go to store-free waves:
   //   early zero  (narrow input): waves 1.. have zero-filled; wave 0 streams
@@ -862,7 +915,7 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   const size_t lds = (size_t)win_words(SW) * 4;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v)
+                                        mask, ld, ew, v, nullptr)
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
@@ -881,6 +934,45 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   }
 #undef FM_LAUNCH_T
 #undef FM_LAUNCH
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
+                          const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                          uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, hipStream_t s) {
+  if (m == 0) return 0;
+  const uint64_t W = (vocab + 31) / 32, W4 = (W + 3) & ~3ull, H = 4 + ((2 * m + 3) & ~3ull);
+  if (!pay || !tok || !lo_in || !hi_in || !lo_out || !hi_out || vocab == 0 || W > kPayMaxWords ||
+      m >= (1ull << 31) || (reinterpret_cast<uintptr_t>(pay) & 15)) {
+    set_error("decode payload: bad arguments (vocab %llu <= 262144, 16-B aligned payload)",
+              (unsigned long long)vocab);
+    return -1;
+  }
+  if (cap < H + m * W4 || H + m * W4 >= (1ull << 32)) {
+    set_error("decode payload: %llu words, %llu needed (< 2^32)", (unsigned long long)cap,
+              (unsigned long long)(H + m * W4));
+    return -1;
+  }
+  if (lo_in == lo_out || hi_in == hi_out) {
+    set_error("fused decode step: state in/out buffers must not alias (ping-pong them)");
+    return -1;
+  }
+  const uint32_t T = decode_threads(m);
+  const uint32_t S = 1, SW = (uint32_t)((vocab + 63) & ~63ull);   // one slice per row: whole-row decisions
+  const unsigned g = (unsigned)((m + 7) / 8 * 8);
+  const size_t lds = (size_t)win_words(SW) * 4;
+  uint8_t* mask = reinterpret_cast<uint8_t*>(pay + H);
+  const uint64_t ld = W4 * 4;
+  if (T == 1024)
+    k_decode<true, true, 1024, true><<<g, 1024, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
+                                                          reset_below, mask, ld, 0, v, pay);
+  else if (T == 512)
+    k_decode<true, true, 512, true><<<g, 512, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
+                                                        reset_below, mask, ld, 0, v, pay);
+  else
+    k_decode<true, true, 256, true><<<g, 256, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
+                                                        reset_below, mask, ld, 0, v, pay);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -65,6 +65,8 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_processor_call": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_shard_payload_capacity": (c_int, [c_uint64, c_uint64, u64p]),
+    "fm_decode_step_payload": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p]),
     "fm_shard_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p,
                               c_uint64, c_void_p]),
     "fm_shard_or_rows": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p, c_uint64,

@@ -353,6 +353,20 @@ class FMIndex:
             hi.copy_(hi_out)
         return mask
 
+    def decode_step_payload(self, tokens, lo, hi, lo_out, hi_out, payload, vocab: int, shift: int,
+                            reset_below: int = -(1 << 63)):
+        """The fused LF step writing the shard exchange's payload with fixed row
+        slots (fm_decode_step_payload): per row the BWT slice of its new range
+        when narrower than ceil(vocab/32) words and streamed whole, else its
+        packed bitmap -- what PeerExchange's readers take in place, no pack
+        pass.  ``payload``: int32, >= payload_capacity(B, vocab) words."""
+        check(lib().fm_decode_step_payload(self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below),
+                                           c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
+                                           c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()), lo.numel(),
+                                           c_void_p(payload.data_ptr()), payload.numel(), int(vocab),
+                                           c_void_p(_stream_of(lo))), "decode_step_payload")
+        return payload
+
     def shard_pack(self, lo, hi, bits, vocab: int, payload=None):
         """The sparse exchange payload of this shard's rows (fm_shard_pack):
         per row its BWT slice when narrower than a bitmap, else its packed

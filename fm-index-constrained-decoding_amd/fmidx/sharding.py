@@ -189,6 +189,8 @@ class ShardedDecoder:
         if not self.fused:
             self.index.lf_step_batch(tokens, self.lo, self.hi, self.shift, reset_below=0)
             return self.mask()
+        if self.group is not None and self.reduce == "peer" and hasattr(self.index, "decode_step_payload"):
+            return self._step_peer(tokens)
         packed = self.group is not None and self.reduce in ("gather_bits", "sparse", "peer")
         if self._buf is None:
             B = self.lo.numel()
@@ -207,6 +209,29 @@ class ShardedDecoder:
         if self.group is not None and self.reduce == "peer":
             return self._combine_peer(self._buf)
         return self._combine(self._buf, packed)
+
+    def _step_peer(self, tokens):
+        """The peer exchange's step: the decode kernel writes this rank's payload
+        itself (fixed row slots, fm_decode_step_payload: no pack pass), then the
+        barrier and the in-place OR of every rank's payload."""
+        import torch
+
+        B = self.lo.numel()
+        if self._peer is None or self._peer.rows < B:
+            self.close()
+            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier)
+        if self._buf is None:              # start() resets it: fresh second state buffers
+            self._lo2 = torch.empty_like(self.lo)
+            self._hi2 = torch.empty_like(self.hi)
+            self._buf = ()
+        pay = self._peer.payload()
+        self.index.decode_step_payload(tokens, self.lo, self.hi, self._lo2, self._hi2, pay, self.vocab, self.shift,
+                                       reset_below=0)
+        self.lo, self._lo2 = self._lo2, self.lo
+        self.hi, self._hi2 = self._hi2, self.hi
+        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
+            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=pay.device)
+        return self._peer(pay, B, self.vocab, self.shift, out=self._out)
 
     def _combine_peer(self, bits):
         import torch

@@ -277,6 +277,17 @@ int fm_or_bits(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, u
  * Layout: csrc/shard.hip.  Replaces the dense OR-exchange SURVEY §8e
  * describes (all_gather of packed [B, V/32] rows). */
 int fm_shard_payload_capacity(uint64_t B, uint64_t vocab, uint64_t* words);
+/* The decode step (fm_decode_step_batch's LF step, packed) writing the exchange
+ * payload itself, with FIXED row slots (row b at H + b * round4(W) words, the
+ * capacity fm_shard_payload_capacity gives): a row whose new range is narrower
+ * than W and streamed whole gets its BWT slice, every other row its bitmap; no
+ * pack pass.  For payloads read in place (fm_shard_or_rows_peers), whose wire
+ * cost is what the reader reads, not the capacity; an all_gather would ship the
+ * whole capacity (use fm_shard_pack there).  vocab <= 262144; d_payload 16-B
+ * aligned, cap_words >= fm_shard_payload_capacity(m, vocab). */
+int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                           const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
+                           uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab, void* stream);
 int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
                   uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,

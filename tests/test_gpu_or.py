@@ -171,3 +171,70 @@ def test_sparse_or_reads_nothing_past_a_short_gather(dev):
         assert torch.equal(got.cpu(), want), m
     full = or_payloads(pay[:used].unsqueeze(0).contiguous(), B, V, 10)
     assert torch.equal(full, ix.allowed_mask(lo_t, hi_t, V, 10))
+
+
+@pytest.mark.parametrize("V", [100, 128256])
+def test_decode_payload_equals_packed_decode_and_unsharded(dev, V):
+    """fm_decode_step_payload (the decode kernel writing the exchange payload
+    itself, fixed row slots): per shard the same new states as
+    fm_decode_step_batch, and the in-place OR of the shards' payloads
+    (fm_shard_or_rows_peers) equal to the unsharded index's mask after the
+    same step -- over rows that restart, go empty, stay narrow and stay wide,
+    for two steps (the payload buffer rewritten)."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from fmidx.sharding import or_peer_payloads, payload_capacity, shard_corpus
+
+    rng = np.random.default_rng(V + 17)
+    vocab_used = min(V, 3000)
+    docs = [rng.integers(0, vocab_used, size=int(rng.integers(5, 400))).tolist() for _ in range(300)]
+    for d in docs[::3]:
+        d[:4] = [1, 2, 3, 4]
+    F = [t for d in reversed(docs) for t in d]
+    world, B, halo = 3, 64, 16
+    starts = rng.integers(0, len(F) - 12, B)
+    pats = [[]] + [[1]] + [[1, 2]] + [F[s:s + int(rng.integers(1, 4))] for s in starts[3:]]
+    full = FMIndex()
+    full.initialize(docs, in_memory=True)
+    shards = []
+    for r in range(world):
+        sd, _ = shard_corpus(docs, world, r, halo)
+        ix = FMIndex()
+        ix.initialize(sd, in_memory=True)
+        shards.append(ix)
+
+    def ranges(ix):
+        lo, hi = ix.get_range_batch(pats, 10)
+        return torch.tensor(lo.astype(np.int64), device=dev), torch.tensor(hi.astype(np.int64), device=dev)
+
+    states = [ranges(ix) for ix in shards]
+    flo, fhi = ranges(full)
+    cap = payload_capacity(B, V)
+    bufs = [torch.full((cap,), -7, dtype=torch.int32, device=dev) for _ in range(world)]
+    ptrs = torch.tensor([b.data_ptr() for b in bufs], dtype=torch.int64, device=dev)
+    W = (V + 31) // 32
+    for step in range(2):
+        nxt = [F[s + len(p)] if s + len(p) < len(F) else -1 for s, p in zip(starts, pats)]
+        tok = [(-1 if i % 11 == 5 else (vocab_used + 3 if i % 13 == 7 else t)) for i, t in enumerate(nxt)]
+        tok_t = torch.tensor(tok, dtype=torch.int64, device=dev)
+        new_states = []
+        for r, ix in enumerate(shards):
+            lo, hi = states[r]
+            lo2, hi2 = torch.empty_like(lo), torch.empty_like(hi)
+            ix.decode_step_payload(tok_t, lo, hi, lo2, hi2, bufs[r], V, 10, reset_below=0)
+            plo, phi = torch.empty_like(lo), torch.empty_like(hi)
+            bits = torch.empty((B, W), dtype=torch.int32, device=dev)
+            ix.decode_step(tok_t, lo, hi, bits, V, 10, reset_below=0, lo_out=plo, hi_out=phi, packed=True)
+            assert torch.equal(lo2, plo) and torch.equal(hi2, phi), (step, r)
+            desc = bufs[r][4:4 + B].cpu().numpy().view(np.uint32)
+            w = (np.minimum(hi2.cpu().numpy(), ix.size()) - lo2.cpu().numpy()).clip(min=0)
+            np.testing.assert_array_equal((desc >> 31) == 0, w < W)     # streamed narrow rows ship their slice
+            new_states.append((lo2, hi2))
+        states = new_states
+        fm = torch.empty((B, V), dtype=torch.uint8, device=dev)
+        flo2, fhi2 = torch.empty_like(flo), torch.empty_like(fhi)
+        full.decode_step(tok_t, flo, fhi, fm, V, 10, reset_below=0, lo_out=flo2, hi_out=fhi2)
+        flo, fhi = flo2, fhi2
+        assert torch.equal(or_peer_payloads(ptrs, cap, B, V, 10), fm), step
+        pats = [([] if t < 0 else p + [t]) for p, t in zip(pats, tok)]
