@@ -231,3 +231,42 @@ def test_halo_guard():
         dec.step(tok)
     with pytest.raises(HaloExceeded):
         ShardedDecoder(shard, V, SHIFT, halo=3).start(pats + [[1, 2, 3]], "cpu")
+
+
+def test_fixed_slot_payload_reads_like_compact():
+    """fm_decode_step_payload's layout -- every row at a fixed slot H + b *
+    round4(W), the unused words of a slot left as they were -- read by the
+    host reader (and, on the GPU, fm_shard_or_rows / _peers, which follow the
+    same desc / off words) gives what the compact payload of the same rows
+    gives, for every row kind: empty, a slice narrower than W, a bitmap."""
+    from fmidx.sharding import or_payloads_host, pack_payload_host
+
+    rng = np.random.default_rng(4)
+    V, B, SH = 200, 24, 10
+    W = (V + 31) // 32
+    n = 3000
+    bwt = rng.integers(0, V + SH, size=n)
+    lo = rng.integers(0, n - 40, size=B)
+    width = rng.choice([0, 1, 3, W - 1, W, W + 9, 37], size=B)
+    hi = lo + width
+    bits = np.zeros((B, W * 32), dtype=np.uint8)
+    for b in range(B):
+        t = bwt[lo[b]:hi[b]] - SH
+        bits[b, t[(t >= 0) & (t < V)]] = 1
+    words = np.packbits(bits, axis=1, bitorder="little").view(np.int32)
+    compact = pack_payload_host(lo, hi, bwt, words, V)
+    H = 4 + ((2 * B + 3) & ~3)
+    W4 = (W + 3) & ~3
+    fixed = rng.integers(-2**31, 2**31, size=H + B * W4).astype(np.int64).astype(np.uint32)   # garbage
+    c = compact.numpy().view(np.uint32)
+    fixed[:4] = [H + B * W4, B, W, c[3]]
+    for b in range(B):
+        d, o = int(c[4 + b]), int(c[4 + B + b])
+        cnt = d & 0x7FFFFFFF
+        fixed[4 + b] = d
+        fixed[4 + B + b] = H + b * W4
+        fixed[H + b * W4:H + b * W4 + cnt] = c[o:o + cnt]
+    got = or_payloads_host(torch.from_numpy(fixed.view(np.int32)).unsqueeze(0), B, V, SH)
+    want = or_payloads_host(compact.unsqueeze(0), B, V, SH)
+    assert torch.equal(got, want)
+    assert torch.equal(want, torch.from_numpy(bits[:, :V]))
