@@ -519,7 +519,7 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
         def step(i):
             nonlocal payload
             src, dst = bufs[i % 2], bufs[(i + 1) % 2]
-            if mode == "peer":          # the decode kernel writes the payload itself (fixed slots, no pack)
+            if mode in ("peer", "peer_flags"):   # the decode kernel writes the payload itself (fixed slots, no pack)
                 pay = peer.payload()
                 ix.decode_step_payload(tokens[i], src[0], src[1], dst[0], dst[1], pay, V, SHIFT, reset_below=0)
                 peer(pay, B, V, SHIFT, out=out)
@@ -571,12 +571,21 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     }
     if peer is not None:
         ms_peer, exact_peer = run("peer")
-        peer.close()
         modes["peer"] = {"ms_per_step": ms_peer, "value": B / (ms_peer / 1e3), "masks_equal_unsharded": exact_peer,
                          "exchange_bytes_per_step_median": modes["sparse"]["exchange_bytes_per_step_median"],
                          "step": "fm_decode_step_payload (the decode kernel writes the payload, fixed row slots) "
                                  "into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
                                  "fm_shard_or_rows_peers reading every rank's payload over xGMI"}
+        peer.barrier_mode = "flags"     # the same buffers, no collective: flag words over xGMI
+        ms_pf, exact_pf = run("peer_flags")
+        t_err = torch.tensor([peer.errors()], device=dev)
+        dist.all_reduce(t_err, op=dist.ReduceOp.MAX)
+        modes["peer_flags"] = {"ms_per_step": ms_pf, "value": B / (ms_pf / 1e3),
+                               "masks_equal_unsharded": exact_pf and not int(t_err.item()),
+                               "flag_timeouts_last_step": int(t_err.item()),
+                               "step": "as peer, with the barrier as flag words: fm_peer_signal (system-scope "
+                                       "stores into every rank's flag array) + fm_shard_or_rows_peers_wait"}
+        peer.close()
     else:
         modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
     exact_modes = [m for m, r in modes.items() if r.get("masks_equal_unsharded")]

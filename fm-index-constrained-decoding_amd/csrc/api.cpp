@@ -1293,7 +1293,26 @@ int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_
                            uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
   FM_API_BEGIN
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
-                                           reinterpret_cast<hipStream_t>(stream));
+                                           nullptr, 0, nullptr, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                                uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
+                                const uint32_t* d_flags, uint32_t step, uint32_t* d_err, void* stream) {
+  FM_API_BEGIN
+  if (!d_flags) {
+    set_error("shard_or_rows_peers_wait: null flags");
+    return -1;
+  }
+  return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
+                                           d_flags, step, d_err, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t step, void* stream) {
+  FM_API_BEGIN
+  return fmidx::launch_peer_signal(d_flag_ptrs, world, step, reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 

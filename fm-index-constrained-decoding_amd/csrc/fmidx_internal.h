@@ -742,7 +742,9 @@ int launch_shard_pack(const DevView& v, const uint64_t* lo, const uint64_t* hi, 
 int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride, uint64_t B, uint64_t vocab,
                          int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s);
 int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
-                               int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s);
+                               int64_t shift, void* out, uint64_t ld, int unpack, const uint32_t* flags,
+                               uint32_t want, uint32_t* err, hipStream_t s);
+int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t value, hipStream_t s);
 int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t wpr,
                    uint64_t vocab, void* out, uint64_t ld_out, int unpack, hipStream_t s);
 

@@ -73,6 +73,9 @@ SIGNATURES = {
                                  c_int, c_void_p]),
     "fm_shard_or_rows_peers": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
                                        c_uint64, c_int, c_void_p]),
+    "fm_peer_signal": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p]),
+    "fm_shard_or_rows_peers_wait": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
+                                            c_uint64, c_int, c_void_p, c_uint32, c_void_p, c_void_p]),
     "fm_ipc_handle": (c_int, [c_void_p, c_void_p, u64p]),
     "fm_ipc_open": (c_int, [c_void_p, POINTER(c_void_p)]),
     "fm_ipc_close": (c_int, [c_void_p]),

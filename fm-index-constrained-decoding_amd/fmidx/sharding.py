@@ -513,8 +513,13 @@ class PeerExchange:
     pack (RCCL runs it after the rank's pack and completes it only when every
     rank's has run, so the OR that follows on the stream sees every payload;
     the processors pass ``barrier_done`` when their facts all_reduce, issued
-    after the pack, already is one); "host" -- synchronize + group barrier
-    (gloo; ranks sharing a GPU, where RCCL refuses to run).  Two buffers are
+    after the pack, already is one); "flags" -- no collective at all: after
+    its pack every rank stores the step number into its word of every rank's
+    flag array (fm_peer_signal, system-scope stores over xGMI) and the OR pass
+    first waits for all of its own words (fm_shard_or_rows_peers_wait,
+    bounded: a step that times out is recorded in ``errors()``); "host" --
+    synchronize + group barrier (gloo; ranks sharing a GPU, where RCCL
+    refuses to run).  Two buffers are
     enough: a rank packs buffer k again two steps later, after a barrier that
     every rank entered only after its OR of buffer k had been issued before it
     on its stream.  ``capacity_rows``: the largest batch the buffers hold
@@ -527,7 +532,7 @@ class PeerExchange:
 
         from ._lib import check, lib
 
-        if barrier not in ("collective", "host"):
+        if barrier not in ("collective", "host", "flags"):
             raise ValueError(barrier)
         self.group, self.barrier_mode, self.vocab = group, barrier, vocab
         self.device = torch.device(device)
@@ -536,9 +541,12 @@ class PeerExchange:
         self.rows = capacity_rows
         self.cap = payload_capacity(capacity_rows, vocab)
         self.bufs = [torch.zeros(self.cap, dtype=torch.int32, device=self.device) for _ in range(2)]
+        # the flag barrier's words (one per rank) and its error word, shared like the payloads
+        self.flags = torch.zeros(max(64, self.world), dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         torch.cuda.synchronize(self.device)
         mine = []
-        for b in self.bufs:
+        for b in self.bufs + [self.flags]:
             hd = (c_uint8 * 64)()
             off = c_uint64(0)
             check(lib().fm_ipc_handle(c_void_p(b.data_ptr()), hd, byref(off)), "ipc_handle")
@@ -546,12 +554,12 @@ class PeerExchange:
         every = [None] * self.world
         dist.all_gather_object(every, mine, group=group)
         self._opened = []
-        table = [[0] * self.world for _ in range(2)]
+        table = [[0] * self.world for _ in range(3)]   # payload buffer 0, buffer 1, flag array
         try:
             for r, hs in enumerate(every):
                 for k, (hd, off) in enumerate(hs):
                     if r == self.rank:
-                        table[k][r] = self.bufs[k].data_ptr()
+                        table[k][r] = (self.bufs + [self.flags])[k].data_ptr()
                         continue
                     base = c_void_p()
                     check(lib().fm_ipc_open((c_uint8 * 64).from_buffer_copy(hd), byref(base)), f"ipc_open (rank {r})")
@@ -560,7 +568,9 @@ class PeerExchange:
         except Exception:
             self._unmap()
             raise
-        self.ptab = torch.tensor(table, dtype=torch.int64, device=self.device)
+        self.ptab = torch.tensor(table[:2], dtype=torch.int64, device=self.device)
+        # this rank's word in every rank's flag array
+        self.signal_to = torch.tensor([a + 4 * self.rank for a in table[2]], dtype=torch.int64, device=self.device)
         self._tok = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.step = 0
 
@@ -585,11 +595,28 @@ class PeerExchange:
             raise ValueError("PeerExchange: pack into payload() of this step")
         if B > self.rows or vocab != self.vocab:
             raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
-        if not barrier_done:
-            self.barrier()
-        out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack)
+        if self.barrier_mode == "flags":
+            import torch
+            from ctypes import c_void_p
+
+            from ._lib import check, lib
+
+            n = (self.step + 1) & 0x7FFFFFFF or 1
+            stream = c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            check(lib().fm_peer_signal(c_void_p(self.signal_to.data_ptr()), self.world, n, stream), "peer_signal")
+            out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack,
+                                   flags=(self.flags, n, self.err))
+        else:
+            if not barrier_done:
+                self.barrier()
+            out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack)
         self.step += 1
         return out
+
+    def errors(self) -> int:
+        """The last step number whose flag barrier timed out (0: none) -- a read of
+        the device error word (synchronises)."""
+        return int(self.err.item())
 
     def _unmap(self):
         from ctypes import c_void_p
@@ -612,7 +639,7 @@ class PeerExchange:
         self._unmap()
 
 
-def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True, flags=None):
     """OR of the payloads at the device addresses ``ptrs`` (int64 [P], on the
     GPU that runs the pass; each payload ``cap`` words, in this process or a
     peer's buffer mapped by fm_ipc_open) -> uint8 [B, vocab] (unpack) or int32
@@ -631,6 +658,13 @@ def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, u
     assert out.stride(1) == 1 and out.device == ptrs.device
     ld = out.stride(0) * out.element_size()
     stream = torch.cuda.current_stream(ptrs.device).cuda_stream
+    if flags is not None:          # (flag words int32 [>= P], step number, error word): the flag barrier first
+        fw, step, err = flags
+        check(lib().fm_shard_or_rows_peers_wait(c_void_p(ptrs.data_ptr()), ptrs.numel(), int(cap), B, vocab,
+                                                int(shift), c_void_p(out.data_ptr()), ld, 1 if unpack else 0,
+                                                c_void_p(fw.data_ptr()), int(step), c_void_p(err.data_ptr()),
+                                                c_void_p(stream)), "shard_or_rows_peers_wait")
+        return out
     check(lib().fm_shard_or_rows_peers(c_void_p(ptrs.data_ptr()), ptrs.numel(), int(cap), B, vocab, int(shift),
                                        c_void_p(out.data_ptr()), ld, 1 if unpack else 0, c_void_p(stream)),
           "shard_or_rows_peers")

@@ -308,6 +308,17 @@ int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_str
 #define FM_IPC_HANDLE_BYTES 64
 int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                            uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
+/* The flag barrier instead of a collective: each rank owns a uint32 flag word per
+ * rank (d_flags[world], zeroed, IPC-shared).  fm_peer_signal stores `step` into
+ * every rank's word for this rank (d_flag_ptrs[world]: the peers' word
+ * addresses, mapped; system-scope vector stores) -- issue it after the kernel
+ * that wrote this rank's payload; fm_shard_or_rows_peers_wait first waits until
+ * every d_flags[p] >= step (system-scope polls, bounded: on timeout *d_err =
+ * step and the pass goes on), then ORs as fm_shard_or_rows_peers. */
+int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t step, void* stream);
+int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                                uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
+                                const uint32_t* d_flags, uint32_t step, uint32_t* d_err, void* stream);
 int fm_ipc_handle(const void* d_ptr, uint8_t* handle, uint64_t* offset);
 int fm_ipc_open(const uint8_t* handle, void** d_base);
 int fm_ipc_close(void* d_base);

@@ -3,9 +3,11 @@ configs[3]) across PROCESSES: two ranks, each its own process with its own
 doc-range shard (halo 32), swap their payload buffers' IPC handles
 (fm_ipc_handle / fm_ipc_open) and OR each other's payloads in place
 (fm_shard_or_rows_peers).  On the one-GPU box both ranks share the GPU, so
-the group is gloo and the barrier is the host one (RCCL refuses two ranks on
-one device; the stream-ordered RCCL barrier runs in the world-1 test of
-test_gpu_shard_processors.py and in bench.py at N > 1).  Each rank checks,
+the group is gloo and the barrier is the host one or the flag words (no
+collective per step at all: each rank's signal kernel stores the step number
+into the other's flag array, its OR pass waits for them); RCCL refuses two
+ranks on one device, so the stream-ordered RCCL barrier runs in the world-1
+test of test_gpu_shard_processors.py and in bench.py at N > 1.  Each rank checks,
 bit for bit, against the unsharded index it builds too:
   * ShardedDecoder(reduce="peer") over 14 steps with restarts, a step where
     every row restarts (every payload a bitmap) and the double-buffered
@@ -31,7 +33,7 @@ def _corpus():
     return docs
 
 
-def _child(rank, world, port, outdir):
+def _child(rank, world, port, outdir, barrier):
     import torch
     import torch.distributed as dist
 
@@ -53,7 +55,7 @@ def _child(rank, world, port, outdir):
         B = 48
         starts = rng.integers(0, len(F) - 40, size=B)
         pats = [F[a:a + 2] for a in starts]
-        dec = ShardedDecoder(ix, V, 10, group=dist.group.WORLD, reduce="peer", halo=HALO, peer_barrier="host")
+        dec = ShardedDecoder(ix, V, 10, group=dist.group.WORLD, reduce="peer", halo=HALO, peer_barrier=barrier)
         ref = ShardedDecoder(full, V, 10)
         dec.start(pats, "cuda")
         ref.start(pats, "cuda")
@@ -68,11 +70,13 @@ def _child(rank, world, port, outdir):
             if not torch.equal(got, want):
                 bad.append(f"decoder step {step}")
         assert dec._peer.step == 14
+        if barrier == "flags" and dec._peer.errors():
+            bad.append(f"flag barrier timed out at step {dec._peer.errors()}")
         dec.close()
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         pr_ref = mk(full)
         sidx = ShardedIndex(ix, full.occurring_distinct, group=dist.group.WORLD, halo=HALO, exchange="peer",
-                            peer_barrier="host")
+                            peer_barrier=barrier)
         pr = mk(sidx)
         for step in range(5):
             ids = torch.tensor([[1] + F[a:a + 1 + step] for a in starts[:16]], dtype=torch.int64).cuda()
@@ -86,14 +90,15 @@ def _child(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_peer_exchange_two_processes(tmp_path):
+@pytest.mark.parametrize("barrier", ["host", "flags"])
+def test_peer_exchange_two_processes(tmp_path, barrier):
     import torch.multiprocessing as mp
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    ctx = mp.spawn(_child, args=(WORLD, port, str(tmp_path)), nprocs=WORLD, join=False)
+    ctx = mp.spawn(_child, args=(WORLD, port, str(tmp_path), barrier), nprocs=WORLD, join=False)
     deadline = time.time() + 240
     try:
         while not ctx.join(timeout=5):

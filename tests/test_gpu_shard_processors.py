@@ -211,14 +211,17 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
             want = full.allowed_mask(dec.lo, dec.hi, V, 10)
             assert torch.equal(got, want), step
         assert dec._xchg.respecified >= 1          # the restart step outgrew the speculative size
-        # the peer exchange, its stream-ordered RCCL barrier (a world of one: the own buffer only)
-        pdec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="peer", halo=None)
-        pdec.start(pats, "cuda")
-        for step in range(6):
-            tok = [F[a + 3 + step] if rng.random() < 0.8 else -1 for a in starts]
-            got = pdec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
-            assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), step
-        pdec.close()
+        # the peer exchange with its stream-ordered RCCL barrier and with the flag barrier (a world of
+        # one: the own buffer and flag word only)
+        for pb in ("collective", "flags"):
+            pdec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="peer", halo=None, peer_barrier=pb)
+            pdec.start(pats, "cuda")
+            for step in range(6):
+                tok = [F[a + 3 + step] if rng.random() < 0.8 else -1 for a in starts]
+                got = pdec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
+                assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), (pb, step)
+            assert pdec._peer.errors() == 0
+            pdec.close()
         occ = full.occurring_distinct
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         ref = mk(full)
