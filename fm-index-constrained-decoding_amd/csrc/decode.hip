@@ -526,6 +526,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
           lf_step_decode<true>(v, t + shift, l, h, tbm, one, content, &cmask);
         }
         if (l >= h) follow = -1;
+        // the payload ships a C-block narrower than a bitmap as its slice, not as its follow bitmap
+        if (PAY && h - l < (vocab + 31) / 32) follow = -1;
         FM_STAMP(v, 2);
       }
     }

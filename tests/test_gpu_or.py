@@ -229,7 +229,10 @@ def test_decode_payload_equals_packed_decode_and_unsharded(dev, V):
             assert torch.equal(lo2, plo) and torch.equal(hi2, phi), (step, r)
             desc = bufs[r][4:4 + B].cpu().numpy().view(np.uint32)
             w = (np.minimum(hi2.cpu().numpy(), ix.size()) - lo2.cpu().numpy()).clip(min=0)
-            np.testing.assert_array_equal((desc >> 31) == 0, w < W)     # streamed narrow rows ship their slice
+            sparse = (desc >> 31) == 0          # a row ships its slice only when narrower than a bitmap
+            assert np.all(w[sparse] < W) and np.array_equal(desc[sparse], w[sparse]), (step, r)
+            assert np.all(desc[~sparse] == (W | 0x80000000)), (step, r)
+            assert sparse[w < min(W, 64)].all(), (step, r)      # narrow streamed rows never write a bitmap
             new_states.append((lo2, hi2))
         states = new_states
         fm = torch.empty((B, V), dtype=torch.uint8, device=dev)
