@@ -878,6 +878,9 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
                 "payload_decode_states_equal": all(s["payload_decode_states_equal"] for s in shards),
                 "barrier_us_assumed": 15.0, "remote_read_model_us": remote_us,
                 "predicted_step_us": slow_pd + 15.0 + remote_us + pp_cold,
+                # the flag barrier instead of the all_reduce: one xGMI store + the poll that sees it
+                "flag_barrier_us_assumed": 3.0,
+                "predicted_step_us_flags": slow_pd + 3.0 + remote_us + pp_cold,
                 "note": "the decode kernel writes each shard's payload (fixed row slots, no pack pass) into "
                         "IPC-mapped buffers read in place (fm_shard_or_rows_peers): no sizes exchange, no "
                         "gather; here over local buffers"}
@@ -1450,7 +1453,8 @@ def main():
                 log(f"c4 on one GPU: slowest shard {c4['slowest_shard_cold_us']:.1f}us cold, OR "
                     f"{c4['or_pass_cold_us']:.1f}us, exact {c4['masks_equal_unsharded']}, predicted 8-GPU step "
                     f"{c4['predicted_step_us']['direct']:.0f}-{c4['predicted_step_us']['ring']:.0f}us (dense), "
-                    f"{c4['peer_exchange']['predicted_step_us']:.0f}us (peer, OR pass "
+                    f"{c4['peer_exchange']['predicted_step_us']:.0f}us (peer; "
+                    f"{c4['peer_exchange']['predicted_step_us_flags']:.0f}us with the flag barrier; OR pass "
                     f"{c4['peer_exchange']['or_rows_peers_cold_us']:.1f}us, exact "
                     f"{c4['peer_exchange']['masks_equal_unsharded']})")
         except Exception as e:  # the replica line must still print
