@@ -538,6 +538,8 @@ class PeerExchange:
         self.device = torch.device(device)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if self.world > 64:
+            raise ValueError("PeerExchange: at most 64 ranks (the OR pass stages one part per lane of a wave)")
         self.rows = capacity_rows
         self.cap = payload_capacity(capacity_rows, vocab)
         self.bufs = [torch.zeros(self.cap, dtype=torch.int32, device=self.device) for _ in range(2)]
