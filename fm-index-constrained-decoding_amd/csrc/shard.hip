@@ -364,7 +364,12 @@ constexpr uint32_t kFlagSpins = 1u << 20;   // flag polls before a step is given
 constexpr int kOrSym0 = 4;   // 16-B symbol loads per thread issued with the dense words (16 K symbols)
 constexpr int kOrSymU = 8;   // per later round (32 K symbols)
 
-template <bool PEERS>
+// PP (per part): a sparse list is loaded through a workgroup-uniform buffer resource over that
+// part's list (16-B loads, 4096 symbols per part and round; past the list's end the descriptor's
+// range check returns zeros without a memory request), the (part, round) pairs eight at a time,
+// instead of over one flat index space searched per load.  In PEERS mode these are 16-B
+// system-scope loads where the flat space needs pairs of 8-B ones.
+template <bool PEERS, bool PP>
 __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts,
                                                             const uint64_t* __restrict__ ptrs, uint32_t nparts,
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
@@ -376,7 +381,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   // flat space of every sparse list padded to a multiple of 4 words
   __shared__ uint32_t s_cnt[kOrMaxParts], s_off[kOrMaxParts], s_pre[kOrMaxParts + 1], s_dense[kOrMaxParts];
   __shared__ uint64_t s_base[PEERS ? kOrMaxParts : 1];
-  __shared__ uint32_t s_nd;
+  __shared__ uint32_t s_nd, s_nq;
   const uint64_t b = blockIdx.x;
   const uint32_t t = threadIdx.x;
   auto base_of = [&](uint32_t p) -> const uint32_t* {
@@ -429,9 +434,13 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
       if constexpr (PEERS) s_base[t] = reinterpret_cast<uint64_t>(pp);
     }
     const uint32_t tot = __shfl(inc, (int)(nparts - 1), 64);
+    uint32_t mq = q;                                    // the longest list, in 16-B quads
+#pragma unroll
+    for (int k = 32; k; k >>= 1) mq = max(mq, (uint32_t)__shfl_xor(mq, k, 64));
     if (t == 0) {
       s_pre[nparts] = tot;
       s_nd = (uint32_t)__popcll(dm);
+      s_nq = (mq + kOrRowThreads - 1) / kOrRowThreads;
     }
   }
   or_lds_barrier();
@@ -454,13 +463,39 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
         atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
     }
   };
-  // the first 16 K sparse symbols, loaded with the first dense round
-  uint4 sq0[kOrSym0];
-  uint32_t sp0[kOrSym0];
+  // PP: (part, round) pair j = k * nparts + p covers quads [k * 1024, (k + 1) * 1024) of part p's list
+  const uint32_t npairs = nparts * s_nq;
+  auto pair_load = [&](uint32_t j) -> or_v4u {
+    const uint32_t k = j / nparts, p = j - k * nparts;
+    const uint32_t bytes = j < npairs ? 4u * ((s_cnt[p] + 3u) & ~3u) : 0u;   // dense parts: 0, no request
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base_of(p) + s_off[p], bytes);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (t + k * kOrRowThreads), 0, PEERS ? kSysLoadAux : 0);
+  };
+  auto pair_set = [&](uint32_t j, const or_v4u& x) {
+    if (j >= npairs) return;                             // workgroup-uniform
+    const uint32_t k = j / nparts, p = j - k * nparts;
+    const uint32_t i0 = 4 * (t + k * kOrRowThreads), cnt = s_cnt[p];
 #pragma unroll
-  for (int u = 0; u < kOrSym0; ++u) {
-    sp0[u] = 0;
-    sq0[u] = total4 ? quad_at(min(u * kOrRowThreads + t, total4 - 1), sp0[u]) : make_uint4(0, 0, 0, 0);
+    for (int e = 0; e < 4; ++e) {
+      const int64_t tok = (int64_t)x[e] - shift;
+      if (i0 + e < cnt && tok >= 0 && (uint64_t)tok < vocab) atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
+    }
+  };
+  constexpr int kPP = 8;                                 // (part, round) pairs per round trip
+  or_v4u pq0[PP ? kPP : 1];
+  if constexpr (PP) {
+#pragma unroll
+    for (int u = 0; u < kPP; ++u) pq0[u] = pair_load((uint32_t)u);
+  }
+  // flat space: the first 16 K sparse symbols, loaded with the first dense round
+  uint4 sq0[PP ? 1 : kOrSym0];
+  uint32_t sp0[PP ? 1 : kOrSym0];
+  if constexpr (!PP) {
+#pragma unroll
+    for (int u = 0; u < kOrSym0; ++u) {
+      sp0[u] = 0;
+      sq0[u] = total4 ? quad_at(min(u * kOrRowThreads + t, total4 - 1), sp0[u]) : make_uint4(0, 0, 0, 0);
+    }
   }
   constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);   // W <= 8192 words
   const uint32_t slots = (W4 + kOrRowThreads - 1) / kOrRowThreads;
@@ -514,15 +549,27 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   // the dense words are in place before any symbol's bit is ORed in (other waves' words may
   // share a symbol's word)
   or_lds_barrier();
+  if constexpr (PP) {
 #pragma unroll
-  for (int u = 0; u < kOrSym0; ++u) set_quad(u * kOrRowThreads + t, sp0[u], sq0[u]);
-  for (uint32_t j0 = kOrSym0 * kOrRowThreads; j0 < total4; j0 += kOrSymU * kOrRowThreads) {   // long lists
-    uint4 sq[kOrSymU];
-    uint32_t sp[kOrSymU];
+    for (int u = 0; u < kPP; ++u) pair_set((uint32_t)u, pq0[u]);
+    for (uint32_t j0 = kPP; j0 < npairs; j0 += kPP) {   // more parts, or lists past 4096 symbols
+      or_v4u pq[kPP];
 #pragma unroll
-    for (int u = 0; u < kOrSymU; ++u) sq[u] = quad_at(min(j0 + u * kOrRowThreads + t, total4 - 1), sp[u]);
+      for (int u = 0; u < kPP; ++u) pq[u] = pair_load(j0 + (uint32_t)u);
 #pragma unroll
-    for (int u = 0; u < kOrSymU; ++u) set_quad(j0 + u * kOrRowThreads + t, sp[u], sq[u]);
+      for (int u = 0; u < kPP; ++u) pair_set(j0 + (uint32_t)u, pq[u]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kOrSym0; ++u) set_quad(u * kOrRowThreads + t, sp0[u], sq0[u]);
+    for (uint32_t j0 = kOrSym0 * kOrRowThreads; j0 < total4; j0 += kOrSymU * kOrRowThreads) {   // long lists
+      uint4 sq[kOrSymU];
+      uint32_t sp[kOrSymU];
+#pragma unroll
+      for (int u = 0; u < kOrSymU; ++u) sq[u] = quad_at(min(j0 + u * kOrRowThreads + t, total4 - 1), sp[u]);
+#pragma unroll
+      for (int u = 0; u < kOrSymU; ++u) set_quad(j0 + u * kOrRowThreads + t, sp[u], sq[u]);
+    }
   }
   or_lds_barrier();
   if (!unpack) {
@@ -550,6 +597,13 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
 }
 
 }  // namespace
+
+// FMIDX_OR_PERPART=0|1 (read per launch): the OR pass's sparse lists per part (1, the default)
+// or over one flat index space (0)
+static bool or_per_part() {
+  const char* e = std::getenv("FMIDX_OR_PERPART");
+  return !(e && *e && std::atoi(e) == 0);
+}
 
 uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab) {
   const uint64_t W = (vocab + 31) / 32;
@@ -592,9 +646,12 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
     set_error("shard_or_rows: the payloads must start on 16-B boundaries (stride a multiple of 4 words)");
     return -1;
   }
-  k_or_rows<false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(parts, nullptr, (uint32_t)nparts, stride, B,
-                                                                        (uint32_t)W, vocab, shift, out, ld, unpack,
-                                                                        nullptr, 0, nullptr);
+  if (or_per_part())
+    k_or_rows<false, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, 0, nullptr);
+  else
+    k_or_rows<false, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, 0, nullptr);
   FM_HIP(hipGetLastError());
   return 0;
 }
@@ -616,9 +673,12 @@ int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t c
     set_error("shard_or_rows_peers: a flag barrier needs an error word");
     return -1;
   }
-  k_or_rows<true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(nullptr, ptrs, (uint32_t)nparts, cap, B,
-                                                                       (uint32_t)W, vocab, shift, out, ld, unpack,
-                                                                       flags, want, err);
+  if (or_per_part())
+    k_or_rows<true, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, want, err);
+  else
+    k_or_rows<true, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, want, err);
   FM_HIP(hipGetLastError());
   return 0;
 }
