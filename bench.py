@@ -350,8 +350,12 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
         np.cumsum([len(p) for p in pats], out=offs[1:])
         flat_by_step[s] = (np.fromiter((t for p in pats for t in p), dtype=np.int64), offs)
 
-    def one_step(mode, s, lo, hi, mask, threads):
-        if mode == "incremental":
+    dist_in_leg = []   # the incremental single-thread leg's own distinct_count time, per repetition
+
+    def one_step(mode, s, lo, hi, mask, threads, acc=None):
+        if mode == "incremental" and acc is not None:
+            acc[0] += ref.decode_step_timed(np.ascontiguousarray(tok_np[s]), SHIFT, 0, lo, hi, mask)
+        elif mode == "incremental":
             ref.decode_step(np.ascontiguousarray(tok_np[s]), SHIFT, 0, lo, hi, mask, threads)
         else:
             flat, offs = flat_by_step[s]
@@ -379,10 +383,13 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
             lo, hi, mask, lo_w, hi_w, rates = state[key]
             lo[:] = lo_w
             hi[:] = hi_w
+            acc = [0.0] if key == ("incremental", 1) else None
             a = time.perf_counter()
             for s in range(first, last + 1):
-                one_step(key[0], s, lo, hi, mask, key[1])
+                one_step(key[0], s, lo, hi, mask, key[1], acc)
             rates.append(window * B / (time.perf_counter() - a))
+            if acc is not None:
+                dist_in_leg.append((acc[0] / window, B / rates[-1]))
         a = time.perf_counter()
         for s in range(first, last + 1):
             ref.distinct_only(lo_all[s], hi_all[s], 1)
@@ -404,7 +411,11 @@ def cpu_baseline(fm, bwt, tokens, lo_hist, hi_hist, pats0, V, warmup, window, re
             f"{reps} x {window} steps; ranges ok {ok}, masks ok {mok}")
     per_step = {"distinct_count_only": float(np.median(dts)),
                 "incremental": B / legs["incremental_1"]["value"],
-                "full_research": B / legs["full_research_1"]["value"]}
+                "full_research": B / legs["full_research_1"]["value"],
+                # measured inside the incremental single-thread leg's own steps (a part of the same run,
+                # per repetition): it cannot exceed that leg's step
+                "distinct_count_in_incremental": float(np.median([d for d, _ in dist_in_leg])),
+                "distinct_count_share_of_incremental": float(np.median([d / w for d, w in dist_in_leg]))}
     log(f"cpu 1-thread seconds per step: {per_step}")
     head = legs["incremental_all"]
     return {"value": head["value"], "unit": "masks/s", "cores": all_cores, "kind": "port",

@@ -26,6 +26,7 @@
 // Only tests/ and bench.py's cpu_baseline leg load this library.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <thread>
@@ -296,9 +297,22 @@ uint64_t cr_distinct_count(void* p, uint64_t low, uint64_t high, uint64_t* out, 
 
 // One incremental decode step for m rows: LF step (token < reset_below ->
 // full range), then distinct_count of the new range, then the uint8 mask row.
+// distinct_seconds (single thread only, may be null): += the time spent in distinct_count, measured
+// inside the same step -- the bench's breakdown of a single-thread step, a part of the same run.
+void cr_decode_step_timed(void* p, const int64_t* tok, int64_t shift, int64_t reset_below, uint64_t* lo,
+                          uint64_t* hi, uint64_t m, uint8_t* mask, uint64_t vocab, int threads,
+                          double* distinct_seconds);
+
 void cr_decode_step(void* p, const int64_t* tok, int64_t shift, int64_t reset_below, uint64_t* lo,
                     uint64_t* hi, uint64_t m, uint8_t* mask, uint64_t vocab, int threads) {
+  cr_decode_step_timed(p, tok, shift, reset_below, lo, hi, m, mask, vocab, threads, nullptr);
+}
+
+void cr_decode_step_timed(void* p, const int64_t* tok, int64_t shift, int64_t reset_below, uint64_t* lo,
+                          uint64_t* hi, uint64_t m, uint8_t* mask, uint64_t vocab, int threads,
+                          double* distinct_seconds) {
   const CpuRef& h = *static_cast<CpuRef*>(p);
+  const bool timed = distinct_seconds && threads <= 1;
   parallel_rows(m, threads, [&](uint64_t i, std::vector<uint64_t>& buf) {
     uint64_t l = lo[i], r = hi[i];
     if (tok[i] < reset_below) {
@@ -319,7 +333,9 @@ void cr_decode_step(void* p, const int64_t* tok, int64_t shift, int64_t reset_be
     }
     lo[i] = l;
     hi[i] = r;
+    const auto t0 = timed ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
     const uint64_t k = h.distinct_count(l, r, buf);
+    if (timed) *distinct_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     uint8_t* row = mask + i * vocab;
     std::memset(row, 0, vocab);
     for (uint64_t q = 0; q < k; ++q) {

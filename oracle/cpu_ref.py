@@ -30,6 +30,8 @@ def lib():
         d.cr_decode_step.argtypes = [c_void_p, POINTER(c_int64), c_int64, c_int64, u64p, u64p, c_uint64,
                                      POINTER(ctypes.c_uint8), c_uint64, c_int]
         d.cr_distinct_only.argtypes = [c_void_p, u64p, u64p, c_uint64, c_int]
+        d.cr_decode_step_timed.argtypes = [c_void_p, POINTER(c_int64), c_int64, c_int64, u64p, u64p, c_uint64,
+                                           POINTER(ctypes.c_uint8), c_uint64, c_int, POINTER(ctypes.c_double)]
         d.cr_full_step.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64), c_int64, c_uint64, u64p, u64p,
                                    POINTER(ctypes.c_uint8), c_uint64, c_int, c_int]
         _lib = d
@@ -118,6 +120,14 @@ class CpuRef:
                     mask: np.ndarray, threads: int):
         lib().cr_decode_step(self._h, _p(tok, c_int64), shift, reset_below, _p(lo), _p(hi), lo.size,
                              _p(mask, ctypes.c_uint8), mask.shape[1], threads)
+
+    def decode_step_timed(self, tok: np.ndarray, shift: int, reset_below: int, lo: np.ndarray, hi: np.ndarray,
+                          mask: np.ndarray) -> float:
+        """decode_step on one thread; returns the seconds its distinct_count calls took."""
+        t = ctypes.c_double(0.0)
+        lib().cr_decode_step_timed(self._h, _p(tok, c_int64), shift, reset_below, _p(lo), _p(hi), lo.size,
+                                   _p(mask, ctypes.c_uint8), mask.shape[1], 1, ctypes.byref(t))
+        return t.value
 
     def distinct_only(self, lo: np.ndarray, hi: np.ndarray, threads: int = 1):
         """distinct_count of every (lo[i], hi[i]) with the results discarded."""

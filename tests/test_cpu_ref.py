@@ -58,3 +58,13 @@ def test_cpu_ref_decode_and_full_step():
             exp.append(ora.backward_search_step(t + 10, l, h - 1))
     assert list(zip(lo.tolist(), hi.tolist())) == exp
     assert np.array_equal(mask, allowed_mask(ora, [e[0] for e in exp], [e[1] for e in exp], V))
+    # the timed single-thread step (the bench's in-leg distinct_count breakdown): same results, and
+    # the distinct_count time it reports is a part of its own wall time
+    lo2, hi2 = np.array([w[0] for w in want], dtype=np.uint64), np.array([w[1] for w in want], dtype=np.uint64)
+    mask2 = np.zeros_like(mask)
+    import time
+    a = time.perf_counter()
+    t_dist = ref.decode_step_timed(nxt, 10, 0, lo2, hi2, mask2)
+    wall = time.perf_counter() - a
+    assert np.array_equal(lo2, lo) and np.array_equal(hi2, hi) and np.array_equal(mask2, mask)
+    assert 0.0 < t_dist <= wall
