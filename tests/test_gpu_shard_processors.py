@@ -221,7 +221,14 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
                 got = pdec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
                 assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), (pb, step)
             assert pdec._peer.errors() == 0
+            # a larger batch on the same decoder: the exchange is rebuilt with room for it
+            pats2 = [F[a:a + 2] for a in rng.integers(0, len(F) - 40, size=3 * B)]
+            pdec.start(pats2, "cuda")
+            got = pdec.step(torch.tensor([F[0]] * (3 * B), dtype=torch.int64, device="cuda"))
+            assert pdec._peer.rows >= 3 * B
+            assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), pb
             pdec.close()
+            assert pdec._peer is None
         occ = full.occurring_distinct
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         ref = mk(full)
