@@ -424,27 +424,6 @@ def payload_capacity(B: int, vocab: int) -> int:
     return _cap(B, vocab)
 
 
-def gather_payloads(payload, group):
-    """all_gather of every rank's sparse-exchange payload: the sizes first
-    (one int64 per rank, read on the host), then each rank's first
-    max(size) words -> (int32 [world, max], [words per rank])."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    used = payload[:1].to(torch.int64)
-    sizes = torch.empty(world, dtype=torch.int64, device=payload.device)
-    dist.all_gather_into_tensor(sizes, used, group=group)
-    words = [int(x) for x in sizes.tolist()]
-    m = max(words)
-    mine = payload[:m]
-    if mine.numel() < m:                  # a host payload is exactly its size
-        mine = torch.cat([mine, torch.zeros(m - mine.numel(), dtype=mine.dtype, device=mine.device)])
-    parts = torch.empty(world * m, dtype=torch.int32, device=payload.device)
-    dist.all_gather_into_tensor(parts, mine.contiguous(), group=group)
-    return parts.view(world, m), words
-
-
 class SparseExchange:
     """The sparse exchange of one rank, per step: all_gather of the payload
     sizes, all_gather of the payloads, the OR pass.  The payload all_gather
@@ -805,5 +784,5 @@ def unpack_bits(packed, vocab: int):
 
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
            "ShardedIndex",
-           "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "gather_payloads", "or_payloads", "SparseExchange",
-           "pack_payload_host", "or_payloads_host"]
+           "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "or_payloads", "SparseExchange",
+           "PeerExchange", "or_peer_payloads", "pack_payload_host", "or_payloads_host"]
