@@ -69,6 +69,29 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpus(env: dict | None = None, topology: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process could use, counted WITHOUT the HIP runtime (the
+    launcher parent must not initialise the GPU: torch.cuda.device_count() asks
+    amdsmi first but falls back to a HIP runtime call): the KFD topology nodes
+    with a nonzero gpu_id, limited by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES
+    / CUDA_VISIBLE_DEVICES when set (an empty list hides every GPU)."""
+    import glob
+
+    env = os.environ if env is None else env
+    n = 0
+    for path in glob.glob(os.path.join(topology, "*", "gpu_id")):
+        try:
+            with open(path) as f:
+                n += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if var in env:
+            ids = [x for x in env[var].split(",") if x.strip()]
+            n = min(n, len(ids))
+    return n
+
+
 def spawn_ranks(n: int, cmd: list, grace_s: float = 30.0, env: dict | None = None) -> int:
     """One fresh child process per GPU running ``cmd`` with the torchrun-style
     rank environment; returns the worst exit code.  The caller must not have
@@ -450,30 +473,35 @@ def shard_trace(fm, text, bwt, B, V, S, dev):
     return tokens, pats0, ref
 
 
-def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, halo=128):
+def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, halo=128):
     """Doc-range sharded decode, measured after the
-    replica run at N > 1.  The trace (tokens + initial patterns) and the
-    reference masks of its last step come from the replica (unsharded) index;
-    then every rank indexes its doc range + halo (one slice of T', built on the
-    device) and decodes all B rows against it into bit-packed rows.  A step is
-    the fused LF + packed mask (fm_decode_step_batch), then the exchange:
+    replica run at N > 1.  The traces (tokens + initial patterns, one per
+    global batch size in ``shs``: the metric's B = 256 and the PAQ eval shape's
+    2048 rows) and the reference masks of their last step come from the replica
+    (unsharded) index; then every rank indexes its doc range + halo (one slice
+    of T', built on the device, once) and decodes all B rows against it.  A
+    step is the fused LF + mask, then the exchange:
     "dense" -- RCCL all_gather of every row's packed bitmap and fm_or_bits;
     "sparse" -- fm_shard_pack (per row the shard's BWT slice when smaller than
     the bitmap, else the bitmap), an all_gather of the payload sizes (read on
     the host), an all_gather of the payloads and ONE fused OR / scatter /
-    unpack pass (fm_shard_or_rows); "peer" -- the same payloads packed into
-    IPC-mapped buffers, a one-element RCCL all_reduce as the stream-ordered
-    barrier, and the OR pass reading every rank's payload in place over xGMI
-    (fm_shard_or_rows_peers).  Each is timed over the same K steps and the
-    last step's mask of each must equal the replica's; ``value`` is the
-    fastest exact one.  FMIDX_BENCH_PEER=0 leaves the peer mode out."""
+    unpack pass (fm_shard_or_rows); "peer" -- the decode kernel writes the
+    payload into IPC-mapped buffers, a one-element RCCL all_reduce as the
+    stream-ordered barrier, and the OR pass reading every rank's payload in
+    place over xGMI (fm_shard_or_rows_peers); "peer_flags" -- the same with
+    the flag barrier (device step counter, fm_peer_signal + the polling OR
+    pass): no collective in the step; "peer_flags_graph" -- that step captured
+    ONCE into a HIP graph and replayed K times (each replay after a copy of
+    the step's tokens into the graph's static input), the serving loop's form.
+    Each mode is timed over the same K steps and its last step's mask must
+    equal the replica's; ``value`` is the fastest exact mode at B = 256.
+    FMIDX_BENCH_PEER=0 leaves the peer modes out."""
     import torch.distributed as dist
 
     from fmidx.sharding import PeerExchange, SparseExchange, or_bits, shard_text_device
 
     fm, bwt = holder.pop(), holder.pop()      # the replica index and its BWT (the caller keeps no reference)
     S = W + K
-    tokens, pats0, ref = sh                   # shard_trace: the same rows on every rank
     del bwt, fm
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -495,24 +523,12 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
     dist.all_reduce(ok_all, op=dist.ReduceOp.MIN)
     if not int(ok_all.item()):
         raise RuntimeError(f"shard build failed on some rank ({err or 'another rank'})")
-    lens = [len(p) for p in pats0]
-    assert max(lens) + S <= halo - 1, "trace patterns would outgrow the halo"
-    offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
-    toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
-    lo0 = torch.zeros(B, dtype=torch.int64, device=dev)
-    hi0 = torch.zeros(B, dtype=torch.int64, device=dev)
-    ix.backward_search_batch(toks, offs, SHIFT, lo0, hi0)
+    Bmax = max(shs)
     Wd = (V + 31) // 32
-    mine = torch.empty((B, Wd), dtype=torch.int32, device=dev)
-    parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
-    out = torch.empty((B, V), dtype=torch.uint8, device=dev)
-    payload = None
-    words_seen = []
-    xchg = SparseExchange(None)
     peer, peer_err = None, ""
     if os.environ.get("FMIDX_BENCH_PEER", "1") != "0":
         try:
-            peer = PeerExchange(None, B, V, dev)
+            peer = PeerExchange(None, Bmax, V, dev, barrier="collective")
         except Exception as e:   # every rank learns of it below
             peer_err = repr(e)
         ok_all = torch.tensor([0 if peer_err else 1], device=dev)
@@ -522,118 +538,153 @@ def sharded_leg(holder, text_seed, n_tokens, V, B, K, W, world, rank, dev, sh, h
                 peer.close()
             peer, peer_err = None, peer_err or "the peer mapping failed on another rank"
 
-    def run(mode):
-        nonlocal payload
-        lo, hi = lo0.clone(), hi0.clone()
-        bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+    def one_batch(B, tokens, pats0, ref):
+        lens = [len(p) for p in pats0]
+        assert max(lens) + S <= halo - 1, "trace patterns would outgrow the halo"
+        offs = torch.tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64), device=dev)
+        toks = torch.tensor([t for p in pats0 for t in p], dtype=torch.int64, device=dev)
+        lo0 = torch.zeros(B, dtype=torch.int64, device=dev)
+        hi0 = torch.zeros(B, dtype=torch.int64, device=dev)
+        ix.backward_search_batch(toks, offs, SHIFT, lo0, hi0)
+        mine = torch.empty((B, Wd), dtype=torch.int32, device=dev)
+        parts = torch.empty((world, B, Wd), dtype=torch.int32, device=dev)
+        out = torch.empty((B, V), dtype=torch.uint8, device=dev)
+        payload = None
+        words_seen = []
+        xchg = SparseExchange(None)
 
-        def step(i):
+        def run(mode):
             nonlocal payload
-            src, dst = bufs[i % 2], bufs[(i + 1) % 2]
-            if mode in ("peer", "peer_flags", "peer_flags_graph"):   # the decode kernel writes the payload itself
-                pay = peer.payload()
-                ix.decode_step_payload(tokens[i], src[0], src[1], dst[0], dst[1], pay, V, SHIFT, reset_below=0)
-                peer(pay, B, V, SHIFT, out=out)
-                return
-            ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0], hi_out=dst[1],
-                           packed=True)
-            if mode == "dense":
-                dist.all_gather_into_tensor(parts, mine)
-                or_bits(parts, V, out=out)
-            else:
-                payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
-                xchg(payload, B, V, SHIFT, out=out)
-                if i >= W:
-                    words_seen.append(xchg.words[-1])
+            lo, hi = lo0.clone(), hi0.clone()
+            bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+            flags = mode in ("peer_flags", "peer_flags_graph")
+            tok_static = torch.empty_like(tokens[0])
 
-        for i in range(W):
-            step(i)
-        g = None
-        if mode == "peer_flags_graph":
-            # no collective in the step (flag words over xGMI): the K timed steps are captured in one
-            # graph, replayed once (their step numbers are baked into the captured launches)
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for i in range(W, S):
-                    step(i)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        a_ev = torch.cuda.Event(enable_timing=True)
-        b_ev = torch.cuda.Event(enable_timing=True)
-        a_ev.record()
-        if g is not None:
-            g.replay()
-        else:
-            for i in range(W, S):
+            def step(i, tok=None):
+                nonlocal payload
+                src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+                if flags:            # state in place, the buffer and the step number on the device
+                    peer.flags_step(ix, tokens[i] if tok is None else tok, lo, hi, V, SHIFT, out)
+                    return
+                if mode == "peer":   # the decode kernel writes the payload itself
+                    pay = peer.payload()
+                    ix.decode_step_payload(tokens[i], src[0], src[1], dst[0], dst[1], pay, V, SHIFT, reset_below=0)
+                    peer(pay, B, V, SHIFT, out=out)
+                    return
+                ix.decode_step(tokens[i], src[0], src[1], mine, V, SHIFT, reset_below=0, lo_out=dst[0],
+                               hi_out=dst[1], packed=True)
+                if mode == "dense":
+                    dist.all_gather_into_tensor(parts, mine)
+                    or_bits(parts, V, out=out)
+                else:
+                    payload = ix.shard_pack(dst[0], dst[1], mine, V, payload=payload)
+                    xchg(payload, B, V, SHIFT, out=out)
+                    if i >= W:
+                        words_seen.append(xchg.words[-1])
+
+            peer_mode = mode in ("peer", "peer_flags", "peer_flags_graph")
+            if peer_mode:
+                peer.barrier_mode = "flags" if flags else "collective"
+            for i in range(W):
                 step(i)
-        b_ev.record()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t = torch.tensor([a_ev.elapsed_time(b_ev) / K], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ok = torch.tensor([1 if bool(torch.equal(out, ref)) else 0], device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        return float(t.item()), bool(ok.item())
+            g = None
+            if mode == "peer_flags_graph":
+                # ONE step captured (no collective in it: the flag words over xGMI, the step number
+                # on the device), replayed for every timed step after its tokens are copied in
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    step(W, tok_static)
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            a_ev = torch.cuda.Event(enable_timing=True)
+            b_ev = torch.cuda.Event(enable_timing=True)
+            a_ev.record()
+            for i in range(W, S):
+                if g is not None:
+                    tok_static.copy_(tokens[i])
+                    g.replay()
+                else:
+                    step(i)
+            b_ev.record()
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t = torch.tensor([a_ev.elapsed_time(b_ev) / K], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            exact = bool(torch.equal(out, ref))
+            timeouts = 0
+            if flags:
+                timeouts = peer.errors()
+            ok = torch.tensor([1 if exact and not timeouts else 0], device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            return float(t.item()), bool(ok.item()), timeouts
 
-    ms_dense, exact_dense = run("dense")
-    ms_sparse, exact_sparse = run("sparse")
-    per_step = [sum(w) for w in words_seen]
-    modes = {
-        "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
-                  "exchange_bytes_per_step": world * B * Wd * 4,
-                  "step": "RCCL all_gather of the packed rows + fm_or_bits"},
-        "sparse": {"ms_per_step": ms_sparse, "value": B / (ms_sparse / 1e3), "masks_equal_unsharded": exact_sparse,
-                   "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
-                   "speculative_gathers_respecified": xchg.respecified,
-                   "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
-                                                       if words_seen else None),
-                   "step": "fm_shard_pack, all_gather of sizes (host read) + payloads, fm_shard_or_rows"},
-    }
+        ms_dense, exact_dense, _ = run("dense")
+        ms_sparse, exact_sparse, _ = run("sparse")
+        per_step = [sum(w) for w in words_seen]
+        modes = {
+            "dense": {"ms_per_step": ms_dense, "value": B / (ms_dense / 1e3), "masks_equal_unsharded": exact_dense,
+                      "exchange_bytes_per_step": world * B * Wd * 4,
+                      "step": "RCCL all_gather of the packed rows + fm_or_bits"},
+            "sparse": {"ms_per_step": ms_sparse, "value": B / (ms_sparse / 1e3),
+                       "masks_equal_unsharded": exact_sparse,
+                       "exchange_bytes_per_step_median": 4.0 * float(np.median(per_step)) if per_step else None,
+                       "speculative_gathers_respecified": xchg.respecified,
+                       "allgather_bytes_per_step_median": (4.0 * world * float(np.median([max(w) for w in words_seen]))
+                                                           if words_seen else None),
+                       "step": "fm_shard_pack, all_gather of sizes (host read) + payloads, fm_shard_or_rows"},
+        }
+        if peer is not None:
+            ms_peer, exact_peer, _ = run("peer")
+            modes["peer"] = {"ms_per_step": ms_peer, "value": B / (ms_peer / 1e3), "masks_equal_unsharded": exact_peer,
+                             "exchange_bytes_per_step_median": modes["sparse"]["exchange_bytes_per_step_median"],
+                             "step": "fm_decode_step_payload (the decode kernel writes the payload, fixed row "
+                                     "slots) into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
+                                     "fm_shard_or_rows_peers reading every rank's payload over xGMI"}
+            ms_pf, exact_pf, to_pf = run("peer_flags")
+            modes["peer_flags"] = {"ms_per_step": ms_pf, "value": B / (ms_pf / 1e3),
+                                   "masks_equal_unsharded": exact_pf, "flag_timeouts": to_pf,
+                                   "step": "as peer, with the flag barrier: fm_peer_signal (the device step counter "
+                                           "advanced, a system-scope release, stores into every rank's flag array) "
+                                           "+ fm_shard_or_rows_peers_wait; state updated in place; eager launches"}
+            try:
+                ms_pg, exact_pg, to_pg = run("peer_flags_graph")
+                modes["peer_flags_graph"] = {"ms_per_step": ms_pg, "value": B / (ms_pg / 1e3),
+                                             "masks_equal_unsharded": exact_pg, "flag_timeouts": to_pg,
+                                             "step": "peer_flags captured ONCE as a one-step HIP graph, replayed K "
+                                                     "times (tokens copied into its static input before each "
+                                                     "replay): the per-token serving loop"}
+            except Exception as e:   # capture refused: the eager figures stand
+                modes["peer_flags_graph"] = {"value": None, "error": repr(e)}
+        else:
+            modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
+        exact_modes = [m for m, r in modes.items() if r.get("masks_equal_unsharded")]
+        best = min(exact_modes, key=lambda m: modes[m]["ms_per_step"]) if exact_modes else "sparse"
+        return {"value": modes[best]["value"], "ms_per_step": modes[best]["ms_per_step"], "global_batch": B,
+                "masks_equal_unsharded": bool(exact_modes) and modes[best]["masks_equal_unsharded"],
+                "exchange": best, "modes": modes}
+
+    by_batch = {}
+    for B in sorted(shs):
+        tokens, pats0, ref = shs[B]
+        by_batch[B] = one_batch(B, tokens, pats0, ref)
+        log(f"sharded B={B}: {by_batch[B]['value'] / 1e6:.2f} M masks/s ({by_batch[B]['exchange']}, "
+            f"{by_batch[B]['ms_per_step'] * 1e3:.1f} us/step), exact {by_batch[B]['masks_equal_unsharded']}")
     if peer is not None:
-        ms_peer, exact_peer = run("peer")
-        modes["peer"] = {"ms_per_step": ms_peer, "value": B / (ms_peer / 1e3), "masks_equal_unsharded": exact_peer,
-                         "exchange_bytes_per_step_median": modes["sparse"]["exchange_bytes_per_step_median"],
-                         "step": "fm_decode_step_payload (the decode kernel writes the payload, fixed row slots) "
-                                 "into IPC-mapped buffers, 1-element RCCL all_reduce (barrier), "
-                                 "fm_shard_or_rows_peers reading every rank's payload over xGMI"}
-        peer.barrier_mode = "flags"     # the same buffers, no collective: flag words over xGMI
-        ms_pf, exact_pf = run("peer_flags")
-        t_err = torch.tensor([peer.errors()], device=dev)
-        dist.all_reduce(t_err, op=dist.ReduceOp.MAX)
-        modes["peer_flags"] = {"ms_per_step": ms_pf, "value": B / (ms_pf / 1e3),
-                               "masks_equal_unsharded": exact_pf and not int(t_err.item()),
-                               "flag_timeouts_last_step": int(t_err.item()),
-                               "step": "as peer, with the barrier as flag words: fm_peer_signal (system-scope "
-                                       "stores into every rank's flag array) + fm_shard_or_rows_peers_wait"}
-        try:
-            ms_pg, exact_pg = run("peer_flags_graph")
-            t_err = torch.tensor([peer.errors()], device=dev)
-            dist.all_reduce(t_err, op=dist.ReduceOp.MAX)
-            modes["peer_flags_graph"] = {"ms_per_step": ms_pg, "value": B / (ms_pg / 1e3),
-                                         "masks_equal_unsharded": exact_pg and not int(t_err.item()),
-                                         "flag_timeouts_last_step": int(t_err.item()),
-                                         "step": "peer_flags with the K steps captured in one HIP graph (no "
-                                                 "collective inside), replayed once"}
-        except Exception as e:   # capture refused: the eager figures stand
-            modes["peer_flags_graph"] = {"value": None, "error": repr(e)}
         peer.close()
-    else:
-        modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
-    exact_modes = [m for m, r in modes.items() if r.get("masks_equal_unsharded")]
-    best = min(exact_modes, key=lambda m: modes[m]["ms_per_step"]) if exact_modes else "sparse"
+    head = by_batch[256] if 256 in by_batch else by_batch[min(by_batch)]
     st = ix.stats()
-    return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": modes[best]["value"],
-            "unit": "masks/s", "ms_per_step": modes[best]["ms_per_step"], "scaling": "strong", "shards": world,
-            "halo": halo, "global_batch": B, "shard_docs": [int(a), int(b)], "shard_rows": ix.size(),
-            "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
-            "masks_equal_unsharded": bool(exact_modes) and modes[best]["masks_equal_unsharded"],
-            "exchange": best, "modes": modes,
+    return {"metric": "allowed-token masks/sec (doc-range sharded, C4)", "value": head["value"],
+            "unit": "masks/s", "ms_per_step": head["ms_per_step"], "scaling": "strong", "shards": world,
+            "halo": halo, "global_batch": head["global_batch"], "shard_docs": [int(a), int(b)],
+            "shard_rows": ix.size(), "shard_device_bytes": st["device_bytes"], "shard_build_s": build_s,
+            "masks_equal_unsharded": head["masks_equal_unsharded"], "exchange": head["exchange"],
+            "modes": head["modes"], "by_global_batch": {str(k): v for k, v in by_batch.items()},
             "payload": "per row the shard's BWT slice (hi - lo < ceil(V/32)) or its packed bitmap",
-            "step": "fused LF + packed mask, then the exchange of 'exchange' (modes: each timed over the same K "
-                    "steps), uint8 [B, V] out; eager launches"}
+            "step": "fused LF + mask, then the exchange of 'exchange' (modes: each timed over the same K steps), "
+                    "uint8 [B, V] out"}
 
 
 COMPACT_ENV = {"FMIDX_TRANS": "1", "FMIDX_LF_E": "0", "FMIDX_PROBE_FIRST": "0"}
@@ -959,6 +1010,8 @@ def main():
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the doc-range sharded leg")
     ap.add_argument("--sharded-at-1", action="store_true",
                     help="run the sharded leg at N = 1 too (one shard; exercises the path on a one-GPU box)")
+    ap.add_argument("--sharded-batches", default="2048",
+                    help="global batch sizes the sharded leg runs besides --batch (comma list; '' = none)")
     ap.add_argument("--no-c4", action="store_true",
                     help="N = 1: skip the one-GPU rehearsal of the 8-way doc-range sharded config (C4)")
     ap.add_argument("--packed", action="store_true",
@@ -974,8 +1027,8 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # plain `python bench.py --gpus N`: this process only launches the ranks and never
-        # touches the GPU (device_count does not initialise it on this image)
-        ndev = torch.cuda.device_count()
+        # touches the GPU -- the devices are counted from the KFD topology, not through torch.cuda
+        ndev = visible_gpus()
         if ndev < args.gpus:
             print(f"[bench] --gpus {args.gpus} but only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
             sys.exit(2)
@@ -1034,6 +1087,13 @@ def main():
     want_sharded = (world > 1 and not args.no_sharded) or args.sharded_at_1
     want_c4 = world == 1 and not args.no_c4 and not args.sharded_at_1 and n > 2e9 and args.corpus == "markov"
     sh = shard_trace(fm, text, bwt, B, V, S, dev) if (want_sharded or want_c4) else None
+    # the sharded leg also at the PAQ eval shape's row count (the exchange amortised over more rows)
+    shs = None
+    if want_sharded:
+        shs = {B: sh}
+        for b2 in (int(x) for x in args.sharded_batches.split(",") if x.strip()):
+            if b2 not in shs:
+                shs[b2] = shard_trace(fm, text, bwt, b2, V, S, dev)
     del text
     torch.cuda.empty_cache()
     PK = bool(args.packed)
@@ -1465,7 +1525,7 @@ def main():
         del bwt, fm
         torch.cuda.empty_cache()
         try:
-            result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, B, K, W, world, rank, dev, sh)
+            result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, K, W, world, rank, dev, shs)
             log(f"sharded: {result['sharded']['value'] / 1e6:.2f} M masks/s, "
                 f"{result['sharded']['ms_per_step'] * 1e3:.1f} us/step, exact {result['sharded']['masks_equal_unsharded']}")
         except Exception as e:  # the replica line must still print

@@ -1040,12 +1040,14 @@ int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, in
 
 int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
                            const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
-                           uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab, void* stream) {
+                           uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab,
+                           uint32_t* d_payload_alt, const uint32_t* d_step, void* stream) {
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   return fmidx::launch_decode_payload(h->idx.view, d_tokens, shift, reset_below, d_lo_in, d_hi_in, d_lo_out, d_hi_out,
-                                      m, d_payload, cap_words, vocab, reinterpret_cast<hipStream_t>(stream));
+                                      m, d_payload, cap_words, vocab, d_payload_alt, d_step,
+                                      reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 
@@ -1293,26 +1295,49 @@ int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_
                            uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
   FM_API_BEGIN
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
-                                           nullptr, 0, nullptr, reinterpret_cast<hipStream_t>(stream));
+                                           nullptr, nullptr, 0, nullptr, reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 
 int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
-                                const uint32_t* d_flags, uint32_t step, uint32_t* d_err, void* stream) {
+                                const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,
+                                void* stream) {
   FM_API_BEGIN
   if (!d_flags) {
     set_error("shard_or_rows_peers_wait: null flags");
     return -1;
   }
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
-                                           d_flags, step, d_err, reinterpret_cast<hipStream_t>(stream));
+                                           d_flags, d_step, spins, err, reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 
-int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t step, void* stream) {
+int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_step, void* stream) {
   FM_API_BEGIN
-  return fmidx::launch_peer_signal(d_flag_ptrs, world, step, reinterpret_cast<hipStream_t>(stream));
+  return fmidx::launch_peer_signal(d_flag_ptrs, world, d_step, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_host_mapped_alloc(uint64_t bytes, void** out) {
+  FM_API_BEGIN
+  if (!out || !bytes) {
+    set_error("host_mapped_alloc: null output or zero bytes");
+    return -1;
+  }
+  *out = nullptr;
+  // coherent (fine-grained) mapped host memory: a kernel's system-scope store lands in host
+  // memory, where the host reads it without a copy or a synchronisation
+  FM_HIP(hipHostMalloc(out, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(*out, 0, bytes);
+  return 0;
+  FM_API_END
+}
+
+int fm_host_mapped_free(void* p) {
+  FM_API_BEGIN
+  if (p) FM_HIP(hipHostFree(p));
+  return 0;
   FM_API_END
 }
 

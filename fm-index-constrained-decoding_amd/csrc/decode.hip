@@ -57,9 +57,9 @@ constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
 // symbols before the slice (128-bit aligned) and ends 64 after it
 __host__ __device__ constexpr uint32_t win_words(uint64_t sw) { return (uint32_t)(sw / 32 + 16); }
 constexpr uint64_t kEarlyZeroWidth = 64;      // rows this narrow get their zeros written up front
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
 constexpr uint32_t kPayMagic = 0x58534D46u;    // the shard payload's magic (csrc/shard.hip)
-constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144                    // uint4 loads in flight per thread while streaming
+constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release/acquire, which on gfx950 also drains every wave's outstanding
@@ -382,7 +382,9 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
                                                        uint64_t early_width, DevView v,
-                                                       uint32_t* __restrict__ pay) {
+                                                       uint32_t* __restrict__ pay,
+                                                       uint32_t* __restrict__ pay_alt,
+                                                       const uint32_t* __restrict__ pay_sel) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
   // zero-filling waves -- from thread 256, 512 or 768 -- measured the same)
@@ -422,7 +424,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   const uint64_t t1 = min(vocab, t0 + SW);
   const uint64_t ntok = t1 - t0;
   const uint64_t nch = (ntok + CH - 1) / CH;
-  uint8_t* out_row = mask + row * ld;
   // Rows whose incoming range is narrow stay narrow after the LF step (it
   // can only shrink a range), so their slice is zero-filled right away --
   // the stores overlap the LF chain -- and the final pass rewrites only the
@@ -442,6 +443,15 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                        in_hi - in_lo <= kScanMax && !(in_lo == 0 && in_hi == v.n) &&
                        (in_hi - in_lo < v.cache_min || !v.trans_cap);
   FM_PRELOAD_VIEW(v);   // after the state loads are in flight (see above)
+  if constexpr (PAY) {
+    // the peer exchange's double buffer picked by the device step counter's parity (a
+    // captured step replays for every step); only the stores at the end depend on it
+    if (pay_sel && (__hip_atomic_load(pay_sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) {
+      mask = reinterpret_cast<uint8_t*>(pay_alt) + (reinterpret_cast<uint8_t*>(mask) - reinterpret_cast<uint8_t*>(pay));
+      pay = pay_alt;
+    }
+  }
+  uint8_t* out_row = mask + row * ld;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
   // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
   const __amdgpu_buffer_rsrc_t orsrc =
@@ -917,7 +927,7 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   const size_t lds = (size_t)win_words(SW) * 4;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v, nullptr)
+                                        mask, ld, ew, v, nullptr, nullptr, nullptr)
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
@@ -942,11 +952,13 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
 
 int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                           const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
-                          uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, hipStream_t s) {
+                          uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, uint32_t* pay_alt,
+                          const uint32_t* pay_sel, hipStream_t s) {
   if (m == 0) return 0;
   const uint64_t W = (vocab + 31) / 32, W4 = (W + 3) & ~3ull, H = 4 + ((2 * m + 3) & ~3ull);
   if (!pay || !tok || !lo_in || !hi_in || !lo_out || !hi_out || vocab == 0 || W > kPayMaxWords ||
-      m >= (1ull << 31) || (reinterpret_cast<uintptr_t>(pay) & 15)) {
+      m >= (1ull << 31) || (reinterpret_cast<uintptr_t>(pay) & 15) || (pay_sel && !pay_alt) ||
+      (reinterpret_cast<uintptr_t>(pay_alt) & 15)) {
     set_error("decode payload: bad arguments (vocab %llu <= 262144, 16-B aligned payload)",
               (unsigned long long)vocab);
     return -1;
@@ -956,8 +968,12 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
               (unsigned long long)(H + m * W4));
     return -1;
   }
-  if (lo_in == lo_out || hi_in == hi_out) {
-    set_error("fused decode step: state in/out buffers must not alias (ping-pong them)");
+  // the state may be updated in place here (one workgroup per row: its one store follows every
+  // read of the row's state behind the workgroup's barriers), so a captured step replays as is;
+  // partial overlap is still refused
+  if ((lo_in != lo_out && lo_in < lo_out + m && lo_out < lo_in + m) ||
+      (hi_in != hi_out && hi_in < hi_out + m && hi_out < hi_in + m)) {
+    set_error("decode payload: state in/out buffers overlap without being the same buffer");
     return -1;
   }
   const uint32_t T = decode_threads(m);
@@ -968,13 +984,13 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
   const uint64_t ld = W4 * 4;
   if (T == 1024)
     k_decode<true, true, 1024, true><<<g, 1024, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                          reset_below, mask, ld, 0, v, pay);
+                                                          reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
   else if (T == 512)
     k_decode<true, true, 512, true><<<g, 512, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay);
+                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
   else
     k_decode<true, true, 256, true><<<g, 256, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay);
+                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -721,7 +721,8 @@ int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t r
 // the same step writing the shard exchange's payload with fixed row slots (PeerExchange)
 int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                           const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
-                          uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, hipStream_t s);
+                          uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, uint32_t* pay_alt,
+                          const uint32_t* pay_sel, hipStream_t s);
 int launch_cache_probe(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m, uint8_t* out,
                        hipStream_t s);
 int launch_follow_bitmaps(const DevView& v, const uint64_t* C, uint64_t nsym, uint32_t* out,
@@ -743,8 +744,8 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
                          int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s);
 int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
                                int64_t shift, void* out, uint64_t ld, int unpack, const uint32_t* flags,
-                               uint32_t want, uint32_t* err, hipStream_t s);
-int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t value, hipStream_t s);
+                               const uint32_t* ctr, uint32_t spins, uint32_t* err, hipStream_t s);
+int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t* ctr, hipStream_t s);
 int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t wpr,
                    uint64_t vocab, void* out, uint64_t ld_out, int unpack, hipStream_t s);
 

@@ -359,7 +359,7 @@ __device__ __forceinline__ uint4 part_quad(const uint32_t* base, uint64_t i) {
   }
 }
 
-constexpr uint32_t kFlagSpins = 1u << 20;   // flag polls before a step is given up (~0.1-1 s)
+constexpr uint32_t kFlagSpins = 1u << 20;   // default flag polls before a step is given up (~0.1-1 s)
 
 constexpr int kOrSym0 = 4;   // 16-B symbol loads per thread issued with the dense words (16 K symbols)
 constexpr int kOrSymU = 8;   // per later round (32 K symbols)
@@ -375,7 +375,8 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
                                                             int unpack, const uint32_t* __restrict__ flags,
-                                                            uint32_t want, uint32_t* __restrict__ err) {
+                                                            const uint32_t* __restrict__ ctr, uint32_t spins,
+                                                            uint32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
   // per part: its sparse count (0 for dense parts), data offset, and first 16-B slot in the
   // flat space of every sparse list padded to a multiple of 4 words
@@ -391,18 +392,28 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   const uint32_t W4 = (W + 3) / 4;
   for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
   if (t < 64) {
+    const uint64_t* tab = ptrs;
     if (PEERS && flags) {
       // the device-side barrier (PeerExchange "flags"): every rank has stored this step's number
       // into its word of this rank's flag array once its payload was complete (k_peer_signal,
-      // after the kernel that wrote it).  Wave 0 waits for all of them (system-scope loads: the
-      // words are written over xGMI), bounded: past kFlagSpins polls the step is marked failed
-      // in *err and the pass goes on, so the grid always drains.
+      // after the kernel that wrote it).  The step number is this rank's device counter, which
+      // its own signal kernel advanced just before this pass (stream order), so one captured
+      // step replays for every step; its parity picks the payload buffer the step wrote
+      // (ptrs = buffer 0's addresses, then buffer 1's).  Wave 0 waits for all of them
+      // (system-scope loads: the words are written over xGMI), bounded: past `spins` polls the
+      // step is recorded in *err (host-visible: a system-scope store) and the pass goes on, so
+      // the grid always drains -- the host raises on the recorded step.
+      const uint32_t want = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tab = ptrs + ((want - 1u) & 1u) * nparts;
       bool ok = t >= nparts;
-      for (uint32_t it = 0; it < kFlagSpins && !__all(ok); ++it) {
+      for (uint32_t it = 0; it < spins && !__all(ok); ++it) {
         if (!ok) ok = (int32_t)(__hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - want) >= 0;
         if (!__all(ok)) __builtin_amdgcn_s_sleep(4);
       }
-      if (!__all(ok) && t == 0) __hip_atomic_store(err, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!__all(ok) && t == 0) __hip_atomic_store(err, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // acquire: the peers' payload stores, released before their flag stores (k_peer_signal),
+      // are visible to every load below (they are system-scope loads as well)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     // wave 0 stages every part's (desc, off) and scans them in registers (nparts <= 64).  A row
     // whose data lies past the part's end (a gather shorter than the payload: the speculative
@@ -411,7 +422,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     uint32_t d = 0, o = 0;
     const uint32_t* pp = nullptr;
     if (t < nparts) {
-      pp = PEERS ? reinterpret_cast<const uint32_t*>(ptrs[t]) : parts + (uint64_t)t * stride;
+      pp = PEERS ? reinterpret_cast<const uint32_t*>(tab[t]) : parts + (uint64_t)t * stride;
       d = part_word<PEERS>(pp, 4 + b);
       o = part_word<PEERS>(pp, 4 + B + b);
       const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
@@ -648,17 +659,17 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
   }
   if (or_per_part())
     k_or_rows<false, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, 0, nullptr);
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr);
   else
     k_or_rows<false, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, 0, nullptr);
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr);
   FM_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
                                int64_t shift, void* out, uint64_t ld, int unpack, const uint32_t* flags,
-                               uint32_t want, uint32_t* err, hipStream_t s) {
+                               const uint32_t* ctr, uint32_t spins, uint32_t* err, hipStream_t s) {
   const uint64_t W = (vocab + 31) / 32;
   if (!ptrs || !out || !nparts || nparts > (uint64_t)kOrMaxParts || W > (uint64_t)kOrRowMaxWords ||
       cap < shard_payload_capacity(B, vocab) || cap >= (1ull << 30) ||
@@ -669,37 +680,45 @@ int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t c
     return -1;
   }
   if (B == 0) return 0;
-  if (flags && !err) {
-    set_error("shard_or_rows_peers: a flag barrier needs an error word");
+  if (flags && (!err || !ctr)) {
+    set_error("shard_or_rows_peers: a flag barrier needs a step counter and an error word");
     return -1;
   }
+  if (!spins) spins = kFlagSpins;
   if (or_per_part())
     k_or_rows<true, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, want, err);
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err);
   else
     k_or_rows<true, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, want, err);
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err);
   FM_HIP(hipGetLastError());
   return 0;
 }
 
 namespace {
-// the flag barrier's signal: lane r stores `value` into rank r's flag word for this rank (an
-// address in rank r's memory, mapped over xGMI) with a system-scope (sc0 sc1) vector store
+// the flag barrier's signal: the step number is this rank's device counter plus one (the
+// counter advances here, so a captured step replays for every step); after a system-scope
+// release -- the payload the previous kernel on this stream wrote is visible at system scope
+// before any flag says so -- lane r stores it into rank r's flag word for this rank (an address
+// in rank r's memory, mapped over xGMI) with a system-scope (sc0 sc1) vector store.  world = 0
+// advances the counter and posts nothing (the timeout path's tests).
 __global__ void __launch_bounds__(64) k_peer_signal(const uint64_t* __restrict__ dst, uint32_t world,
-                                                    uint32_t value) {
+                                                    uint32_t* __restrict__ ctr) {
   const uint32_t t = threadIdx.x;
+  const uint32_t value = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (t < world)
     __hip_atomic_store(reinterpret_cast<uint32_t*>(dst[t]), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) __hip_atomic_store(ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 }  // namespace
 
-int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t value, hipStream_t s) {
-  if (!dst || world == 0 || world > 64) {
-    set_error("peer_signal: 1..64 flag addresses");
+int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t* ctr, hipStream_t s) {
+  if (!ctr || (world && !dst) || world > 64) {
+    set_error("peer_signal: 0..64 flag addresses and a step counter");
     return -1;
   }
-  k_peer_signal<<<1, 64, 0, s>>>(dst, (uint32_t)world, value);
+  k_peer_signal<<<1, 64, 0, s>>>(dst, (uint32_t)world, ctr);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -66,16 +66,19 @@ SIGNATURES = {
     "fm_processor_call": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "fm_shard_payload_capacity": (c_int, [c_uint64, c_uint64, u64p]),
     "fm_decode_step_payload": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p]),
+                                       c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p,
+                                       c_void_p]),
     "fm_shard_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p,
                               c_uint64, c_void_p]),
     "fm_shard_or_rows": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p, c_uint64,
                                  c_int, c_void_p]),
     "fm_shard_or_rows_peers": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
                                        c_uint64, c_int, c_void_p]),
-    "fm_peer_signal": (c_int, [c_void_p, c_uint64, c_uint32, c_void_p]),
+    "fm_peer_signal": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p]),
     "fm_shard_or_rows_peers_wait": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
-                                            c_uint64, c_int, c_void_p, c_uint32, c_void_p, c_void_p]),
+                                            c_uint64, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+    "fm_host_mapped_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
+    "fm_host_mapped_free": (c_int, [c_void_p]),
     "fm_ipc_handle": (c_int, [c_void_p, c_void_p, u64p]),
     "fm_ipc_open": (c_int, [c_void_p, POINTER(c_void_p)]),
     "fm_ipc_close": (c_int, [c_void_p]),

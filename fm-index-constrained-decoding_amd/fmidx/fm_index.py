@@ -354,16 +354,25 @@ class FMIndex:
         return mask
 
     def decode_step_payload(self, tokens, lo, hi, lo_out, hi_out, payload, vocab: int, shift: int,
-                            reset_below: int = -(1 << 63)):
+                            reset_below: int = -(1 << 63), payload_alt=None, step=None):
         """The fused LF step writing the shard exchange's payload with fixed row
         slots (fm_decode_step_payload): per row the BWT slice of its new range
         when narrower than ceil(vocab/32) words and streamed whole, else its
         packed bitmap -- what PeerExchange's readers take in place, no pack
-        pass.  ``payload``: int32, >= payload_capacity(B, vocab) words."""
+        pass.  ``payload``: int32, >= payload_capacity(B, vocab) words.  The
+        state may be updated in place (lo_out is lo).  ``step`` (the flag
+        barrier's device counter, int32 [1]) with ``payload_alt``: the kernel
+        writes ``payload`` on an even counter and ``payload_alt`` on an odd one."""
+        if (step is None) != (payload_alt is None):
+            raise ValueError("decode_step_payload: payload_alt and step go together")
+        if payload_alt is not None and payload_alt.numel() < payload.numel():
+            raise ValueError("decode_step_payload: payload_alt smaller than payload")
         check(lib().fm_decode_step_payload(self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below),
                                            c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()),
                                            c_void_p(lo_out.data_ptr()), c_void_p(hi_out.data_ptr()), lo.numel(),
                                            c_void_p(payload.data_ptr()), payload.numel(), int(vocab),
+                                           c_void_p(payload_alt.data_ptr()) if payload_alt is not None else None,
+                                           c_void_p(step.data_ptr()) if step is not None else None,
                                            c_void_p(_stream_of(lo))), "decode_step_payload")
         return payload
 
@@ -376,7 +385,7 @@ class FMIndex:
         import torch
 
         B = lo.numel()
-        if payload is None:
+        if payload is None or payload.numel() < payload_capacity(B, vocab):   # the batch may have grown
             payload = torch.empty(payload_capacity(B, vocab), dtype=torch.int32, device=lo.device)
         check(lib().fm_shard_pack(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), B,
                                   c_void_p(bits.data_ptr()), bits.stride(0), int(vocab), c_void_p(payload.data_ptr()),

@@ -371,7 +371,8 @@ class _ShardedDeviceStep(_DeviceStep):
     def finish(self, h, facts_sum, bits_or):
         """The decisions from the summed facts and the epilogue with the ORed
         bits (int32 [B, >= ceil(V/32)]); None when the call needs the host
-        path (end markers, boost overflow) -- not available over a shard."""
+        path (end markers, boost overflow), which the processor then runs over
+        the shards (the same decision on every rank: it depends on the inputs)."""
         from .sharding import HaloExceeded
 
         a = self._args
@@ -386,8 +387,12 @@ class _ShardedDeviceStep(_DeviceStep):
                                               c_void_p(bits_or.data_ptr()), bits_or.stride(0),
                                               c_void_p(stream.cuda_stream)), "processor_shard_finish")
         self._ev.synchronize()
+        # the exchange's OR pass ran before this event: a timed-out flag barrier is seen here
+        self.sidx.check_exchange()
         st = self._status_np
         if st[0] != 0 or st[1] != st[2]:
+            # rows without exactly one end marker / a boost outside the float range: the
+            # processor's host path runs next, over the shards (ShardedIndex's sharded forms)
             self._prev_ok = False
             return None
         halo = self.sidx.halo
@@ -422,8 +427,13 @@ class _BatchedCore:
     def counts(self, patterns: Sequence[Sequence[int]]) -> List[int]:
         if not patterns:
             return []
+        sharded = getattr(self.index, "sharded", False)
+        if sharded:
+            self.index.check_patterns(patterns)
         lo, hi = self.index.get_range_batch(patterns, SHIFT)
-        return (hi.astype(np.int64) - lo.astype(np.int64)).tolist()
+        c = (hi.astype(np.int64) - lo.astype(np.int64)).tolist()
+        # a doc-sharded index: summed over the ranks (zero exactly when the unsharded count is)
+        return self.index.sum_counts(c) if sharded else c
 
     def ranges(self, patterns: Sequence[Sequence[int]]):
         """get_range of every pattern (index.py:103-114), incrementally: during
@@ -436,6 +446,8 @@ class _BatchedCore:
             self._prev = {}
             z = np.zeros(0, dtype=np.uint64)
             return z, z
+        if getattr(self.index, "sharded", False):
+            self.index.check_patterns(patterns)
         n = self.index.size()
         keys = [tuple(map(int, p)) for p in patterns]
         toks, slo, shi = [], np.zeros(len(keys), dtype=np.uint64), np.zeros(len(keys), dtype=np.uint64)

@@ -33,6 +33,7 @@ them in place (fm_shard_or_rows_peers) -- no host read of sizes, no gather.
 from __future__ import annotations
 
 import bisect
+import ctypes
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -117,20 +118,31 @@ class ShardedDecoder:
     """
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8",
-                 halo: Optional[int] = None, peer_barrier: str = "collective"):
+                 halo: Optional[int] = None, peer_barrier: str = "flags", graph: bool = False,
+                 spins: Optional[int] = None):
         """reduce: "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
         (all_gather of the packed rows + fm_or_bits), "sparse" (BWT slices /
         bitmaps per row, fm_shard_pack + all_gather + fm_shard_or_rows) or
         "peer" (the same payloads read in place over xGMI: PeerExchange, whose
-        ``barrier`` is ``peer_barrier``)."""
+        ``barrier`` is ``peer_barrier``, with at most ``spins`` flag polls).
+        ``graph`` (peer + flags): the step -- the payload decode, the signal,
+        the OR pass -- is captured into ONE HIP graph at its first call and
+        replayed for every later step (the tokens copied into its static
+        input); the step number and the buffer parity live on the device."""
         self.index = index
         self.vocab = vocab
         self.shift = shift
         self.group = group
         if reduce not in ("max_u8", "gather_bits", "sparse", "peer"):
             raise ValueError(reduce)
+        if graph and not (reduce == "peer" and peer_barrier == "flags"):
+            raise ValueError("graph: only the peer exchange with the flag barrier holds no collective")
         self.reduce = reduce
         self.peer_barrier = peer_barrier
+        self.graph = graph
+        self.spins = spins
+        self._g = None         # the captured step (graph=True) and its static token input
+        self._g_tok = None
         self._peer = None      # its PeerExchange (reduce="peer")
         self.halo = halo
         self.fused = hasattr(index, "decode_step")
@@ -169,6 +181,7 @@ class ShardedDecoder:
         self.lo = torch.tensor(lo.astype(np.int64), device=device)
         self.hi = torch.tensor(hi.astype(np.int64), device=device)
         self._buf = None
+        self._g = None         # the captured step names the old state buffers
         return self.mask()
 
     def step(self, tokens):
@@ -213,13 +226,41 @@ class ShardedDecoder:
     def _step_peer(self, tokens):
         """The peer exchange's step: the decode kernel writes this rank's payload
         itself (fixed row slots, fm_decode_step_payload: no pack pass), then the
-        barrier and the in-place OR of every rank's payload."""
+        barrier and the in-place OR of every rank's payload.  With the flag
+        barrier the state is updated in place and the payload buffer picked by
+        the device counter, so the same launches serve every step (graph)."""
         import torch
 
         B = self.lo.numel()
         if self._peer is None or self._peer.rows < B:
             self.close()
-            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier)
+            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier,
+                                      spins=self.spins)
+            self._g = None
+        self._peer.check()                 # a timed-out step before this one: raise, return no mask
+        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != self.lo.device:
+            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=self.lo.device)
+            self._g = None
+        if self.peer_barrier == "flags":
+            px = self._peer
+
+            def launch(tok):
+                px.flags_step(self.index, tok, self.lo, self.hi, self.vocab, self.shift, self._out)
+
+            if not self.graph:
+                launch(tokens)
+            else:
+                if self._g is None:
+                    self._g_tok = torch.empty_like(tokens)
+                    torch.cuda.synchronize(self.lo.device)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        launch(self._g_tok)
+                    self._g = g
+                self._g_tok.copy_(tokens)
+                self._g.replay()
+            px.step += 1
+            return self._out
         if self._buf is None:              # start() resets it: fresh second state buffers
             self._lo2 = torch.empty_like(self.lo)
             self._hi2 = torch.empty_like(self.hi)
@@ -229,8 +270,6 @@ class ShardedDecoder:
                                        reset_below=0)
         self.lo, self._lo2 = self._lo2, self.lo
         self.hi, self._hi2 = self._hi2, self.hi
-        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
-            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=pay.device)
         return self._peer(pay, B, self.vocab, self.shift, out=self._out)
 
     def _combine_peer(self, bits):
@@ -239,7 +278,9 @@ class ShardedDecoder:
         B = self.lo.numel()
         if self._peer is None or self._peer.rows < B:
             self.close()
-            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier)
+            self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier,
+                                      spins=self.spins)
+        self._peer.check()
         pay = self._peer.payload()
         self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=pay)
         if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
@@ -247,10 +288,12 @@ class ShardedDecoder:
         return self._peer(pay, B, self.vocab, self.shift, out=self._out)
 
     def close(self):
-        """Release the peer exchange's mappings (collective: every rank calls it)."""
+        """Release the peer exchange's mappings (collective: every rank calls it);
+        raises PeerBarrierTimeout if one of its steps timed out."""
+        self._g = None
         if self._peer is not None:
-            self._peer.close()
-            self._peer = None
+            px, self._peer = self._peer, None
+            px.close()
 
     def _combine_sparse(self, bits):
         """The sparse exchange of this step's rows (new state self.lo/hi,
@@ -324,17 +367,29 @@ class ShardedIndex:
     shard's BWT slice or bitmap, all_gathered), "peer" (the same payloads read
     in place over xGMI, PeerExchange; the facts all_reduce, issued after the
     pack, is its barrier) or "dense" (every row's bitmap).  A pattern
-    longer than ``halo`` - 1 tokens raises HaloExceeded; stop_at_count must
-    be 0 (counts include halo duplicates), and inputs that need the host path
-    (rows without exactly one end marker, boost overflow) raise.  The
-    ``index.py`` query surface (get_range, distinct, ...) is the unsharded
-    index's business and is not offered here."""
+    longer than ``halo`` - 1 tokens raises HaloExceeded and stop_at_count must
+    be 0 (counts include halo duplicates).  Inputs the device path hands to the
+    processors' host path (rows without exactly one end marker, boosts outside
+    the float range) run it over the shards: the host path's index calls
+    become this class's sharded forms -- ``get_range_batch`` /
+    ``allowed_mask`` on the shard, ``sum_counts`` (count([last]) summed over
+    the ranks: zero exactly when the unsharded count is zero) and the allowed
+    bits ORed over the ranks -- so such a call returns the unsharded host
+    path's output, or raises where the reference raises.  Every rank makes the
+    same calls in the same order (they depend on the inputs, not the shard).
+    The default exchange is the fastest exact one: "peer" with the flag barrier
+    (no collective per exchange; a timed-out barrier raises
+    PeerBarrierTimeout).  The ``index.py`` query surface (get_range, distinct,
+    ...) is the unsharded index's business and is not offered here."""
 
-    def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "sparse",
-                 shift: int = 10, peer_barrier: str = "collective"):
+    sharded = True
+
+    def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "peer",
+                 shift: int = 10, peer_barrier: str = "flags", spins: Optional[int] = None):
         if exchange not in ("sparse", "dense", "peer"):
             raise ValueError(exchange)
         self.peer_barrier = peer_barrier
+        self.spins = spins
         self._peer = None
         self._staged = False
         self.shard = shard
@@ -367,16 +422,25 @@ class ShardedIndex:
         B = lo.numel()
         if self._peer is None or self._peer.rows < B or self._peer.vocab != vocab:
             self.close()
-            self._peer = PeerExchange(self.group, B, vocab, lo.device, barrier=self.peer_barrier)
+            self._peer = PeerExchange(self.group, B, vocab, lo.device, barrier=self.peer_barrier, spins=self.spins)
+        self._peer.check()
         self.shard.shard_pack(lo, hi, bits, vocab, payload=self._peer.payload())
         self._staged = True
         return self.peer_barrier == "collective"
 
-    def close(self):
-        """Release the peer exchange's mappings (collective: every rank calls it)."""
+    def check_exchange(self):
+        """Raise PeerBarrierTimeout if a peer-exchange step has timed out (no
+        synchronisation: a host read; the processors call it after the wait
+        they make anyway)."""
         if self._peer is not None:
-            self._peer.close()
-            self._peer = None
+            self._peer.check()
+
+    def close(self):
+        """Release the peer exchange's mappings (collective: every rank calls it);
+        raises PeerBarrierTimeout if one of its steps timed out."""
+        if self._peer is not None:
+            px, self._peer = self._peer, None
+            px.close()
 
     def or_bits(self, lo, hi, bits, vocab: int, staged: bool = False):
         """OR of every rank's packed allowed bits (int32 [B, W]) -> int32 [B, W].
@@ -406,15 +470,60 @@ class ShardedIndex:
         dist.all_gather_into_tensor(self._parts, mine, group=self.group)
         return or_bits(self._parts, vocab, unpack=False)
 
-    def _no_host_path(self, *a, **k):
-        raise NotImplementedError("this call needs the processors' host path (a row without exactly one end "
-                                  "marker, or a boost outside the float range), which a doc-sharded index cannot run")
+    # ---- the processors' host path over the shards (see the class docstring)
+    def check_patterns(self, patterns):
+        """HaloExceeded if a pattern is longer than the halo allows."""
+        if self.halo is None or not patterns:
+            return
+        longest = max(len(p) for p in patterns)
+        if longest > self.halo - 1:
+            raise HaloExceeded(f"a pattern of {longest} tokens needs a halo of >= {longest + 1}; the shards were "
+                               f"built with {self.halo}")
 
-    get_range_batch = _no_host_path
-    allowed_mask = _no_host_path
+    def get_range_batch(self, patterns, shift: int = 10, starts=None):
+        """get_range of every pattern on this rank's SHARD (shard-local (lo, hi):
+        only its emptiness and the allowed bits it yields are global facts)."""
+        return self.shard.get_range_batch(patterns, shift, starts=starts)
+
+    def sum_counts(self, counts):
+        """Per-pattern counts summed over the ranks (all_reduce SUM): zero exactly
+        when the unsharded count is zero (halo duplicates inflate the rest)."""
+        if self.group is None or not len(counts):
+            return list(counts)
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=torch.device("cuda", self.device))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t.tolist()
+
+    def allowed_mask(self, lo, hi, vocab: int, shift: int, out=None, packed: bool = False):
+        """The allowed tokens of the shard-local ranges (lo, hi), ORed over the
+        ranks -> int32 [B, ceil(V/32)] words (packed) or uint8 [B, V]: the
+        unsharded index's mask of the same patterns."""
+        bits = self.shard.allowed_mask(lo, hi, vocab, shift, packed=True)
+        words = self.or_bits(lo, hi, bits, vocab)
+        if packed:
+            if out is not None:
+                out.copy_(words)
+                return out
+            return words
+        import torch
+
+        W = (vocab + 31) // 32
+        u8 = unpack_bits(words[:, :W].contiguous().view(torch.uint8), vocab)
+        if out is not None:
+            out.copy_(u8)
+            return out
+        return u8
 
     def size(self) -> int:
         return self.shard.size()
+
+
+def payload_header_words(B: int) -> int:
+    """Words of a payload's header (csrc/shard.hip: 4 + 2B rounded to 4)."""
+    return 4 + ((2 * B + 3) & ~3)
 
 
 def payload_capacity(B: int, vocab: int) -> int:
@@ -440,7 +549,8 @@ class SparseExchange:
         self.group = group
         self.slack = slack
         self.history = history
-        self._max = []          # largest payload (words) of the recent steps
+        self._max = []          # largest payload (words) of the recent steps (of this batch size)
+        self._B = None
         self.words = []         # words every rank shipped, per step
         self.respecified = 0    # steps whose speculative size was too small
 
@@ -465,9 +575,13 @@ class SparseExchange:
         sizes = torch.empty(world, dtype=torch.int64, device=payload.device)
         dist.all_gather_into_tensor(sizes, used, group=self.group)
         guess = 0
+        if B != self._B:                      # sizes of another batch size say nothing about this one
+            self._max, self._B = [], B
         if self._max:
             # the same value on every rank (the sizes were gathered), never above a payload's capacity
-            guess = min(payload_capacity(B, vocab), (int(max(self._max) * self.slack) + 3) & ~3)
+            # nor below its header
+            guess = min(payload_capacity(B, vocab),
+                        max(payload_header_words(B), (int(max(self._max) * self.slack) + 3) & ~3))
             res = or_payloads(self._gather(payload, guess), B, vocab, shift, out=out, unpack=unpack)
         words = [int(x) for x in sizes.tolist()]
         m = max(words)
@@ -478,6 +592,15 @@ class SparseExchange:
         if guess:
             self.respecified += 1
         return or_payloads(self._gather(payload, m), B, vocab, shift, out=out, unpack=unpack)
+
+
+class PeerBarrierTimeout(RuntimeError):
+    """The flag barrier of a peer exchange timed out: some rank did not post
+    its payload within the spin bound, so the OR pass of that step read
+    payloads that may be stale or half-written.  Masks must be exact or
+    absent: every later call of the exchange raises this too (the step's
+    output was already returned -- the error is read without a per-step
+    synchronisation, at the next call and at close())."""
 
 
 class PeerExchange:
@@ -492,19 +615,25 @@ class PeerExchange:
     pack (RCCL runs it after the rank's pack and completes it only when every
     rank's has run, so the OR that follows on the stream sees every payload;
     the processors pass ``barrier_done`` when their facts all_reduce, issued
-    after the pack, already is one); "flags" -- no collective at all: after
-    its pack every rank stores the step number into its word of every rank's
-    flag array (fm_peer_signal, system-scope stores over xGMI) and the OR pass
-    first waits for all of its own words (fm_shard_or_rows_peers_wait,
-    bounded: a step that times out is recorded in ``errors()``); "host" --
-    synchronize + group barrier (gloo; ranks sharing a GPU, where RCCL
-    refuses to run).  Two buffers are
-    enough: a rank packs buffer k again two steps later, after a barrier that
-    every rank entered only after its OR of buffer k had been issued before it
-    on its stream.  ``capacity_rows``: the largest batch the buffers hold
-    (payload_capacity words each)."""
+    after the pack, already is one); "flags" (the default) -- no collective at
+    all: after its pack every rank advances its device step counter and stores
+    the new value into its word of every rank's flag array (fm_peer_signal,
+    a system-scope release, then system-scope stores over xGMI) and the OR pass
+    first waits for all of its own words (fm_shard_or_rows_peers_wait, then a
+    system-scope acquire).  The step number and the buffer parity live on the
+    device, so a step (decode + signal + OR) captured once into a HIP graph
+    replays for every decode step.  The wait is bounded by ``spins`` polls
+    (None: the library's 2^20, ~0.1-1 s); a step that times out is recorded in
+    an error word in coherent host memory and the NEXT call (or close())
+    raises PeerBarrierTimeout -- no per-step synchronisation; "host" --
+    synchronize + group barrier (gloo; ranks sharing a GPU, where RCCL refuses
+    to run).  Two buffers are enough: a rank packs buffer k again two steps
+    later, after a barrier that every rank entered only after its OR of buffer
+    k had been issued before it on its stream.  ``capacity_rows``: the largest
+    batch the buffers hold (payload_capacity words each)."""
 
-    def __init__(self, group, capacity_rows: int, vocab: int, device, barrier: str = "collective"):
+    def __init__(self, group, capacity_rows: int, vocab: int, device, barrier: str = "flags",
+                 spins: Optional[int] = None):
         import torch
         import torch.distributed as dist
         from ctypes import byref, c_uint8, c_uint64, c_void_p
@@ -514,6 +643,9 @@ class PeerExchange:
         if barrier not in ("collective", "host", "flags"):
             raise ValueError(barrier)
         self.group, self.barrier_mode, self.vocab = group, barrier, vocab
+        self.spins = int(spins or 0)
+        if not 0 <= self.spins < (1 << 32):
+            raise ValueError("spins: 0 .. 2^32 - 1 polls")
         self.device = torch.device(device)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -522,9 +654,16 @@ class PeerExchange:
         self.rows = capacity_rows
         self.cap = payload_capacity(capacity_rows, vocab)
         self.bufs = [torch.zeros(self.cap, dtype=torch.int32, device=self.device) for _ in range(2)]
-        # the flag barrier's words (one per rank) and its error word, shared like the payloads
+        # the flag barrier's words (one per rank) and this rank's step counter, shared like the payloads
         self.flags = torch.zeros(max(64, self.world), dtype=torch.int32, device=self.device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # its error word: coherent host memory the OR pass stores into on a timeout
+        ep = c_void_p()
+        check(lib().fm_host_mapped_alloc(4, byref(ep)), "host_mapped_alloc")
+        self._err_ptr = ep.value
+        self._err_word = ctypes.c_int32.from_address(self._err_ptr)
+        self._failed = 0
+        self._skip_signal = 0        # tests: steps whose signal posts nothing (a rank that falls behind)
         torch.cuda.synchronize(self.device)
         mine = []
         for b in self.bufs + [self.flags]:
@@ -549,6 +688,8 @@ class PeerExchange:
         except Exception:
             self._unmap()
             raise
+        # [2, P]: buffer 0's addresses, then buffer 1's (the flag barrier's pass picks the row by
+        # the device counter's parity; the other barriers pass the row of the host step)
         self.ptab = torch.tensor(table[:2], dtype=torch.int64, device=self.device)
         # this rank's word in every rank's flag array
         self.signal_to = torch.tensor([a + 4 * self.rank for a in table[2]], dtype=torch.int64, device=self.device)
@@ -558,6 +699,17 @@ class PeerExchange:
     def payload(self):
         """This step's payload buffer (pack into it, then call)."""
         return self.bufs[self.step % 2]
+
+    def check(self):
+        """Raise PeerBarrierTimeout if a flag-barrier step has timed out (a read
+        of host memory: no synchronisation; a pass still running is seen at a
+        later call)."""
+        v = self._failed or (self._err_word.value if self._err_ptr else 0)
+        if v:
+            self._failed = v
+            raise PeerBarrierTimeout(f"rank {self.rank}: the flag barrier of step {v & 0xFFFFFFFF} timed out "
+                                     f"(a peer did not post its payload within the spin bound); that step's "
+                                     f"OR was not exact and the exchange is unusable")
 
     def barrier(self):
         import torch
@@ -569,24 +721,57 @@ class PeerExchange:
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.group)
 
+    def signal(self, stream=None):
+        """fm_peer_signal: advance the device step counter and post it to every rank."""
+        import torch
+        from ctypes import c_void_p
+
+        from ._lib import check, lib
+
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        world = self.world
+        if self._skip_signal:
+            self._skip_signal -= 1
+            world = 0
+        check(lib().fm_peer_signal(c_void_p(self.signal_to.data_ptr()), world, c_void_p(self.ctr.data_ptr()),
+                                   c_void_p(stream)), "peer_signal")
+
+    def flags_step(self, index, tokens, lo, hi, vocab: int, shift: int, out, unpack: bool = True,
+                   reset_below: int = 0):
+        """One decode step with the flag barrier, as three stream-ordered
+        launches and nothing else (capturable; a captured call replays for
+        every step): the payload decode of ``index`` -- the state (lo, hi)
+        updated in place, the payload buffer picked by the counter's parity --
+        the signal, the OR pass into ``out``.  The caller counts executed steps
+        in ``self.step`` (host parity = device parity, for payload())."""
+        if self.barrier_mode != "flags":
+            raise ValueError("flags_step: the exchange's barrier is not the flag barrier")
+        B = lo.numel()
+        if B > self.rows or vocab != self.vocab:
+            raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
+        index.decode_step_payload(tokens, lo, hi, lo, hi, self.bufs[0], vocab, shift, reset_below=reset_below,
+                                  payload_alt=self.bufs[1], step=self.ctr)
+        self.signal()
+        return self.or_flags(B, vocab, shift, out=out, unpack=unpack)
+
+    def or_flags(self, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+        """The flag barrier's OR pass of the step the counter names (its payload
+        buffer by the counter's parity)."""
+        return or_peer_payloads(self.ptab, self.cap, B, vocab, shift, out=out, unpack=unpack,
+                                flags=(self.flags, self.ctr, self._err_ptr, self.spins), buffers=2)
+
     def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True,
                  barrier_done: bool = False):
+        self.check()
         k = self.step % 2
         if payload.data_ptr() != self.bufs[k].data_ptr():
             raise ValueError("PeerExchange: pack into payload() of this step")
         if B > self.rows or vocab != self.vocab:
             raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
         if self.barrier_mode == "flags":
-            import torch
-            from ctypes import c_void_p
-
-            from ._lib import check, lib
-
-            n = (self.step + 1) & 0x7FFFFFFF or 1
-            stream = c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-            check(lib().fm_peer_signal(c_void_p(self.signal_to.data_ptr()), self.world, n, stream), "peer_signal")
-            out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack,
-                                   flags=(self.flags, n, self.err))
+            self.signal()
+            out = self.or_flags(B, vocab, shift, out=out, unpack=unpack)
         else:
             if not barrier_done:
                 self.barrier()
@@ -595,9 +780,12 @@ class PeerExchange:
         return out
 
     def errors(self) -> int:
-        """The last step number whose flag barrier timed out (0: none) -- a read of
-        the device error word (synchronises)."""
-        return int(self.err.item())
+        """The last step number whose flag barrier timed out (0: none), after a
+        synchronisation of the device."""
+        import torch
+
+        torch.cuda.synchronize(self.device)
+        return int(self._failed or (self._err_word.value if self._err_ptr else 0))
 
     def _unmap(self):
         from ctypes import c_void_p
@@ -611,42 +799,61 @@ class PeerExchange:
     def close(self):
         """Unmap the peers' buffers once no rank reads any buffer (a
         synchronize + group barrier: no rank frees its buffers while a peer
-        may still read them)."""
+        may still read them); raises PeerBarrierTimeout if a step timed out."""
         import torch
         import torch.distributed as dist
+        from ctypes import c_void_p
+
+        from ._lib import lib
 
         torch.cuda.synchronize(self.device)
         dist.barrier(group=self.group)
         self._unmap()
+        failed = self._failed or (self._err_word.value if self._err_ptr else 0)
+        if self._err_ptr:
+            lib().fm_host_mapped_free(c_void_p(self._err_ptr))
+            self._err_ptr, self._err_word = 0, None
+        if failed:
+            self._failed = failed
+            self.check()
 
 
-def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True, flags=None):
+def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True, flags=None,
+                     buffers: int = 1):
     """OR of the payloads at the device addresses ``ptrs`` (int64 [P], on the
     GPU that runs the pass; each payload ``cap`` words, in this process or a
     peer's buffer mapped by fm_ipc_open) -> uint8 [B, vocab] (unpack) or int32
-    [B, ceil(vocab/32)] words (fm_shard_or_rows_peers)."""
+    [B, ceil(vocab/32)] words (fm_shard_or_rows_peers).  ``flags`` = (flag
+    words int32 [>= P], the step counter int32 [1], the error word's address,
+    spins): the flag barrier first (fm_shard_or_rows_peers_wait); ``ptrs`` is
+    then [2, P], the double buffer's two address rows (``buffers`` = 2)."""
     import torch
     from ctypes import c_void_p
 
     from ._lib import check, lib
 
     W = (vocab + 31) // 32
-    if not (ptrs.is_cuda and ptrs.dtype == torch.int64 and ptrs.dim() == 1 and ptrs.is_contiguous()):
-        raise ValueError("ptrs: a contiguous int64 device tensor [P]")
+    if not (ptrs.is_cuda and ptrs.dtype == torch.int64 and ptrs.dim() == buffers and ptrs.is_contiguous()):
+        raise ValueError(f"ptrs: a contiguous int64 device tensor of {buffers} dimension(s)")
+    if (flags is None) != (buffers == 1):
+        raise ValueError("the flag barrier reads both payload buffers' address rows; the others one row")
+    nparts = ptrs.shape[-1]
     if out is None:
         out = (torch.empty((B, vocab), dtype=torch.uint8, device=ptrs.device) if unpack
                else torch.empty((B, W), dtype=torch.int32, device=ptrs.device))
     assert out.stride(1) == 1 and out.device == ptrs.device
     ld = out.stride(0) * out.element_size()
     stream = torch.cuda.current_stream(ptrs.device).cuda_stream
-    if flags is not None:          # (flag words int32 [>= P], step number, error word): the flag barrier first
-        fw, step, err = flags
-        check(lib().fm_shard_or_rows_peers_wait(c_void_p(ptrs.data_ptr()), ptrs.numel(), int(cap), B, vocab,
+    if flags is not None:
+        fw, ctr, err_ptr, spins = flags
+        if fw.numel() < nparts:
+            raise ValueError("flag words: one per part")
+        check(lib().fm_shard_or_rows_peers_wait(c_void_p(ptrs.data_ptr()), nparts, int(cap), B, vocab,
                                                 int(shift), c_void_p(out.data_ptr()), ld, 1 if unpack else 0,
-                                                c_void_p(fw.data_ptr()), int(step), c_void_p(err.data_ptr()),
-                                                c_void_p(stream)), "shard_or_rows_peers_wait")
+                                                c_void_p(fw.data_ptr()), c_void_p(ctr.data_ptr()), int(spins),
+                                                c_void_p(err_ptr), c_void_p(stream)), "shard_or_rows_peers_wait")
         return out
-    check(lib().fm_shard_or_rows_peers(c_void_p(ptrs.data_ptr()), ptrs.numel(), int(cap), B, vocab, int(shift),
+    check(lib().fm_shard_or_rows_peers(c_void_p(ptrs.data_ptr()), nparts, int(cap), B, vocab, int(shift),
                                        c_void_p(out.data_ptr()), ld, 1 if unpack else 0, c_void_p(stream)),
           "shard_or_rows_peers")
     return out
@@ -785,4 +992,5 @@ def unpack_bits(packed, vocab: int):
 __all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
            "ShardedIndex",
            "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "or_payloads", "SparseExchange",
-           "PeerExchange", "or_peer_payloads", "pack_payload_host", "or_payloads_host"]
+           "PeerExchange", "PeerBarrierTimeout", "or_peer_payloads", "pack_payload_host", "or_payloads_host",
+           "payload_header_words"]

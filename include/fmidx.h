@@ -285,9 +285,14 @@ int fm_shard_payload_capacity(uint64_t B, uint64_t vocab, uint64_t* words);
  * cost is what the reader reads, not the capacity; an all_gather would ship the
  * whole capacity (use fm_shard_pack there).  vocab <= 262144; d_payload 16-B
  * aligned, cap_words >= fm_shard_payload_capacity(m, vocab). */
+/* The state may be updated in place (d_lo_out == d_lo_in, d_hi_out == d_hi_in), so a captured step
+ * replays for every step.  With d_step != NULL (the flag barrier's device step counter) the kernel
+ * writes d_payload when *d_step is even and d_payload_alt when it is odd -- the peer exchange's
+ * double buffer picked on the device, in step with fm_shard_or_rows_peers_wait; NULL: d_payload. */
 int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
                            const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
-                           uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab, void* stream);
+                           uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab,
+                           uint32_t* d_payload_alt, const uint32_t* d_step, void* stream);
 int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
                   uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
@@ -309,16 +314,33 @@ int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_str
 int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                            uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
 /* The flag barrier instead of a collective: each rank owns a uint32 flag word per
- * rank (d_flags[world], zeroed, IPC-shared).  fm_peer_signal stores `step` into
- * every rank's word for this rank (d_flag_ptrs[world]: the peers' word
- * addresses, mapped; system-scope vector stores) -- issue it after the kernel
- * that wrote this rank's payload; fm_shard_or_rows_peers_wait first waits until
- * every d_flags[p] >= step (system-scope polls, bounded: on timeout *d_err =
- * step and the pass goes on), then ORs as fm_shard_or_rows_peers. */
-int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t step, void* stream);
+ * rank (d_flags[world], zeroed, IPC-shared) and a uint32 step counter d_step
+ * (device, zeroed).  fm_peer_signal: step = *d_step + 1 (mod 2^32); a
+ * system-scope release (the payload the previous kernel on the stream wrote is
+ * visible before any flag says so), step stored into every rank's word for this
+ * rank (d_flag_ptrs[world]: the peers' word addresses, mapped; system-scope
+ * vector stores), *d_step = step -- issue it after the kernel that wrote this
+ * rank's payload; world = 0 advances the counter and posts nothing.
+ * fm_shard_or_rows_peers_wait: step = *d_step; the payloads are
+ * d_part_ptrs[((step - 1) & 1) * nparts ..] (d_part_ptrs holds buffer 0's
+ * nparts addresses, then buffer 1's); waits until every (int32)(d_flags[p] -
+ * step) >= 0 (system-scope polls, at most `spins`, 0 = 2^20 ~ 0.1-1 s), then a
+ * system-scope acquire, then ORs as fm_shard_or_rows_peers.  On timeout
+ * *err = step (a system-scope store: err may be fm_host_mapped_alloc memory,
+ * read by the host without a synchronisation) and the pass goes on, so the
+ * grid drains -- its output is then NOT exact and the caller must raise.
+ * The step number lives on the device, so decode + signal + OR captured once
+ * into a graph replay for every step. */
+int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_step, void* stream);
 int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
-                                const uint32_t* d_flags, uint32_t step, uint32_t* d_err, void* stream);
+                                const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,
+                                void* stream);
+/* Coherent host memory mapped for the device (hipHostMalloc mapped | coherent),
+ * zeroed: kernels store into it, the host reads it without a copy (the flag
+ * barrier's error word). */
+int fm_host_mapped_alloc(uint64_t bytes, void** out);
+int fm_host_mapped_free(void* p);
 int fm_ipc_handle(const void* d_ptr, uint8_t* handle, uint64_t* offset);
 int fm_ipc_open(const uint8_t* handle, void** d_base);
 int fm_ipc_close(void* d_base);

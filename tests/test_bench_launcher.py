@@ -84,3 +84,47 @@ def test_bench_refuses_more_gpus_than_visible(tmp_path):
                        env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
     assert r.returncode == 2, r.stderr[-2000:]
     assert "GPU(s) visible" in r.stderr
+
+
+def test_visible_gpus_from_topology(tmp_path):
+    """The launcher's GPU count reads the KFD topology (CPU nodes have gpu_id 0)
+    and honours the visibility lists -- no HIP runtime involved."""
+    for i, gid in enumerate([0, 1234, 0, 5678, 91011]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "gpu_id").write_text(f"{gid}\n")
+    topo = str(tmp_path)
+    assert bench.visible_gpus({}, topo) == 3
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,1"}, topo) == 2
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": ""}, topo) == 0
+    assert bench.visible_gpus({"CUDA_VISIBLE_DEVICES": "0,1,2,3,4,5"}, topo) == 3
+    assert bench.visible_gpus({}, str(tmp_path / "missing")) == 0
+
+
+def test_launcher_parent_never_calls_torch_cuda(monkeypatch):
+    """`bench.py --gpus N` without WORLD_SIZE: the parent counts GPUs and
+    spawns the ranks without a single torch.cuda call (any of them could
+    initialise HIP in the parent, whose children are then new programs)."""
+    import torch
+
+    calls = []
+
+    def boom(name):
+        def f(*a, **k):
+            calls.append(name)
+            raise AssertionError(f"the launcher parent called torch.cuda.{name}")
+        return f
+
+    for name in ("device_count", "is_available", "init", "set_device", "current_device", "synchronize",
+                 "get_device_properties", "mem_get_info", "_lazy_init"):
+        monkeypatch.setattr(torch.cuda, name, boom(name))
+    spawned = []
+    monkeypatch.setattr(bench, "visible_gpus", lambda *a, **k: 8)
+    monkeypatch.setattr(bench, "spawn_ranks", lambda n, cmd, **k: spawned.append((n, cmd)) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    assert not calls
+    assert spawned and spawned[0][0] == 4 and spawned[0][1][-4:] == ["--gpus", "4", "--steps", "3"]

@@ -213,14 +213,16 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
         assert dec._xchg.respecified >= 1          # the restart step outgrew the speculative size
         # the peer exchange with its stream-ordered RCCL barrier and with the flag barrier (a world of
         # one: the own buffer and flag word only)
-        for pb in ("collective", "flags"):
-            pdec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="peer", halo=None, peer_barrier=pb)
+        for pb, graph in (("collective", False), ("flags", False), ("flags", True)):
+            pdec = ShardedDecoder(full, V, 10, group=dist.group.WORLD, reduce="peer", halo=None, peer_barrier=pb,
+                                  graph=graph)
             pdec.start(pats, "cuda")
             for step in range(6):
                 tok = [F[a + 3 + step] if rng.random() < 0.8 else -1 for a in starts]
                 got = pdec.step(torch.tensor(tok, dtype=torch.int64, device="cuda"))
-                assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), (pb, step)
+                assert torch.equal(got, full.allowed_mask(pdec.lo, pdec.hi, V, 10)), (pb, graph, step)
             assert pdec._peer.errors() == 0
+            assert (pdec._g is not None) == graph
             # a larger batch on the same decoder: the exchange is rebuilt with room for it
             pats2 = [F[a:a + 2] for a in rng.integers(0, len(F) - 40, size=3 * B)]
             pdec.start(pats2, "cuda")
@@ -232,7 +234,7 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
         occ = full.occurring_distinct
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         ref = mk(full)
-        for exchange in ("sparse", "peer"):
+        for exchange in ("sparse", "peer", "dense"):
             sidx = ShardedIndex(full, occ, group=dist.group.WORLD, exchange=exchange)
             sp = mk(sidx)
             for step in range(4):
@@ -240,6 +242,66 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
                 scores = torch.from_numpy(rng.standard_normal((8, V)).astype(np.float32)).cuda()
                 assert torch.equal(sp(ids, scores.clone()).view(torch.int32),
                                    ref(ids, scores.clone()).view(torch.int32)), (exchange, step)
+            # the sparse exchange with a larger batch on the same index (its payload and speculative
+            # gather size are rebuilt for it: ADVICE r4)
+            ids = torch.tensor([[1] + F[a:a + 3] for a in rng.integers(0, len(F) - 40, size=40)],
+                               dtype=torch.int64).cuda()
+            scores = torch.from_numpy(rng.standard_normal((40, V)).astype(np.float32)).cuda()
+            assert torch.equal(sp(ids, scores.clone()).view(torch.int32), ref(ids, scores.clone()).view(torch.int32))
+            # the host path over the shard: a row without the end marker, boosts past the float range
+            _qwen_host_path(full, sidx, F, rng)
             sidx.close()
     finally:
         dist.destroy_process_group()
+
+
+def _qwen_host_path(full, sidx, F, rng):
+    """Qwen inputs the device path hands to the host path (a row without the
+    end marker; 10 * 2^k past fp32's range: the reference's RuntimeError),
+    and a bf16 call whose boosts are inf (written on the device, as the
+    reference writes them): the processor over ShardedIndex gives the
+    unsharded processor's outcome, bit for bit or the same exception."""
+    import fmidx.processors as P
+
+    marker, think = [151645, 198, 151644, 77091, 198], [151667, 271, 151668, 271]
+    kw = dict(num_beams=1, min_new_tokens=3, always_allow_eos=True, length_reward_factor=2.0)
+    ref_p = P.QwenIndexBasedLogitsProcessor(index=full, **kw)
+    sh_p = P.QwenIndexBasedLogitsProcessor(index=sidx, **kw)
+    B = 6
+    st = rng.integers(0, len(F) - 200, size=B)
+    eos_rows = [b for b in range(B) if b % 3 == 1]
+
+    def rows(k, drop_marker=False):
+        out = []
+        for b in range(B):
+            s = [int(x) for x in F[int(st[b]):int(st[b]) + 5]]
+            if b in eos_rows:
+                s = [int(x) for x in rng.integers(0, 2000, size=k - 1)] + [2]
+            out.append([100, 101] + marker + think + s)
+        w = max(len(r) for r in out)
+        out = [r + [0] * (w - len(r)) for r in out]
+        if drop_marker:
+            out[2][2:7] = [9, 9, 9, 9, 9]
+        return out
+
+    def outcome(p, ids, sc):
+        try:
+            o = p(ids, sc.clone())
+        except Exception as e:  # noqa: BLE001 -- the reference's exception is the expected outcome
+            return type(e).__name__, str(e)
+        return "ok", o.view(torch.int32 if o.dtype == torch.float32 else torch.int16).cpu()
+
+    for name, ids_l, dt in (("k>=125 bf16", rows(130), torch.bfloat16), ("k>=125 fp32", rows(130), torch.float32),
+                            ("no marker", rows(6, True), torch.bfloat16), ("ordinary", rows(6), torch.float32)):
+        ids = torch.tensor(ids_l, dtype=torch.int64).cuda()
+        sc = torch.from_numpy(rng.standard_normal((B, V)).astype(np.float32)).to(dt).cuda()
+        want, got = outcome(ref_p, ids, sc), outcome(sh_p, ids, sc)
+        assert want[0] == got[0], (name, want[0], got[0], got[1] if got[0] != "ok" else "")
+        if want[0] == "ok":
+            assert torch.equal(want[1], got[1]), name
+        else:
+            assert want[1] == got[1], name
+        if name == "k>=125 fp32":
+            assert want[0] == "RuntimeError", want
+        if name == "k>=125 bf16":
+            assert want[0] == "ok" and torch.isinf(ref_p(ids, sc.clone()).float()).any()

@@ -121,7 +121,7 @@ def expected_masks(docs, patterns, steps):
     return out
 
 
-def _worker(rank, world, port, halo, reduce, outdir, fused=False):
+def _worker(rank, world, port, halo, reduce, outdir, fused=False, grow=False):
     import torch.distributed as dist
 
     from fmidx.sharding import ShardedDecoder, shard_corpus
@@ -137,6 +137,12 @@ def _worker(rank, world, port, halo, reduce, outdir, fused=False):
     masks = [dec.start(patterns, "cpu").numpy().copy()]
     for tk in steps:
         masks.append(dec.step(torch.tensor(tk, dtype=torch.int64)).numpy().copy())
+    if grow:
+        # the same decoder restarted with a batch three times larger: the payload and the
+        # speculative gather size of the smaller batch must not be reused for it
+        masks = [dec.start(patterns * 3, "cpu").numpy().copy()]
+        for tk in steps:
+            masks.append(dec.step(torch.tensor(tk * 3, dtype=torch.int64)).numpy().copy())
     np.save(os.path.join(outdir, f"r{rank}.npy"), np.stack(masks))
     dist.barrier()
     dist.destroy_process_group()
@@ -150,9 +156,9 @@ def _free_port():
     return p
 
 
-def _run(world, halo, reduce, fused=False):
+def _run(world, halo, reduce, fused=False, grow=False):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d, fused), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d, fused, grow), nprocs=world, join=True)
         return [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
 
 
@@ -164,6 +170,15 @@ def test_sharded_or_equals_unsharded(reduce, fused):
     want = np.stack(expected_masks(docs, patterns, steps))
     got = _run(2, 8 + 8 + 1, reduce, fused)      # halo >= longest pattern (7 + 8 steps) + 1
     for g in got:                          # every rank holds the reduced mask
+        assert np.array_equal(g, want)
+
+
+def test_sparse_exchange_survives_a_larger_batch():
+    """a decoder whose batch grows (start() with more rows) must not
+    reuse the smaller batch's payload buffer or speculative gather size."""
+    docs, patterns, steps = make_case()
+    want = np.stack(expected_masks(docs, patterns * 3, [tk * 3 for tk in steps]))
+    for g in _run(2, 8 + 8 + 1, "sparse", fused=True, grow=True):
         assert np.array_equal(g, want)
 
 
