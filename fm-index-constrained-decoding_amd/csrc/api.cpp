@@ -1401,6 +1401,30 @@ int fm_device_bwt(const fm_index* h, const uint32_t** out) {
   FM_API_END
 }
 
+int fm_release_bwt_view(fm_index* h) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (h->idx.bwt_view) {
+    // the caller's pointers into it are dead from here: synchronise the device first, so no
+    // stream-ordered reader of it is still in flight
+    FM_HIP(hipDeviceSynchronize());
+    FM_HIP(hipFree(h->idx.bwt_view));
+    h->idx.bwt_view = nullptr;
+  }
+  return 0;
+  FM_API_END
+}
+
+int fm_stats_views(const fm_index* h, uint64_t* bwt_view_bytes) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  if (bwt_view_bytes) *bwt_view_bytes = h->idx.bwt_view ? h->idx.n * 4 : 0;
+  return 0;
+  FM_API_END
+}
+
 int fm_device_struct(const fm_index* h, int which, const void** out, uint64_t* bytes) {
   FM_API_BEGIN
   FM_CHECK_BUILT(h);

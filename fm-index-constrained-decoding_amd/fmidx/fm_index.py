@@ -257,6 +257,9 @@ class FMIndex:
         check(lib().fm_stats_mem(self._h, *[byref(v) for v in mem]), "stats_mem")
         for k, v in zip(["lf_e_bytes", "sample_bytes", "device_bytes"], mem):
             out[k] = int(v.value)
+        bv = c_uint64()
+        check(lib().fm_stats_views(self._h, byref(bv)), "stats_views")
+        out["bwt_view_bytes"] = int(bv.value)     # a materialised BWT copy (device_bwt), outside device_bytes
         return out
 
     def cache_contains(self, lo, hi):
@@ -463,9 +466,12 @@ class FMIndex:
         return [tuple(flat[o[i]:o[i + 1]]) for i in range(m)]
 
     def device_bwt(self):
-        """The handle's BWT (uint32[n] in HBM) as a zero-copy int32 torch
-        tensor on the index's device (valid while this index lives; read-only
-        by contract) -- for samplers, traces and the CPU baseline."""
+        """The handle's BWT (uint32[n] in HBM) as an int32 torch tensor on
+        the index's device (read-only by contract) -- for samplers, traces and
+        the CPU baseline.  With the plain BWT freed (the default: E holds the
+        symbols) this MATERIALISES an n * 4-byte copy held by the handle
+        (stats()["bwt_view_bytes"]); release_bwt_view() frees it, after which
+        the tensor must not be used."""
         import torch
 
         idx = self
@@ -480,6 +486,11 @@ class FMIndex:
         with torch.cuda.device(self._device):
             t = torch.as_tensor(_View(), device=torch.device("cuda", self._device))
         return t
+
+    def release_bwt_view(self) -> None:
+        """Free the BWT copy device_bwt() materialised (synchronises the
+        device; tensors from device_bwt() are dead afterwards)."""
+        check(lib().fm_release_bwt_view(self._h), "release_bwt_view")
 
     def device_bwt_ptr(self) -> int:
         p = c_void_p()

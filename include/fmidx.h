@@ -508,8 +508,16 @@ int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_h
 int fm_probe_gather(const void* d_buf, uint64_t bytes, int chase, uint64_t loads, uint32_t threads,
                     uint64_t* d_sink, void* stream);
 
-/* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces. */
+/* Device pointer to the plain BWT (uint32[n]) for samplers / bench traces.
+ * When the index keeps no plain BWT (E holds its symbols: the default), the
+ * first call MATERIALISES a copy (n * 4 bytes of HBM, held by the handle and
+ * not counted in fm_stats_mem's total: see fm_stats_views) -- release it with
+ * fm_release_bwt_view once done (it synchronises the device). */
 int fm_device_bwt(const fm_index* h, const uint32_t** out);
+int fm_release_bwt_view(fm_index* h);
+/* Bytes the handle holds outside its query structures: the BWT copy
+ * fm_device_bwt materialised (0 when none). */
+int fm_stats_views(const fm_index* h, uint64_t* bwt_view_bytes);
 
 /* Device pointer and byte size of one index structure, for the bench's
  * gather ceilings over the index's own allocations: which = 0 plain BWT,
