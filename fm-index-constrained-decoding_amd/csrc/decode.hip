@@ -424,6 +424,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   const uint64_t t1 = min(vocab, t0 + SW);
   const uint64_t ntok = t1 - t0;
   const uint64_t nch = (ntok + CH - 1) / CH;
+  uint8_t* out_row = mask + row * ld;
   // Rows whose incoming range is narrow stay narrow after the LF step (it
   // can only shrink a range), so their slice is zero-filled right away --
   // the stores overlap the LF chain -- and the final pass rewrites only the
@@ -447,11 +448,10 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     // the peer exchange's double buffer picked by the device step counter's parity (a
     // captured step replays for every step); only the stores at the end depend on it
     if (pay_sel && (__hip_atomic_load(pay_sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) {
-      mask = reinterpret_cast<uint8_t*>(pay_alt) + (reinterpret_cast<uint8_t*>(mask) - reinterpret_cast<uint8_t*>(pay));
+      out_row = reinterpret_cast<uint8_t*>(pay_alt) + (out_row - reinterpret_cast<uint8_t*>(pay));
       pay = pay_alt;
     }
   }
-  uint8_t* out_row = mask + row * ld;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(out_row + t0) & 15) == 0);
   // the slice's bytes (uint8) or words (packed) as one buffer, offsets relative to token t0
   const __amdgpu_buffer_rsrc_t orsrc =
