@@ -687,16 +687,14 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
                     "uint8 [B, V] out"}
 
 
-COMPACT_ENV = {"FMIDX_TRANS": "1", "FMIDX_LF_E": "0", "FMIDX_PROBE_FIRST": "0"}
-
-
 def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace, sh, world=8, halo=128):
     """Legs that need the replica index gone (N = 1, C3): the compact memory
     profile of the same corpus, then C4 on one GPU.  Returns
     (compact, c4) result dicts.
 
-    Compact: the index rebuilt with COMPACT_ENV (transitions to cached children
-    only, no E array, no probe-first) -- the same BWT, so the headline trace's K
+    Compact: the index rebuilt with the compact build profile (fm_build_options
+    FM_PROFILE_COMPACT: transitions to cached children only, no E array, no
+    probe-first) -- the same BWT, so the headline trace's K
     steps replay from the same state and must end in the same ranges; timed
     cold like the headline.
 
@@ -738,20 +736,11 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
     compact = {}
     try:
         m_tok, m_lo, m_hi, f_lo, f_hi = main_trace
-        old = {k: os.environ.get(k) for k in COMPACT_ENV}
-        os.environ.update(COMPACT_ENV)
-        try:
-            t0 = time.time()
-            cx = FMIndex(device=dev.index)
-            cx.initialize_from_text_device(text)
-            torch.cuda.synchronize()
-            cbuild = time.time() - t0
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+        t0 = time.time()
+        cx = FMIndex(device=dev.index, options="compact")
+        cx.initialize_from_text_device(text)
+        torch.cuda.synchronize()
+        cbuild = time.time() - t0
         mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
         lo, hi = m_lo.clone(), m_hi.clone()
         bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
@@ -770,7 +759,8 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
         cold = replay(g, True) / K * 1e3
         fin = bufs[K % 2]
         cst = cx.stats()
-        compact = {"env": dict(COMPACT_ENV), "device_bytes": int(cst["device_bytes"]), "build_s": round(cbuild, 1),
+        compact = {"build_options": cx.build_options(), "device_bytes": int(cst["device_bytes"]),
+                   "build_s": round(cbuild, 1),
                    "cold_ms_per_step": cold / 1e3, "warm_ms_per_step": float(np.median(warm)) / 1e3,
                    "value_cold": B / (cold * 1e-6),
                    "ranges_equal_default_profile": bool(torch.equal(fin[0], f_lo) and torch.equal(fin[1], f_hi))}
@@ -1067,7 +1057,7 @@ def main():
     mem_log("index built", dev)
     n = bwt.numel()
     st = fm.stats()
-    st["lf_e"] = os.environ.get("FMIDX_LF_E", "1") != "0" and n < (1 << 36)
+    st["lf_e"] = fm.build_options()["lf_e"] != 0 and n < (1 << 36)
     S = W + K
     if args.cpu_window < 0:
         args.cpu_window = max(3, -(-768 // B))

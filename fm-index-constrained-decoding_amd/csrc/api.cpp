@@ -264,13 +264,10 @@ int ws_release(fm_index* h, hipStream_t s) {
 
 // Above this many rows the reference's construction entry points
 // (initialize / initialize_from_file, fm_index.cpp:33-48) sort on the GPU.
-uint64_t gpu_sort_min() {
-  const char* e = std::getenv("FMIDX_GPU_SORT_MIN");
-  return (e && *e) ? std::strtoull(e, nullptr, 10) : (1ull << 20);
-}
+uint64_t gpu_sort_min(const fm_index* h) { return h->idx.opts.gpu_sort_min; }
 
 // Build from a host text T' (+ sentinel already appended): suffix array by
-// GPU prefix doubling (n >= gpu_sort_min(), n < 2^34) or host SA-IS, then
+// GPU prefix doubling (n >= the gpu_sort_min option, n < 2^34) or host SA-IS, then
 // the device structures; the suffix array is reduced to its samples (locate /
 // extract by LF walks) and freed.
 int build_from_text(fm_index* h, std::vector<uint32_t>& text) {
@@ -280,7 +277,7 @@ int build_from_text(fm_index* h, std::vector<uint32_t>& text) {
   FM_HIP(hipMalloc(reinterpret_cast<void**>(&x.bwt), n * 4));
   uint64_t* d_sa = nullptr;
   FM_HIP(hipMalloc(reinterpret_cast<void**>(&d_sa), n * 8));
-  if (n >= gpu_sort_min() && n < (1ull << 34)) {
+  if (n >= gpu_sort_min(h) && n < (1ull << 34)) {
     uint32_t* d_text = nullptr;
     FM_HIP(hipMalloc(reinterpret_cast<void**>(&d_text), n * 4));
     FM_HIP(hipMemcpyAsync(d_text, text.data(), n * 4, hipMemcpyHostToDevice, x.stream));
@@ -474,6 +471,11 @@ int fm_create(fm_index** out, int device) {
   }
   auto* h = new fm_index();
   h->idx.device = device;
+  h->idx.opts = fmidx::build_profile(FM_PROFILE_DEFAULT);
+  if (fmidx::apply_build_overrides(h->idx.opts)) {
+    delete h;
+    return -1;
+  }
   DeviceGuard g(device);
   if (!g.ok || hipStreamCreateWithFlags(&h->idx.stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&h->scratch), 64 * 8) != hipSuccess) {
@@ -928,7 +930,178 @@ int fm_save(fm_index* h, const char* path) {
   FM_API_END
 }
 
-int fm_load(fm_index** out, const char* path, int device) {
+// ---- options (fm_build_options: per handle; fm_tuning: process-wide) ----
+}  // extern "C"
+
+namespace {
+
+fmidx::BuildOpts to_internal(const fm_build_options& o) {
+  // every field of the profile's, where the caller left the "profile" sentinel (-1 / 0)
+  fmidx::BuildOpts x = fmidx::build_profile(o.profile);
+  if (o.transitions >= 0) x.transitions = o.transitions;
+  if (o.lf_e >= 0) x.lf_e = o.lf_e;
+  if (o.lf_e2 >= 0) x.lf_e2 = o.lf_e2;
+  if (o.probe_first >= 0) x.probe_first = o.probe_first;
+  if (o.keep_bwt >= 0) x.keep_bwt = o.keep_bwt;
+  if (o.follow_bitmaps >= 0) x.follow_bitmaps = o.follow_bitmaps;
+  if (o.bm_log2 >= 0) x.bm_log2 = o.bm_log2;
+  if (o.cache_min) x.cache_min = o.cache_min;
+  if (o.cache_mb) x.cache_mb = o.cache_mb;
+  if (o.trans_mb) x.trans_mb = o.trans_mb;
+  if (o.gpu_sort_min) x.gpu_sort_min = o.gpu_sort_min;
+  return x;
+}
+
+void to_public(const fmidx::BuildOpts& x, fm_build_options* o) {
+  o->size = sizeof(fm_build_options);
+  o->profile = x.profile;
+  o->transitions = x.transitions;
+  o->lf_e = x.lf_e;
+  o->lf_e2 = x.lf_e2;
+  o->probe_first = x.probe_first;
+  o->keep_bwt = x.keep_bwt;
+  o->follow_bitmaps = x.follow_bitmaps;
+  o->bm_log2 = x.bm_log2;
+  o->reserved = 0;
+  o->cache_min = x.cache_min;
+  o->cache_mb = x.cache_mb;
+  o->trans_mb = x.trans_mb;
+  o->gpu_sort_min = x.gpu_sort_min;
+}
+
+bool valid(const fmidx::BuildOpts& x) {
+  auto b = [](int32_t v) { return v == 0 || v == 1; };
+  if ((x.profile != FM_PROFILE_DEFAULT && x.profile != FM_PROFILE_COMPACT) || x.transitions < 0 ||
+      x.transitions > 2 || !b(x.lf_e) || !b(x.lf_e2) || !b(x.probe_first) || !b(x.keep_bwt) ||
+      !b(x.follow_bitmaps) || x.bm_log2 < -1 || x.bm_log2 > 30 || x.cache_min < 2) {
+    set_error("build options: profile 0/1, transitions 0..2, switches 0/1, bm_log2 -1..30, cache_min >= 2");
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fm_build_options_init(fm_build_options* o, int profile) {
+  FM_API_BEGIN
+  if (!o || (profile != FM_PROFILE_DEFAULT && profile != FM_PROFILE_COMPACT)) {
+    set_error("build_options_init: null options or unknown profile %d", profile);
+    return -1;
+  }
+  to_public(fmidx::build_profile(profile), o);
+  return 0;
+  FM_API_END
+}
+
+int fm_set_build_options(fm_index* h, const fm_build_options* o) {
+  FM_API_BEGIN
+  FM_CHECK_HANDLE(h);
+  if (!o || o->size != sizeof(fm_build_options)) {
+    set_error("set_build_options: null options or size %u != %zu (fm_build_options_init sets it)",
+              o ? o->size : 0u, sizeof(fm_build_options));
+    return -1;
+  }
+  fmidx::BuildOpts x = to_internal(*o);
+  if (fmidx::apply_build_overrides(x) || !valid(x)) return -1;
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->idx.opts = x;
+  return 0;
+  FM_API_END
+}
+
+int fm_get_build_options(const fm_index* h, fm_build_options* o) {
+  FM_API_BEGIN
+  FM_CHECK_HANDLE(h);
+  if (!o) {
+    set_error("get_build_options: null options");
+    return -1;
+  }
+  to_public(h->idx.opts, o);
+  return 0;
+  FM_API_END
+}
+
+int fm_tuning_init(fm_tuning* t) {
+  FM_API_BEGIN
+  if (!t) {
+    set_error("tuning_init: null tuning");
+    return -1;
+  }
+  const fmidx::Tuning d;
+  std::memset(t, 0, sizeof(*t));
+  t->size = sizeof(fm_tuning);
+  t->lf_group = d.lf_group;
+  t->search_group = d.search_group;
+  t->dec_threads = d.dec_threads;
+  t->mask_slices = d.mask_slices;
+  t->lf_group_min = d.lf_group_min;
+  t->lf_work = d.lf_work;
+  t->lf_gprobe = d.lf_gprobe;
+  t->lf_quad = d.lf_quad;
+  t->lf_split = d.lf_split;
+  t->search_p8 = d.search_p8;
+  t->lf_sweep_min = d.lf_sweep_min;
+  t->sa_chunk = d.sa_chunk;
+  return 0;
+  FM_API_END
+}
+
+int fm_set_tuning(const fm_tuning* t) {
+  FM_API_BEGIN
+  if (!t || t->size != sizeof(fm_tuning)) {
+    set_error("set_tuning: null tuning or size %u != %zu (fm_tuning_init sets it)", t ? t->size : 0u,
+              sizeof(fm_tuning));
+    return -1;
+  }
+  fmidx::Tuning x;
+  x.lf_group = t->lf_group;
+  x.search_group = t->search_group;
+  x.dec_threads = t->dec_threads;
+  x.mask_slices = t->mask_slices;
+  x.lf_group_min = t->lf_group_min;
+  x.lf_work = t->lf_work;
+  x.lf_gprobe = t->lf_gprobe;
+  x.lf_quad = t->lf_quad;
+  x.lf_split = t->lf_split;
+  x.search_p8 = t->search_p8;
+  x.lf_sweep_min = t->lf_sweep_min;
+  x.sa_chunk = t->sa_chunk;
+  if (fmidx::set_tuning(x)) return -1;
+  fmidx::reload_lf_tuning();
+  return 0;
+  FM_API_END
+}
+
+int fm_get_tuning(fm_tuning* t) {
+  FM_API_BEGIN
+  if (!t) {
+    set_error("get_tuning: null tuning");
+    return -1;
+  }
+  const fmidx::Tuning& x = fmidx::tuning();
+  std::memset(t, 0, sizeof(*t));
+  t->size = sizeof(fm_tuning);
+  t->lf_group = x.lf_group;
+  t->search_group = x.search_group;
+  t->dec_threads = x.dec_threads;
+  t->mask_slices = x.mask_slices;
+  t->lf_group_min = x.lf_group_min;
+  t->lf_work = x.lf_work;
+  t->lf_gprobe = x.lf_gprobe;
+  t->lf_quad = x.lf_quad;
+  t->lf_split = x.lf_split;
+  t->search_p8 = x.search_p8;
+  t->lf_sweep_min = x.lf_sweep_min;
+  t->sa_chunk = x.sa_chunk;
+  return 0;
+  FM_API_END
+}
+
+int fm_load(fm_index** out, const char* path, int device) { return fm_load_ex(out, path, device, nullptr); }
+
+int fm_load_ex(fm_index** out, const char* path, int device, const fm_build_options* opts) {
   FM_API_BEGIN
   if (!out) {
     set_error("null out");
@@ -944,6 +1117,10 @@ int fm_load(fm_index** out, const char* path, int device) {
   const uint64_t n = f.n;
   fm_index* h = nullptr;
   if (fm_create(&h, device)) return -1;
+  if (opts && fm_set_build_options(h, opts)) {
+    fm_destroy(h);
+    return -1;
+  }
   {
     DeviceGuard g(device);
     auto& x = h->idx;
@@ -1459,6 +1636,8 @@ int fm_debug_set_stamps(fm_index* h, uint64_t* d_buf) {
 
 int fm_reload_tuning(void) {
   FM_API_BEGIN
+  // the library defaults with the FMIDX_TUNING overrides on top
+  if (fmidx::set_tuning(fmidx::Tuning{})) return -1;
   fmidx::reload_lf_tuning();
   return 0;
   FM_API_END

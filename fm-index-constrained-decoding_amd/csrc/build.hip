@@ -424,12 +424,6 @@ int exclusive_scan_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStr
   return 0;
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* v = std::getenv(name);
-  if (!v || !*v) return dflt;
-  return (uint32_t)std::strtoul(v, nullptr, 10);
-}
-
 __global__ void __launch_bounds__(kThreads) k_e_symbols(const uint64_t* __restrict__ E, uint64_t n,
                                                         uint32_t* __restrict__ out) {
   for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kThreads)
@@ -566,7 +560,8 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   // small indexes keep 2^12 so that they still get a hierarchy and a cache.
   // From 2^31 rows 2^16 (round 4, with the plain BWT freed: C3 122.0 -> 117.9 GiB,
   // 13.72 vs 13.86 us cold, build 12.0 -> 14.6 s; profiles/r04_memory/).
-  const uint32_t log2b0 = env_u32("FMIDX_BM_LOG2", n >= (1ull << 31) ? 16 : n >= (1ull << 26) ? 14 : 12);
+  const uint32_t log2b0 = h->opts.bm_log2 >= 0 ? (uint32_t)h->opts.bm_log2
+                                               : (n >= (1ull << 31) ? 16 : n >= (1ull << 26) ? 14 : 12);
   const uint32_t words = (uint32_t)(((uint64_t)max_sym + 1 + 127) / 128 * 4);
   const uint64_t nb0 = n >> log2b0;
   uint32_t bm_levels = 0;
@@ -639,12 +634,12 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   // a decode range of >= cache_min rows is cached (every such range reachable
   // from the root is), so its probe hits: waiting for the probe alone before
   // any rank load measured 17.5 -> 16.1 us/step cold, 10.4 -> 9.8 warm at C3
-  v.probe_first = env_u32("FMIDX_PROBE_FIRST", 1) != 0;
+  v.probe_first = h->opts.probe_first != 0;
   // -- follow-set bitmaps (one per symbol's C-block), built with the mask
   //    kernel itself once the view above is complete
   // (off by default: the range-bitmap cache below holds every C-block of
   // width >= its threshold, and narrower ones are streamed)
-  if (bm_ok && env_u32("FMIDX_FOLLOW_BITMAPS", 0) != 0) {
+  if (bm_ok && h->opts.follow_bitmaps != 0) {
     const uint64_t nsym = (uint64_t)max_sym + 1;
     uint32_t* fb = nullptr;
     if (dmalloc(&fb, nsym * words)) return -1;
@@ -665,8 +660,8 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   build_phase("range cache + transitions", t, s);
   // The plain BWT duplicates E's symbol field (4 bytes per row: 16.8 GiB at C3).  Once E is
   // built every kernel reads symbols through bwt_sym() / stream_symbols_e(), so the copy is
-  // freed; fm_device_bwt materialises one on request (FMIDX_KEEP_BWT=1 keeps it).
-  if (h->E && d_bwt == h->bwt && env_u32("FMIDX_KEEP_BWT", 0) == 0) {
+  // freed; fm_device_bwt materialises one on request (the keep_bwt option keeps it).
+  if (h->E && d_bwt == h->bwt && h->opts.keep_bwt == 0) {
     FM_HIP(hipStreamSynchronize(s));
     FM_HIP(hipFree(h->bwt));
     h->bwt = nullptr;
@@ -775,7 +770,7 @@ int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) 
 // chunks of <= 2^29 occurrences (cut at C boundaries): select the chunk's
 // positions (ascending), stable radix sort them by symbol, write base + k.
 int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
-  if (env_u32("FMIDX_LF_E", 1) == 0) return 0;
+  if (h->opts.lf_e == 0) return 0;
   if (n >= (1ull << kESymShift) || h->max_sym >= (1ull << (64 - kESymShift))) return 0;
   const uint64_t K = (uint64_t)h->max_sym + 1;
   std::vector<uint64_t> C(K + 1);
@@ -831,14 +826,14 @@ int device_build_lfe(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s)
   FM_HIP(hipFree(key2));
   FM_HIP(hipFree(d_cnt));
   h->view.E = h->E;
-  // E2 (FMIDX_LF_E2=1, off by default): the decode kernel's narrow rows read
+  // E2 (the lf_e2 option, off by default): the decode kernel's narrow rows read
   // their new range's content with the LF scan instead of streaming it after
   // the plan.  Measured (profiles/r02_cold_sweep/r02e2b_*): C3 13.5 vs 13.4 us
   // cold, C2 8.4 vs 8.5, C5 46.7 vs 48.1 -- the second array's cold misses
   // lengthen the scan about as much as the stream round trip it removes, so
   // its 4n bytes (17 GiB at C3) are not spent by default.
   h->view.E2 = nullptr;
-  if (env_u32("FMIDX_LF_E2", 0) != 0) {
+  if (h->opts.lf_e2 != 0) {
     if (dmalloc(&h->E2, n)) return -1;
     k_write_e2<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 18), kThreads, 0, s>>>(
         h->E, d_bwt, n, h->E2);

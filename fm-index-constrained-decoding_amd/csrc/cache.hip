@@ -36,10 +36,10 @@ struct PairHash {
   size_t operator()(const std::pair<uint64_t, uint64_t>& p) const { return (size_t)cache_hash(p.first, p.second); }
 };
 
-uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
-}
+#ifndef FMIDX_CACHE_STATS
+#define FMIDX_CACHE_STATS 0
+#endif
+constexpr bool kCacheStats = FMIDX_CACHE_STATS != 0;   // diagnostic build: cache construction statistics on stderr
 
 template <typename T>
 struct DBuf {
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
 }
 
 // Transition table of the cached ranges (all their children, or -- when that
-// would exceed FMIDX_TRANS_MB -- only the cached ones), built on the GPU from
+// would exceed the trans_mb budget -- only the cached ones), built on the GPU from
 // two k_distinct passes over the cached parents: one to count the entries,
 // one to insert them.
 int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>& nodes, hipStream_t s) {
@@ -132,9 +132,9 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   if (h->trans_tab) (void)hipFree(h->trans_tab);
   h->trans_tab = nullptr;
   h->trans_entries = h->trans_dropped = h->trans_bytes = 0;
-  const uint64_t mode = env_u64("FMIDX_TRANS", 2);   // 2 = every child, 1 = cached children only, 0 = none
+  const uint64_t mode = (uint64_t)h->opts.transitions;   // 2 = every child, 1 = cached children only, 0 = none
   if (mode == 0 || nodes.size() < 2 || !v.cache_mask) return 0;
-  const uint64_t budget = env_u64("FMIDX_TRANS_MB", 72ull << 10) << 20;
+  const uint64_t budget = h->opts.trans_mb << 20;
   const uint64_t sigma = (uint64_t)h->max_sym + 1;
   const uint64_t kChunkCap = 1ull << 26;   // child slots per k_distinct launch
   const uint64_t kChunkRows = 1ull << 20;
@@ -243,8 +243,8 @@ int device_build_cache(Index* h, hipStream_t s) {
   v.cblock = nullptr;
   v.cache_tab = nullptr;
   const uint64_t n = h->n;
-  const uint64_t Wc = std::max<uint64_t>(2, env_u64("FMIDX_CACHE_MIN", 4096));
-  const uint64_t budget = env_u64("FMIDX_CACHE_MB", 48ull << 10) << 20;
+  const uint64_t Wc = std::max<uint64_t>(2, h->opts.cache_min);
+  const uint64_t budget = h->opts.cache_mb << 20;
   const uint64_t words = v.bm_words;
   if (words == 0 || v.bm_levels == 0 || n < Wc || budget == 0) return 0;
   const uint64_t max_nodes = std::max<uint64_t>(1, budget / (words * 4));
@@ -323,7 +323,7 @@ int device_build_cache(Index* h, hipStream_t s) {
   }
   seen.clear();
 
-  if (env_u64("FMIDX_CACHE_STATS", 0)) {
+  if (kCacheStats) {
     // diagnostic: distinct symbols summed over the cached ranges, and their width histogram
     uint64_t sum = 0, maxk = 0, hist[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t wsum = 0, ksum_w[6] = {0, 0, 0, 0, 0, 0};   // distinct summed over parents of width < 8K,32K,128K,512K,2M,inf

@@ -56,7 +56,10 @@ constexpr uint32_t kMaxSliceTokens = 262144;  // 32 KB of LDS bits
 // LDS window words for a slice of sw tokens: the window starts at most 127
 // symbols before the slice (128-bit aligned) and ends 64 after it
 __host__ __device__ constexpr uint32_t win_words(uint64_t sw) { return (uint32_t)(sw / 32 + 16); }
-constexpr uint64_t kEarlyZeroWidth = 64;      // rows this narrow get their zeros written up front
+#ifndef FMIDX_EARLY_ZERO_WIDTH
+#define FMIDX_EARLY_ZERO_WIDTH 64   // measurement variant (make variant VFLAGS=-DFMIDX_EARLY_ZERO_WIDTH=512)
+#endif
+constexpr uint64_t kEarlyZeroWidth = FMIDX_EARLY_ZERO_WIDTH;   // rows this narrow get their zeros written up front
 constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
 constexpr uint32_t kPayMagic = 0x58534D46u;    // the shard payload's magic (csrc/shard.hip)
 constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144
@@ -853,12 +856,6 @@ __global__ void __launch_bounds__(256) k_cache_probe(DevView v, const uint64_t* 
   if ((threadIdx.x & 63u) == 0) out[i] = hit ? 1 : 0;
 }
 
-uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* s = std::getenv(name);
-  if (!s || !*s) return dflt;
-  return (uint32_t)std::strtoul(s, nullptr, 10);
-}
-
 }  // namespace
 
 // Workgroup size by batch: one 1024-thread workgroup per row while the rows
@@ -867,12 +864,16 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // chains overlap on each CU (measured at B = 2048: 49.6 us/step with 256
 // threads, 60.1 with 512, 79.1 with 1024, 71.4 with 128; B = 512: 15.2 /
 // 17.6 / 18.1 / 22.4; B = 256: 1024 and 256 threads x 4 slices tie at 10.4).
-// FMIDX_DEC_THREADS overrides.
+// The tuning's dec_threads overrides.
 static uint32_t decode_threads(uint64_t m) {
-  const uint32_t e = env_u32("FMIDX_DEC_THREADS", 0);
+  const uint32_t e = tuning().dec_threads;
   if (e == 256 || e == 512 || e == 1024) return e;
   return m <= 256 ? 1024 : 256;
 }
+
+#ifndef FMIDX_WAVE_BUDGET
+#define FMIDX_WAVE_BUDGET 4096   // measurement variant: resident waves the slice geometry aims at
+#endif
 
 // Slice geometry.  Residency budget: kernels of this shape keep about 16 waves
 // per CU resident (measured, profiles/r01_tuning); a launch of more waves than
@@ -880,11 +881,11 @@ static uint32_t decode_threads(uint64_t m) {
 // per row are chosen to keep rows * S * (threads / 64) waves within the
 // budget (default one slice per row at B >= 256), slices a multiple of 64 tokens.
 static void mask_geometry(uint64_t m, uint64_t vocab, uint32_t threads, uint32_t& S, uint32_t& SW) {
-  uint32_t s = env_u32("FMIDX_MASK_SLICES", 0);
+  uint32_t s = tuning().mask_slices;
   const uint64_t s_min = (vocab + kMaxSliceTokens - 1) / kMaxSliceTokens;
   if (s == 0) {
     const uint64_t rows = (m + 7) / 8 * 8;
-    const uint64_t budget = env_u32("FMIDX_WAVE_BUDGET", 4096);
+    const uint64_t budget = FMIDX_WAVE_BUDGET;
     const uint64_t want = std::max<uint64_t>(1, budget / (rows * (threads / 64)));
     const uint64_t max_s = std::max<uint64_t>(1, (vocab + 8191) / 8192);
     s = (uint32_t)std::min(want, max_s);
@@ -920,10 +921,7 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
     return -1;
   }
   const unsigned g = (unsigned)grid;
-  static const uint64_t ew = [] {
-    const char* e = std::getenv("FMIDX_EARLY_ZERO_WIDTH");
-    return (e && *e) ? (uint64_t)std::strtoull(e, nullptr, 10) : kEarlyZeroWidth;
-  }();
+  const uint64_t ew = kEarlyZeroWidth;
   const size_t lds = (size_t)win_words(SW) * 4;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \

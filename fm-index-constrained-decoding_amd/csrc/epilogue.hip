@@ -260,10 +260,11 @@ int launch_epilogue(int dtype, const void* scores, void* out, uint64_t B, uint64
     set_error("apply_boosts: B = %llu, V = %llu exceed 2^32", (unsigned long long)B, (unsigned long long)V);
     return -1;
   }
-  static const uint32_t chunks = [] {
-    const char* e = getenv("FMIDX_EPI_CHUNKS");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 1u;
-  }();
+  // chunks per thread: a measurement variant (make variant VFLAGS=-DFMIDX_EPI_CHUNKS=2); 1 measured fastest
+#ifndef FMIDX_EPI_CHUNKS
+#define FMIDX_EPI_CHUNKS 1
+#endif
+  const uint32_t chunks = FMIDX_EPI_CHUNKS;
   const RowParams* rp = reinterpret_cast<const RowParams*>(row_params);
   switch (dtype) {
     case 0: launch_epi_dt<float>(chunks, scores, out, B, V, lds, ldo, bits, ldb, uni, rp, eos, s); break;

@@ -628,8 +628,51 @@ struct SampleView {
 };
 
 // ---------------------------------------------------------------------------
+// Index-structure options (fm_build_options, include/fmidx.h), resolved: the
+// profile's values, then the caller's explicit fields, then the
+// FMIDX_BUILD_OPTIONS overrides ("key=value,..."; options.cpp).
+struct BuildOpts {
+  int32_t profile = 0;          // 0 default, 1 compact
+  int32_t transitions = 2;      // 0 none, 1 cached children only, 2 every child of a cached range
+  int32_t lf_e = 1;             // the E array
+  int32_t lf_e2 = 0;            // BWT[LF(i)] beside E
+  int32_t probe_first = 1;      // a cached range's LF step waits for its transition probe
+  int32_t keep_bwt = 0;         // keep the plain BWT although E holds its symbols
+  int32_t follow_bitmaps = 0;   // per-symbol C-block bitmaps
+  int32_t bm_log2 = -1;         // aligned bitmap block; -1: by n
+  uint64_t cache_min = 4096;    // range-bitmap cache threshold (rows)
+  uint64_t cache_mb = 48ull << 10;
+  uint64_t trans_mb = 72ull << 10;
+  uint64_t gpu_sort_min = 1ull << 20;
+};
+BuildOpts build_profile(int profile);
+// the FMIDX_BUILD_OPTIONS overrides applied to o (0, or -1 + set_error on a malformed string)
+int apply_build_overrides(BuildOpts& o);
+
+// Launch tuning of the query kernels, process-wide (fm_tuning): library
+// defaults, then fm_set_tuning, with FMIDX_TUNING overrides on top.
+struct Tuning {
+  uint32_t lf_group = 2;         // lanes per row of LF launches above lf_group_min rows (64 = never group)
+  uint32_t search_group = 1;     // the same for get_range launches
+  uint32_t dec_threads = 0;      // decode workgroup size; 0 = by batch
+  uint32_t mask_slices = 0;      // decode slices per row; 0 = by the wave budget
+  uint64_t lf_group_min = 8192;
+  int32_t lf_work = -1;          // -1 by row count, 0 grouped kernel, 1 worklist + tail, 2 in-wave sweep
+  int32_t lf_gprobe = 1;
+  int32_t lf_quad = 1;
+  int32_t lf_split = 0;
+  int32_t search_p8 = 1;
+  uint64_t lf_sweep_min = 1ull << 20;
+  uint64_t sa_chunk = 1ull << 29;
+};
+const Tuning& tuning();
+// replaces the process tuning (FMIDX_TUNING overrides on top); 0 or -1 + set_error
+int set_tuning(const Tuning& t);
+
+// ---------------------------------------------------------------------------
 // host-side owner of the device structures
 struct Index {
+  BuildOpts opts;                // resolved index-structure options (kept across release())
   int device = 0;
   hipStream_t stream = nullptr;  // internal stream for host-API calls
   DevView view{};

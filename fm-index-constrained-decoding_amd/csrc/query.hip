@@ -1324,45 +1324,39 @@ __global__ void __launch_bounds__(256) k_csr_pairs(const uint64_t* __restrict__ 
   }
 }
 
-uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* s = std::getenv(name);
-  if (!s || !*s) return dflt;
-  return (uint32_t)std::strtoul(s, nullptr, 10);
-}
-
-// LF / search launch variants, read from the environment once and again on
-// fm_reload_tuning() (tests select every variant in one process that way).
+// LF / search launch variants, from the process tuning (fm_tuning / fm_set_tuning;
+// tests select every variant in one process that way).
 //  * lanes per row: 64 (one wave per row) while the rows fit the chip's wave
 //    slots (latency: no row waits behind another's wide step), else
-//    FMIDX_LF_GROUP lanes (default 2; 64 = never group) above
-//    FMIDX_LF_GROUP_MIN rows (default 8192 = 256 CUs x 32 waves).  Measured on
+//    lf_group lanes (default 2; 64 = never group) above
+//    lf_group_min rows (default 8192 = 256 CUs x 32 waves).  Measured on
 //    the C3 index (tools/probe_rank.py, 2^19 pairs, cold): one wave per row
 //    308 us, G = 16 / 8 / 4 / 2 / 1: 179 / 125 / 99 / 90 / 100 us; get_range of
 //    2^18 patterns 2658 us -> 539 us at G = 2.
-//  * FMIDX_SEARCH_GROUP (default 1): the same for get_range launches
+//  * search_group (default 1): the same for get_range launches
 //    (k_search_group).  Since the wave-packed E scan (round 3), 2^18 patterns
 //    on the C3 index take 364 / 416 / 527 us cold at G = 1 / 2 / 4 (the LF
 //    step kernel: 79.2 / 77.3 / 79.4 us), so get_range groups one lane per row.
-//  * FMIDX_SEARCH_P8 (default 1): get_range at one lane per row probes its
+//  * search_p8 (default 1): get_range at one lane per row probes its
 //    cached wide rows eight per round trip (group_step<P8>, LDS-staged runs,
 //    123 VGPRs under a 4-wave cap) before the one-at-a-time loop: 2^18
 //    patterns 314-316 vs 367-374 us cold.  (The same stage in place of the
 //    four-row one of G = 2 LF launches measured no better: 75-87 vs 72-75 us.)
-//  * FMIDX_LF_GPROBE (default 1): grouped launches with G >= 4 probe the
+//  * lf_gprobe (default 1): grouped launches with G >= 4 probe the
 //    transition table inside the group, so a cached range's hit needs no
 //    wave-wide step.
-//  * FMIDX_LF_QUAD (default 1): G = 2 LF launches settle wide rows four at a
+//  * lf_quad (default 1): G = 2 LF launches settle wide rows four at a
 //    time (16 lanes each: a probe or a <= 128-row E scan) before the serial
 //    loop: 2^19 cold pairs 87 vs 93 us.  Not in k_search_group, where the extra
 //    registers (155 VGPRs: 3 waves per SIMD) cost more than it saves (565 vs
 //    548 us).
-//  * FMIDX_LF_SPLIT (default 0): 1 runs a G = 2 LF launch as two passes,
+//  * lf_split (default 0): 1 runs a G = 2 LF launch as two passes,
 //    k_lf_cheap (every row but the wide ones: 36 VGPRs, 8 waves per SIMD) then
 //    k_lf_wide (the wide rows only).  Exact, but slower at C3: 2^19 cold pairs
 //    98.4 vs 76.0 us (the second pass still steps wide rows a few per wave).
-//  * FMIDX_LF_WORK: 0 = the grouped kernel only, 1 / 2 = the worklist sweeps
-//    above (k_lf_sweep + k_lf_tail, or tail rows in-wave); unset = chosen by
-//    the launch's row count: the in-wave sweep from FMIDX_LF_SWEEP_MIN rows
+//  * lf_work: 0 = the grouped kernel only, 1 / 2 = the worklist sweeps
+//    above (k_lf_sweep + k_lf_tail, or tail rows in-wave); -1 = chosen by
+//    the launch's row count: the in-wave sweep from lf_sweep_min rows
 //    (default 2^20), the grouped kernel below.  Measured on the C3 index, cold
 //    / warm us (profiles/r03_rank/worklist/): 2^19 pairs 71.8 / 60.9 grouped vs
 //    76.6 / 47.7 in-wave; 2^20 126.6 / 109.5 vs 123.0 / 77.6; 2^21 216.4 / 202.4
@@ -1376,26 +1370,26 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
-  uint64_t sweep_min; // work_inline from this many rows (FMIDX_LF_WORK unset: 2^20; set: min_rows)
+  uint64_t sweep_min; // work_inline from this many rows (lf_work -1: lf_sweep_min; 2: min_rows)
   bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
 
 LfTuning load_lf_tuning() {
+  const Tuning& p = tuning();
   LfTuning t;
-  const uint32_t g = env_u32("FMIDX_LF_GROUP", 2);
+  const uint32_t g = p.lf_group;
   t.G = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : 64u;
-  const uint32_t gs = env_u32("FMIDX_SEARCH_GROUP", 1);
+  const uint32_t gs = p.search_group;
   t.Gs = (gs == 1 || gs == 2 || gs == 4 || gs == 8 || gs == 16) ? gs : 64u;
-  t.min_rows = env_u32("FMIDX_LF_GROUP_MIN", 8192);
-  t.gprobe = env_u32("FMIDX_LF_GPROBE", 1) != 0;
-  t.quad = env_u32("FMIDX_LF_QUAD", 1) != 0;
-  t.split = env_u32("FMIDX_LF_SPLIT", 0) != 0;
-  const char* w = std::getenv("FMIDX_LF_WORK");
-  const bool autow = !w || !*w;
-  t.work = !autow && env_u32("FMIDX_LF_WORK", 0) == 1;
-  t.work_inline = autow || env_u32("FMIDX_LF_WORK", 0) == 2;
-  t.sweep_min = autow ? env_u32("FMIDX_LF_SWEEP_MIN", 1u << 20) : 0;
-  t.search_p8 = env_u32("FMIDX_SEARCH_P8", 1) != 0;
+  t.min_rows = p.lf_group_min;
+  t.gprobe = p.lf_gprobe != 0;
+  t.quad = p.lf_quad != 0;
+  t.split = p.lf_split != 0;
+  const bool autow = p.lf_work < 0;
+  t.work = p.lf_work == 1;
+  t.work_inline = autow || p.lf_work == 2;
+  t.sweep_min = autow ? p.lf_sweep_min : 0;
+  t.search_p8 = p.search_p8 != 0;
   return t;
 }
 
@@ -1539,8 +1533,11 @@ int launch_distinct(const DevView& v, const uint64_t* lo, const uint64_t* hi, ui
   fr.hi[1] = fr.lo[1] + T;
   fr.pre[0] = reinterpret_cast<uint32_t*>(fr.hi[1] + T);
   fr.pre[1] = fr.pre[0] + T;
+#ifndef FMIDX_DISTINCT_CACHED
+#define FMIDX_DISTINCT_CACHED 1   // measurement variant: 0 = every range through the BFS
+#endif
   const bool cached_path = v.trans_cap && v.cache_mask && (min_count ? min_count : 1) == 1 &&
-                           env_u32("FMIDX_DISTINCT_CACHED", 1) != 0;
+                           FMIDX_DISTINCT_CACHED != 0;
   k_distinct<<<(unsigned)m, 256, 0, s>>>(v, lo, hi, m, cap_off, syms, counts, k, fr,
                                          min_count ? min_count : 1, child_lo, cached_path);
   FM_HIP(hipGetLastError());

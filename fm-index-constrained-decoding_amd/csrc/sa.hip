@@ -225,10 +225,6 @@ uint32_t bit_width_u64(uint64_t x) {
   return b;
 }
 
-uint64_t env_u64(const char* name, uint64_t dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::strtoull(v, nullptr, 10) : dflt;
-}
 
 }  // namespace
 
@@ -315,7 +311,7 @@ int gpu_suffix_sort(const uint32_t* text, uint64_t n, uint32_t* bwt_out, uint64_
     RP(hipStreamSynchronize(s));
   }
 
-  const uint64_t CH = std::max<uint64_t>(1024, env_u64("FMIDX_SA_CHUNK", 1ull << 29));
+  const uint64_t CH = std::max<uint64_t>(1024, tuning().sa_chunk);
   Buf<uint64_t> kin, kout, vin, vout, d_cnt, d_end;
   if (d_cnt.alloc(1) || d_end.alloc(1)) return -1;
   uint8_t* head = flag.p;

@@ -609,12 +609,12 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
 
 }  // namespace
 
-// FMIDX_OR_PERPART=0|1 (read per launch): the OR pass's sparse lists per part (1, the default)
-// or over one flat index space (0)
-static bool or_per_part() {
-  const char* e = std::getenv("FMIDX_OR_PERPART");
-  return !(e && *e && std::atoi(e) == 0);
-}
+// the OR pass's sparse lists per part (1, the default) or over one flat index space (0): a
+// measurement variant (make ... VFLAGS=-DFMIDX_OR_PERPART=0; tools/or_perpart_ab.sh)
+#ifndef FMIDX_OR_PERPART
+#define FMIDX_OR_PERPART 1
+#endif
+static bool or_per_part() { return FMIDX_OR_PERPART != 0; }
 
 uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab) {
   const uint64_t W = (vocab + 31) / 32;

@@ -41,6 +41,13 @@ SIGNATURES = {
     "fm_extract_text": (c_int, [c_void_p, c_uint64, c_uint64, u64p, c_uint64, u64p]),
     "fm_save": (c_int, [c_void_p, c_char_p]),
     "fm_load": (c_int, [POINTER(c_void_p), c_char_p, c_int]),
+    "fm_load_ex": (c_int, [POINTER(c_void_p), c_char_p, c_int, c_void_p]),
+    "fm_build_options_init": (c_int, [c_void_p, c_int]),
+    "fm_set_build_options": (c_int, [c_void_p, c_void_p]),
+    "fm_get_build_options": (c_int, [c_void_p, c_void_p]),
+    "fm_tuning_init": (c_int, [c_void_p]),
+    "fm_set_tuning": (c_int, [c_void_p]),
+    "fm_get_tuning": (c_int, [c_void_p]),
     "fm_lf_step_batch": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_uint64, c_void_p]),
     "fm_backward_search_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_int64, c_void_p,

@@ -85,10 +85,26 @@ def _stream_of(t) -> int:
 class FMIndex:
     """Drop-in for the SWIG proxy class ``cpp_modules.fm_index.FMIndex``."""
 
-    def __init__(self, device: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, options=None):
+        """``options``: the index structures this handle builds
+        (fmidx.options: a BuildOptions, a profile name -- "default" /
+        "compact" -- or a dict of fm_build_options fields; None = default)."""
+        from .options import as_build_options
+
         self._h = c_void_p()
         self._device = _default_device() if device is None else int(device)
         check(lib().fm_create(byref(self._h), self._device), "FMIndex()")
+        o = as_build_options(options)
+        if o is not None:
+            check(lib().fm_set_build_options(self._h, byref(o)), "set_build_options")
+
+    def build_options(self) -> dict:
+        """The fm_build_options in force on this handle (FMIDX_BUILD_OPTIONS applied)."""
+        from .options import BuildOptions
+
+        o = BuildOptions()
+        check(lib().fm_get_build_options(self._h, byref(o)), "get_build_options")
+        return o.as_dict()
 
     # -- lifecycle ----------------------------------------------------------
     def __del__(self):
@@ -244,7 +260,7 @@ class FMIndex:
         check(lib().fm_stats(self._h, *[byref(v) for v in vals]), "stats")
         keys = ["levels", "wm_bytes", "bwt_bytes", "bitmap_bytes", "bitmap_block"]
         out = {k: int(v.value) for k, v in zip(keys, vals)}
-        out["follow_bytes"] = int(os.environ.get("FMIDX_FOLLOW_BITMAPS", "0") != "0" and out["bitmap_block"] > 0)
+        out["follow_bytes"] = int(self.build_options()["follow_bitmaps"] != 0 and out["bitmap_block"] > 0)
         ex = [c_uint64() for _ in range(5)]
         check(lib().fm_stats_ex(self._h, *[byref(v) for v in ex]), "stats_ex")
         for k, v in zip(["lf_levels", "lf_wm_bytes", "cache_nodes", "cache_bytes", "cache_min"], ex):
@@ -509,18 +525,22 @@ class FMIndex:
         check(lib().fm_synchronize(self._h), "synchronize")
 
 
-def load_FMIndex(path: str, device: Optional[int] = None) -> FMIndex:
+def load_FMIndex(path: str, device: Optional[int] = None, options=None) -> FMIndex:
     """fm_index.cpp:201-209: this engine's own file (csrc/fileformat.h), or a
     reference ``.fmi`` (sdsl csa_wt_int<> serialisation, fmidx/sdsl_fmi.py --
-    parity unpinned: no sdsl file exists to test against)."""
+    parity unpinned: no sdsl file exists to test against).  ``options``: the
+    index structures to build (as FMIndex's)."""
+    from .options import as_build_options
     from .sdsl_fmi import is_sdsl_file, load_sdsl_fmi
 
     if os.path.isfile(path) and is_sdsl_file(path):
-        return load_sdsl_fmi(path, device)
+        return load_sdsl_fmi(path, device, options=options)
+    o = as_build_options(options)
     obj = FMIndex.__new__(FMIndex)
     obj._h = c_void_p()
     obj._device = _default_device() if device is None else int(device)
-    check(lib().fm_load(byref(obj._h), str(path).encode(), obj._device), "load_FMIndex")
+    check(lib().fm_load_ex(byref(obj._h), str(path).encode(), obj._device, byref(o) if o is not None else None),
+          "load_FMIndex")
     return obj
 
 

@@ -53,8 +53,8 @@ class FMIndex(_FMIndex):
     occurring_counts: List[int]
     labels: Optional[List[str]]
 
-    def __init__(self, device: Optional[int] = None):
-        super().__init__(device)
+    def __init__(self, device: Optional[int] = None, options=None):
+        super().__init__(device, options=options)
         self.beginnings = [0]
         self.occurring = set()
         self.occurring_distinct = []
@@ -176,9 +176,9 @@ class FMIndex(_FMIndex):
         return super().save(path + ".fmi")
 
     @classmethod
-    def load(cls, path: str, device: Optional[int] = None) -> "FMIndex":
-        """index.py:197-207."""
-        index = load_FMIndex(path + ".fmi", device)
+    def load(cls, path: str, device: Optional[int] = None, options=None) -> "FMIndex":
+        """index.py:197-207 (``options``: fmidx.options build options)."""
+        index = load_FMIndex(path + ".fmi", device, options=options)
         index.__class__ = cls
         index.beginnings, index.occurring, index.labels = read_oth(path + ".oth")
         index.occurring_distinct, index.occurring_counts = index.get_distinct_count(0, len(index))

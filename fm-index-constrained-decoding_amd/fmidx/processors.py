@@ -136,6 +136,9 @@ class _DeviceStep:
     overflows): the caller then runs the host path, which reproduces the
     reference's behaviour for such inputs."""
 
+    WAIT_STREAM = False    # measurement: wait for the whole call instead of the status event
+    VERIFY_HARD = False    # measurement: hard-mask calls read their status too
+
     def __init__(self, core: "_BatchedCore", boost: float, lrf: float, fdf: Optional[List[int]]):
         self.core = core
         self.index = core.index
@@ -158,12 +161,12 @@ class _DeviceStep:
         # The call's status is read after an event recorded right behind the row
         # bookkeeping (k_prep + the status copy), not after the whole call: the
         # mask and the epilogue are still running when the output is returned
-        # (torch's stream order covers its consumers).  FMIDX_PROC_WAIT=stream
-        # restores the full synchronize (measurement only).
+        # (torch's stream order covers its consumers).  WAIT_STREAM = True
+        # restores the full synchronize (measurement only: tools/bench_generate.py).
         self._ev = torch.cuda.Event()
         self._ev_ready = False
-        self._wait_stream = os.environ.get("FMIDX_PROC_WAIT", "event") == "stream"
-        self._verify = os.environ.get("FMIDX_PROC_VERIFY", "0") != "0"    # hard calls: read the status anyway
+        self._wait_stream = type(self).WAIT_STREAM
+        self._verify = type(self).VERIFY_HARD    # hard calls: read the status anyway
         # FMIDX_PROC_STATUS=deferred (opt-in, measurement of the wait's cost): a soft call returns
         # without waiting for its status; the status is checked at the next call (or check_pending())
         # and a call that needed the host path raises SpeculativeCallError there -- its output was

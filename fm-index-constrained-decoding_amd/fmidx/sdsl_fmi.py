@@ -336,7 +336,7 @@ def decode_wt_int_device(tree_words: np.ndarray, n: int, L: int, device, chunk: 
     return val
 
 
-def load_sdsl_fmi(path: str, device: Optional[int] = None, verify_samples: bool = True):
+def load_sdsl_fmi(path: str, device: Optional[int] = None, verify_samples: bool = True, options=None):
     """An engine FMIndex (fmidx.fm_index.FMIndex, the SWIG surface) from a
     reference ``.fmi`` file (see the module docstring; parity unpinned)."""
     import torch
@@ -360,7 +360,7 @@ def load_sdsl_fmi(path: str, device: Optional[int] = None, verify_samples: bool 
     del sym
     if int((bwt == 0).sum()) != 1:
         raise SdslFormatError(f"{path}: the decoded BWT must hold exactly one sentinel 0")
-    ix = FMIndex(device=dev_index)
+    ix = FMIndex(device=dev_index, options=options)
     ix.initialize_from_bwt_device(bwt)
     del bwt
     isa = torch.from_numpy(f.isa_samples.view(np.int64)).to(dev)

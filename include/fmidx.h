@@ -50,6 +50,68 @@ int fm_create(fm_index** out, int device);
 /* FMIndex::~FMIndex() -- fm_index.cpp:31 (frees host and device memory). */
 void fm_destroy(fm_index* h);
 
+/* ---- options ----------------------------------------------------------- */
+
+/* Which acceleration structures an index is built with (no reference
+ * counterpart: sdsl's csa_wt_int<> has one layout, fm_index.hpp:36).  Set on
+ * a handle before any fm_initialize* (or give it to fm_load_ex); the values
+ * in force are fm_get_build_options'.  fm_build_options_init fills a profile:
+ *   FM_PROFILE_DEFAULT -- every structure (117.9 GiB at n = 4.5e9, V = 128256;
+ *     13.8 us per cold B = 256 decode step);
+ *   FM_PROFILE_COMPACT -- transitions to cached children only, no E array,
+ *     the transition probe issued with the descent (54.3 GiB there, +24 % cold).
+ * Then change fields as needed.  An int field of -1 or a size field of 0 means
+ * "the profile's value".  The environment variable FMIDX_BUILD_OPTIONS
+ * ("key=value,...", keys = the field names) overrides the fields at
+ * fm_create / fm_set_build_options time (measurement runs). */
+#define FM_PROFILE_DEFAULT 0
+#define FM_PROFILE_COMPACT 1
+typedef struct fm_build_options {
+  uint32_t size;            /* sizeof(fm_build_options) (set by fm_build_options_init) */
+  int32_t profile;          /* FM_PROFILE_* */
+  int32_t transitions;      /* transition table: 0 none, 1 cached children only, 2 every child of a cached range */
+  int32_t lf_e;             /* 1: the E array (LF(i) | BWT[i]: one scan for the LF step of a narrow range) */
+  int32_t lf_e2;            /* 1: BWT[LF(i)] beside E (measured neutral: 0) */
+  int32_t probe_first;      /* 1: a cached range's LF step waits for its transition probe before any rank load */
+  int32_t keep_bwt;         /* 1: keep the plain BWT although E holds its symbols */
+  int32_t follow_bitmaps;   /* 1: a bitmap per symbol of its C-block (0: the range cache holds the wide ones) */
+  int32_t bm_log2;          /* aligned bitmap block, log2 rows; -1: by n (16 from 2^31 rows, 14 from 2^26, 12 below) */
+  int32_t reserved;
+  uint64_t cache_min;       /* range-bitmap cache: every SA range of >= cache_min rows reachable from the root (4096) */
+  uint64_t cache_mb;        /* its budget, MiB (48 GiB) */
+  uint64_t trans_mb;        /* the transition table's budget, MiB (72 GiB; past it: cached children only) */
+  uint64_t gpu_sort_min;    /* fm_initialize / fm_initialize_from_file sort on the GPU from this many rows (2^20) */
+} fm_build_options;
+int fm_build_options_init(fm_build_options* o, int profile);
+int fm_set_build_options(fm_index* h, const fm_build_options* o);
+int fm_get_build_options(const fm_index* h, fm_build_options* o);
+
+/* Launch tuning of the query kernels, process-wide (the measured defaults of
+ * DESIGN.md §4 from fm_tuning_init).  fm_set_tuning while no launch is being
+ * issued; FMIDX_TUNING ("key=value,...") overrides it for measurement runs,
+ * and fm_reload_tuning restores the defaults with those overrides. */
+typedef struct fm_tuning {
+  uint32_t size;            /* sizeof(fm_tuning) (set by fm_tuning_init) */
+  uint32_t lf_group;        /* lanes per row of LF launches above lf_group_min rows: 1, 2, 4, 8, 16; 64 never groups (2) */
+  uint32_t search_group;    /* the same for get_range launches (1) */
+  uint32_t dec_threads;     /* decode workgroup size 256 / 512 / 1024; 0 = by batch (1024 up to 256 rows, 256 beyond) */
+  uint32_t mask_slices;     /* vocabulary slices per decode row; 0 = by the resident-wave budget */
+  uint32_t reserved;
+  uint64_t lf_group_min;    /* grouped LF / get_range kernels above this many rows (8192) */
+  int32_t lf_work;          /* -1: the in-wave sweep from lf_sweep_min rows, else the grouped kernel; 0 grouped only;
+                               1 sweep + worklist tail; 2 in-wave sweep whenever grouped */
+  int32_t lf_gprobe;        /* groups of >= 4 lanes probe the transition table themselves (1) */
+  int32_t lf_quad;          /* two-lane LF launches settle wide rows four at a time first (1) */
+  int32_t lf_split;         /* two-pass LF launch, cheap rows then wide rows (0: measured slower) */
+  int32_t search_p8;        /* get_range probes cached wide rows eight per round trip (1) */
+  int32_t reserved2;
+  uint64_t lf_sweep_min;    /* see lf_work (2^20) */
+  uint64_t sa_chunk;        /* suffix sorter: rows per sort chunk (2^29) */
+} fm_tuning;
+int fm_tuning_init(fm_tuning* t);
+int fm_set_tuning(const fm_tuning* t);
+int fm_get_tuning(fm_tuning* t);
+
 /* ---- construction ------------------------------------------------------ */
 
 /* FMIndex::initialize(const vector<char_type>&) -- fm_index.cpp:33-41.
@@ -164,6 +226,8 @@ int fm_extract_text(fm_index* h, uint64_t begin, uint64_t end, uint64_t* out, ui
  * BWT + SA/ISA samples; everything else is rebuilt on load. */
 int fm_save(fm_index* h, const char* path);
 int fm_load(fm_index** out, const char* path, int device);
+/* fm_load with the index built under `options` (NULL: the defaults). */
+int fm_load_ex(fm_index** out, const char* path, int device, const fm_build_options* options);
 
 /* ---- batched hot path (device pointers, stream-ordered) ---------------- */
 
@@ -529,10 +593,9 @@ int fm_device_struct(const fm_index* h, int which, const void** out, uint64_t* b
 /* Synchronise the handle's device (hipDeviceSynchronize on its device). */
 int fm_synchronize(fm_index* h);
 
-/* Re-reads the launch-variant environment variables of the LF / get_range
- * launches (FMIDX_LF_GROUP, FMIDX_LF_GROUP_MIN, FMIDX_LF_GPROBE,
- * FMIDX_LF_QUAD), which are otherwise read once per process.  Call it while
- * no launch is being issued (tuning and tests).  No reference counterpart. */
+/* Restores the launch tuning to the library defaults with the FMIDX_TUNING
+ * overrides (re-read) on top.  Call it while no launch is being issued.  No
+ * reference counterpart. */
 int fm_reload_tuning(void);
 
 #ifdef __cplusplus

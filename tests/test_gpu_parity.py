@@ -19,23 +19,15 @@ def dev():
     return torch.device("cuda:0")
 
 
-def ours_index(docs, bm_log2=None, cache_min=None, trans=None):
+def ours_index(docs, bm_log2=None, cache_min=None, trans=None, **options):
+    """The engine index of ``docs`` built with fm_build_options fields
+    (fmidx.options; small thresholds make every acceleration structure exist
+    on a small corpus)."""
     from fmidx.index import FMIndex
 
-    env = {"FMIDX_BM_LOG2": bm_log2, "FMIDX_CACHE_MIN": cache_min, "FMIDX_TRANS": trans}
-    old = {k: os.environ.get(k) for k in env}
-    for k, val in env.items():
-        if val is not None:
-            os.environ[k] = str(val)
-    try:
-        idx = FMIndex(device=0)
-        idx.initialize(docs, in_memory=True)
-    finally:
-        for k, val in old.items():
-            if val is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = val
+    opts = {"bm_log2": bm_log2, "cache_min": cache_min, "transitions": trans, **options}
+    idx = FMIndex(device=0, options={k: v for k, v in opts.items() if v is not None})
+    idx.initialize(docs, in_memory=True)
     return idx
 
 
@@ -54,21 +46,18 @@ def markov_docs(seed, n_docs, vocab, max_len, sticky=0.7):
 
 
 # ---------------------------------------------------------------- golden
-@pytest.mark.parametrize("gpu_sort_min", [None, "1"])
-def test_golden_index_cases(dev, golden_index_cases, gpu_sort_min, monkeypatch):
+@pytest.mark.parametrize("gpu_sort_min", [None, 1])
+def test_golden_index_cases(dev, golden_index_cases, gpu_sort_min):
     """gpu_sort_min=1: FMIndex.initialize sorts every corpus on the GPU (the
     path of corpora >= 2^20 tokens); locate / extract / get_doc go through the
     SA / ISA samples and LF walks either way."""
     from fmidx.index import FMIndex
 
-    if gpu_sort_min is not None:
-        monkeypatch.setenv("FMIDX_GPU_SORT_MIN", gpu_sort_min)
-
     checked = 0
     for case in golden_index_cases:
         if "docs" not in case:
             continue
-        idx = FMIndex(device=0)
+        idx = FMIndex(device=0, options={"gpu_sort_min": gpu_sort_min} if gpu_sort_min else None)
         idx.initialize(case["docs"], in_memory=case["in_memory"])
         name = case["name"]
         assert idx.size() == case["n"], name
@@ -274,39 +263,33 @@ def _grouped_case(cache_min):
 # every launch variant of the LF kernels (csrc/query.hip lf_tuning): the grouped
 # kernels -- lanes per row, the in-group transition probe (G >= 4), the
 # four-at-a-time wide stage (G = 2) -- and the opt-in worklist sweeps
-_GROUPED_VARIANTS = [{}, {"FMIDX_LF_GROUP": "1"}, {"FMIDX_LF_QUAD": "0"}, {"FMIDX_LF_SPLIT": "1"},
-                     {"FMIDX_LF_SPLIT": "1", "FMIDX_LF_QUAD": "0"}, {"FMIDX_SEARCH_GROUP": "2"},
-                     {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "0"},
-                     {"FMIDX_LF_GROUP": "4", "FMIDX_SEARCH_GROUP": "4", "FMIDX_LF_GPROBE": "1"},
-                     {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "0"},
-                     {"FMIDX_LF_GROUP": "8", "FMIDX_SEARCH_GROUP": "8", "FMIDX_LF_GPROBE": "1"},
-                     {"FMIDX_LF_GROUP": "16", "FMIDX_SEARCH_GROUP": "16"},
-                     {"FMIDX_LF_GROUP": "64", "FMIDX_SEARCH_GROUP": "64"}]
-_LF_VARIANTS = _GROUPED_VARIANTS + [{"FMIDX_LF_WORK": "1"}, {"FMIDX_LF_WORK": "2"}, {"FMIDX_SEARCH_P8": "0"}]
+_GROUPED_VARIANTS = [{}, {"lf_group": 1}, {"lf_quad": 0}, {"lf_split": 1},
+                     {"lf_split": 1, "lf_quad": 0}, {"search_group": 2},
+                     {"lf_group": 4, "search_group": 4, "lf_gprobe": 0},
+                     {"lf_group": 4, "search_group": 4, "lf_gprobe": 1},
+                     {"lf_group": 8, "search_group": 8, "lf_gprobe": 0},
+                     {"lf_group": 8, "search_group": 8, "lf_gprobe": 1},
+                     {"lf_group": 16, "search_group": 16},
+                     {"lf_group": 64, "search_group": 64}]
+_LF_VARIANTS = _GROUPED_VARIANTS + [{"lf_work": 0}, {"lf_work": 1}, {"lf_work": 2}, {"search_p8": 0}]
 
 
-@pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k[6:]}{x}" for k, x in v.items()) or "default")
+@pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k}{x}" for k, x in v.items()) or "default")
 @pytest.mark.parametrize("cache_min", [None, 4])
-def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
-    """Launches above FMIDX_LF_GROUP_MIN (8192) rows take the grouped kernels
+def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant):
+    """Launches above lf_group_min (8192) rows take the grouped kernels
     (G lanes per row, wide rows by the whole wave): get_range of 20011
     patterns (index.py:103-114 with its early exit) and one LF step of 20011
     (state, token) pairs, against the oracle -- dead, empty, full-range,
     narrow, wide and cached rows, unknown ids, hi past n, reset rows -- for
-    every launch variant (selected through fm_reload_tuning in this process)."""
+    every launch variant (selected through fm_set_tuning in this process)."""
     import torch
 
-    from fmidx._lib import lib
+    from fmidx.options import tuning
 
     ours, pats, want, nxt, li, hv, want_lf = _grouped_case(cache_min)
     m = len(pats)
-    for k in ("FMIDX_LF_GROUP", "FMIDX_SEARCH_GROUP", "FMIDX_LF_GPROBE", "FMIDX_LF_QUAD", "FMIDX_LF_SPLIT",
-              "FMIDX_LF_WORK", "FMIDX_SEARCH_P8"):
-        monkeypatch.delenv(k, raising=False)
-    for k, x in variant.items():
-        monkeypatch.setenv(k, x)
-    lib().fm_reload_tuning()
-    try:
+    with tuning(**variant):
         toks = torch.tensor([t for p in pats for t in p], dtype=torch.int64, device=dev)
         offs = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pats])]), dtype=torch.int64, device=dev)
         lo = torch.zeros(m, dtype=torch.int64, device=dev)
@@ -328,9 +311,6 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant, monkeypatch):
         got = list(zip(lo_in.cpu().tolist(), hi_in.cpu().tolist()))
         bad = [i for i in range(m) if got[i] != want_lf[i]]
         assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
-    finally:
-        monkeypatch.undo()
-        lib().fm_reload_tuning()
 
 
 @pytest.mark.parametrize("cache_min", [None, 4])
@@ -366,14 +346,13 @@ def test_small_lf_batches_vs_oracle(dev, cache_min):
 
 
 @pytest.mark.parametrize("cache_min,e2", [(None, "0"), (4, "0"), (None, "1"), (4, "1")])
-def test_decode_step_fused_and_reset(dev, cache_min, e2, monkeypatch):
+def test_decode_step_fused_and_reset(dev, cache_min, e2):
     """Fused LF + mask against the oracle, with and without E2 (the narrow
     rows' content read with their E scan instead of streamed afterwards)."""
     import torch
 
-    monkeypatch.setenv("FMIDX_LF_E2", e2)
     docs = markov_docs(11, 80, 40, 90)
-    ours = ours_index(docs, bm_log2=5, cache_min=cache_min)
+    ours = ours_index(docs, bm_log2=5, cache_min=cache_min, lf_e2=int(e2))
     ora = OracleIndex()
     ora.initialize(docs, in_memory=True)
     n = ora.size()
@@ -406,7 +385,7 @@ def test_decode_step_fused_and_reset(dev, cache_min, e2, monkeypatch):
                                                        (256, None, 512, 12), (64, None, 256, 12),
                                                        (64, None, None, 151936), (64, None, 256, 151936),
                                                        (None, None, None, 128256)])
-def test_decode_step_wide_ranges(dev, cache_min, trans, threads, V, monkeypatch):
+def test_decode_step_wide_ranges(dev, cache_min, trans, threads, V):
     """Decode steps through every LF path of the fused kernel: the workgroup
     E scan (uncached ranges of 513..4096 rows), the transition table (cached
     parents -> any child, incl. one-row children and cached children), the
@@ -419,8 +398,15 @@ def test_decode_step_wide_ranges(dev, cache_min, trans, threads, V, monkeypatch)
         r2 = np.random.default_rng(7)
         docs = [[t if r2.random() < 0.7 else int(r2.integers(8, V - 10)) for t in d] for d in docs]
     ours = ours_index(docs, bm_log2=6, cache_min=cache_min, trans=trans)
-    if threads is not None:     # workgroup size of the decode kernel (default by batch)
-        monkeypatch.setenv("FMIDX_DEC_THREADS", str(threads))
+    from fmidx.options import tuning
+
+    with tuning(dec_threads=threads or 0):     # workgroup size of the decode kernel (0: by batch)
+        _decode_wide_ranges(dev, ours, docs, cache_min, trans, V)
+
+
+def _decode_wide_ranges(dev, ours, docs, cache_min, trans, V):
+    import torch
+
     st = ours.stats()
     if trans != 0 and st["cache_nodes"] > 1:
         assert st["trans_entries"] > 0
@@ -639,16 +625,15 @@ def _sa_cases():
 @pytest.mark.parametrize("chunk", [None, "1024"])
 def test_gpu_suffix_sort_vs_oracle(dev, chunk):
     """fm_suffix_sort_device == suffix sorting by definition, including the
-    multi-chunk and larger-than-a-chunk group paths (FMIDX_SA_CHUNK=1024)."""
+    multi-chunk and larger-than-a-chunk group paths (tuning sa_chunk = 1024)."""
     import torch
 
     from fmidx.fm_index import suffix_sort_device
     from oracle.fm_oracle import suffix_array
 
-    old = os.environ.get("FMIDX_SA_CHUNK")
-    if chunk:
-        os.environ["FMIDX_SA_CHUNK"] = chunk
-    try:
+    from fmidx.options import tuning
+
+    with tuning(sa_chunk=int(chunk) if chunk else 1 << 29):
         for name, t in _sa_cases().items():
             text = np.asarray(t, dtype=np.int64)
             want = suffix_array(text)
@@ -658,12 +643,6 @@ def test_gpu_suffix_sort_vs_oracle(dev, chunk):
             n = text.size
             want_bwt = text[(want + n - 1) % n]
             assert np.array_equal(bwt.cpu().numpy(), want_bwt.astype(np.int32)), name
-    finally:
-        if chunk:
-            if old is None:
-                del os.environ["FMIDX_SA_CHUNK"]
-            else:
-                os.environ["FMIDX_SA_CHUNK"] = old
 
 
 def test_gpu_suffix_sort_rejects_bad_sentinel(dev):
@@ -724,15 +703,10 @@ def test_gpu_suffix_sort_at_scale_matches_doubling(dev):
 
     text, _ = markov_corpus_gpu(50_000_000, 128256, 99, dev)
     want = bwt_from_sa(text, suffix_array_gpu(text))
-    old = os.environ.get("FMIDX_SA_CHUNK")
-    os.environ["FMIDX_SA_CHUNK"] = str(1 << 22)
-    try:
+    from fmidx.options import tuning
+
+    with tuning(sa_chunk=1 << 22):
         got, _ = suffix_sort_device(text)
-    finally:
-        if old is None:
-            del os.environ["FMIDX_SA_CHUNK"]
-        else:
-            os.environ["FMIDX_SA_CHUNK"] = old
     assert torch.equal(got, want)
 
 

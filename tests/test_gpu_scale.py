@@ -79,9 +79,18 @@ def _decode_vs_cpu_ref(ix, B, S, seed, dev, threads=None, monkeypatch=None):
 
     from fmidx.synth import decode_trace
 
+    from fmidx.options import tuning
+
+    with tuning(dec_threads=threads or 0):
+        return _decode_vs_cpu_ref_body(ix, B, S, seed, dev)
+
+
+def _decode_vs_cpu_ref_body(ix, B, S, seed, dev):
+    import torch
+
+    from fmidx.synth import decode_trace
+
     fm, text, bwt, ref = ix["fm"], ix["text"], ix["bwt"], ix["ref"]
-    if threads is not None:
-        monkeypatch.setenv("FMIDX_DEC_THREADS", str(threads))
     tokens, init, _, _, _ = decode_trace(fm, text, bwt, B, V, S, seed, dev)
     lo, hi = init[0].clone(), init[1].clone()
     clo = init[0].cpu().numpy().astype(np.uint64)
@@ -443,7 +452,7 @@ def test_c2_bwt_equals_host_sais(dev, c2, monkeypatch):
     the BWT from the host SA-IS sorter (csrc/sais.h, induced sorting: no code
     shared with the GPU path), taken through the reference's own construction
     entry point FMIndex.initialize (fm_index.cpp:33-41) with the GPU sort
-    switched off (FMIDX_GPU_SORT_MIN above n).  The host build's SA samples
+    switched off (the gpu_sort_min build option above n).  The host build's SA samples
     come from the host suffix array, so locate of 2^20 random rows must agree
     as well.  A heartbeat line every 30 s keeps the run visibly alive."""
     import threading
@@ -456,8 +465,7 @@ def test_c2_bwt_equals_host_sais(dev, c2, monkeypatch):
     text, bwt_gpu = c2["text"], c2["bwt"]
     n = text.numel()
     body = text[:-1].to(torch.int64).cpu().numpy().astype(np.uint64)
-    monkeypatch.setenv("FMIDX_GPU_SORT_MIN", str(1 << 40))
-    host = FMIndex(device=0)
+    host = FMIndex(device=0, options={"gpu_sort_min": 1 << 40})
     err = []
 
     def run():

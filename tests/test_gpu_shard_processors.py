@@ -35,29 +35,19 @@ def _corpus(seed):
 
 @pytest.fixture(scope="module")
 def indexes():
-    import os
-
     from fmidx.index import FMIndex
     from fmidx.sharding import shard_corpus
 
     docs = _corpus(3)
-    old = {k: os.environ.get(k) for k in ("FMIDX_CACHE_MIN", "FMIDX_BM_LOG2")}
-    os.environ.update({"FMIDX_CACHE_MIN": "8", "FMIDX_BM_LOG2": "6"})   # cache / transitions / hierarchy exist
-    try:
-        full = FMIndex()
-        full.initialize(docs, in_memory=True)
-        shards = []
-        for r in range(WORLD):
-            sd, _ = shard_corpus(docs, WORLD, r, HALO)
-            ix = FMIndex()
-            ix.initialize(sd, in_memory=True)
-            shards.append(ix)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    opts = {"cache_min": 8, "bm_log2": 6}   # cache / transitions / hierarchy exist on a small corpus
+    full = FMIndex(options=opts)
+    full.initialize(docs, in_memory=True)
+    shards = []
+    for r in range(WORLD):
+        sd, _ = shard_corpus(docs, WORLD, r, HALO)
+        ix = FMIndex(options=opts)
+        ix.initialize(sd, in_memory=True)
+        shards.append(ix)
     assert full.stats()["cache_nodes"] > 1
     return docs, full, shards
 

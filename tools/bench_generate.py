@@ -7,7 +7,7 @@
   Causal processor, Qwen3-0.6B (vocab 151936) with the Qwen processor -- 128
   prompts x 2 beams, N new tokens; ms per decode step without a processor,
   with the device path (status event wait, the default), with the device path
-  waiting for the whole call (FMIDX_PROC_WAIT=stream, round 2's behaviour) and
+  waiting for the whole call (_DeviceStep WAIT_STREAM, round 2's behaviour) and
   with the host path of the same class.  A wrapper times every processor call
   (host wall clock, the call returning).
 * vLLM V0's per-sequence hook (/root/reference/index_for_vllm.py:31-32,

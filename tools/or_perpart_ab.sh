@@ -1,4 +1,5 @@
 #!/bin/bash
+# (round 5: FMIDX_OR_PERPART is a compile-time variant now -- make ... VFLAGS=-DFMIDX_OR_PERPART=0 and FMIDX_LIB)
 # The OR pass's sparse lists per part (FMIDX_OR_PERPART=1) vs over one flat index space (0):
 # GPU tests of the exchange, the synthetic OR micro-bench and the C4 rehearsal, both ways.
 set -euo pipefail

@@ -39,6 +39,6 @@ for packed in (False, True):
         b.record()
         torch.cuda.synchronize()
         ts.append(a.elapsed_time(b) / K * 1e3)
-    print(f"floor B={B} slices={os.environ.get('FMIDX_MASK_SLICES', 'auto')} lib={os.environ.get('FMIDX_LIB', '')[-20:]} "
+    print(f"floor B={B} slices={os.environ.get('FMIDX_TUNING', 'auto')} lib={os.environ.get('FMIDX_LIB', '')[-20:]} "
           f"({'packed' if packed else 'uint8'} mask, all rows empty): {min(ts):.1f} us/step "
           f"(median {sorted(ts)[2]:.1f})", flush=True)

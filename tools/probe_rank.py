@@ -47,7 +47,7 @@ def main():
     fm, text, bwt, _ = bench.build_index(int(args.tokens), args.vocab, 20250905, dev)
     n = bwt.numel()
     st = fm.stats()
-    st["lf_e"] = os.environ.get("FMIDX_LF_E", "1") != "0"
+    st["lf_e"] = fm.build_options()["lf_e"] != 0
     stream = torch.cuda.current_stream(dev).cuda_stream
     sink = torch.zeros(1024, dtype=torch.int64, device=dev)
     flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
@@ -139,12 +139,13 @@ def main():
         torch.cuda.empty_cache()
 
     # ---- the last (largest) launch split by LF path: one grouped launch per class
-    # (FMIDX_LF_GROUP_MIN=0 through fm_reload_tuning, so even a small class takes the
+    # (tuning lf_group_min = 0 through fm_set_tuning, so even a small class takes the
     # grouped kernel), each cold, bytes by the LF plan.  With tools/pmc_rank.sh the
     # LAST len(by_path) k_lf_group dispatches are these, in this order.
     if args.by_path:
-        os.environ["FMIDX_LF_GROUP_MIN"] = "0"
-        lib().fm_reload_tuning()
+        from fmidx.options import set_tuning
+
+        old_tuning = set_tuning(lf_group_min=0)
         R = 1 << max(int(x) for x in args.rows_log2.split(",") if x)
         S = args.steps
         tokens, _, lo_h, hi_h, _ = decode_trace(fm, text, bwt, max(1, R // (S - 1)), args.vocab, S, 777, dev)
@@ -187,8 +188,7 @@ def main():
             res["by_path"].append(e)
             print(f"by path {name:22s} {e['rows']:7d} rows {us:8.1f} us {e['GBps']:7.0f} GB/s "
                   f"({by.sum() / max(1, e['rows']):.0f} B/row), exact {ok}", flush=True)
-        del os.environ["FMIDX_LF_GROUP_MIN"]
-        lib().fm_reload_tuning()
+        set_tuning(old_tuning)
 
     # ---- get_range (k_search) over P true patterns of U{1..32} tokens
     P = args.patterns

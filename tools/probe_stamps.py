@@ -31,9 +31,9 @@ dl = lib()
 dl.fm_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
 T = 1024                       # kDecThreads (decode.hip)
-S = int(os.environ.get("FMIDX_MASK_SLICES", "0"))
+S = int(os.environ.get("MASK_SLICES", "0"))
 if S == 0:                     # mirrors mask_geometry() in decode.hip
-    want = max(1, int(os.environ.get("FMIDX_WAVE_BUDGET", "4096")) // (((B + 7) // 8 * 8) * (T // 64)))
+    want = max(1, int("4096") // (((B + 7) // 8 * 8) * (T // 64)))
     S = min(want, max(1, (V + 8191) // 8192))
 SW = min(262144, (((V + S - 1) // S) + 63) & ~63)
 S = (V + SW - 1) // SW

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (round 5: FMIDX_EPI_CHUNKS is a compile-time variant now -- make ... VFLAGS=-DFMIDX_EPI_CHUNKS=2)
 # Epilogue chunks per thread (FMIDX_EPI_CHUNKS), one process each:
 # tools/bench_epilogue.py lines per variant into $1.
 set -uo pipefail
