@@ -36,7 +36,7 @@ void Index::release() {
   // no kernel on any stream may still read what is freed here (the callers
   // hold the handle's device)
   (void)hipDeviceSynchronize();
-  void* ptrs[] = {wm, sb, Z, D, C, bwt, bwt_view, bm, bm_full, bm_follow, sa, text, ws};
+  void* ptrs[] = {C, bwt, bwt_view, bm, bm_full, bm_follow, sa, text, ws};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int l = 0; l < kW2MaxLevels; ++l) {
@@ -69,13 +69,9 @@ void Index::release() {
   w2_Z = nullptr;
   D2 = nullptr;
   w2_bytes = 0;
-  wm = nullptr;
-  sb = nullptr;
-  Z = nullptr;
   bm_full = nullptr;
   bm_follow = nullptr;
   follow_bytes = 0;
-  D = nullptr;
   C = nullptr;
   bwt = nullptr;
   bwt_view = nullptr;
@@ -945,6 +941,7 @@ fmidx::BuildOpts to_internal(const fm_build_options& o) {
   if (o.keep_bwt >= 0) x.keep_bwt = o.keep_bwt;
   if (o.follow_bitmaps >= 0) x.follow_bitmaps = o.follow_bitmaps;
   if (o.bm_log2 >= 0) x.bm_log2 = o.bm_log2;
+  if (o.trans_min > 0) x.trans_min = o.trans_min;
   if (o.cache_min) x.cache_min = o.cache_min;
   if (o.cache_mb) x.cache_mb = o.cache_mb;
   if (o.trans_mb) x.trans_mb = o.trans_mb;
@@ -962,7 +959,7 @@ void to_public(const fmidx::BuildOpts& x, fm_build_options* o) {
   o->keep_bwt = x.keep_bwt;
   o->follow_bitmaps = x.follow_bitmaps;
   o->bm_log2 = x.bm_log2;
-  o->reserved = 0;
+  o->trans_min = x.trans_min;
   o->cache_min = x.cache_min;
   o->cache_mb = x.cache_mb;
   o->trans_mb = x.trans_mb;
@@ -973,8 +970,8 @@ bool valid(const fmidx::BuildOpts& x) {
   auto b = [](int32_t v) { return v == 0 || v == 1; };
   if ((x.profile != FM_PROFILE_DEFAULT && x.profile != FM_PROFILE_COMPACT) || x.transitions < 0 ||
       x.transitions > 2 || !b(x.lf_e) || !b(x.lf_e2) || !b(x.probe_first) || !b(x.keep_bwt) ||
-      !b(x.follow_bitmaps) || x.bm_log2 < -1 || x.bm_log2 > 30 || x.cache_min < 2) {
-    set_error("build options: profile 0/1, transitions 0..2, switches 0/1, bm_log2 -1..30, cache_min >= 2");
+      !b(x.follow_bitmaps) || x.bm_log2 < -1 || x.bm_log2 > 30 || x.cache_min < 2 || x.trans_min < 1) {
+    set_error("build options: profile 0/1, transitions 0..2, switches 0/1, bm_log2 -1..30, cache_min >= 2, trans_min >= 1");
     return false;
   }
   return true;
@@ -1282,9 +1279,9 @@ int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, u
   if (sample_bytes) *sample_bytes = x.samp_bytes;
   if (total_bytes)
     // (cache_bytes already holds the transition table: build_transitions adds it there)
-    *total_bytes = x.wm_bytes + (x.bwt ? x.n * 4 : 0) + x.bm_bytes + x.follow_bytes +
+    *total_bytes = (x.bwt ? x.n * 4 : 0) + x.bm_bytes + x.follow_bytes +
                    (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0) + x.w2_bytes + e + x.cache_bytes + x.samp_bytes +
-                   (x.sa ? x.n * 8 : 0) + (x.text ? x.n * 4 : 0) + 3 * K * 8;
+                   (x.sa ? x.n * 8 : 0) + (x.text ? x.n * 4 : 0) + 2 * K * 8;
   return 0;
   FM_API_END
 }
@@ -1294,8 +1291,8 @@ int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* 
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
   const auto& x = h->idx;
-  if (levels) *levels = x.NL;
-  if (wm_bytes) *wm_bytes = x.wm_bytes;
+  if (levels) *levels = x.view.NL2;   // the one wavelet matrix: the 2-level one
+  if (wm_bytes) *wm_bytes = x.w2_bytes;
   if (bwt_bytes) *bwt_bytes = x.bwt ? x.n * 4 : 0;
   if (bitmap_bytes) *bitmap_bytes = x.bm_bytes + x.follow_bytes + (x.bm_full ? (uint64_t)x.view.bm_words * 4 : 0);
   if (bitmap_block) *bitmap_block = x.view.bm_levels ? (1ull << x.view.bm_log2) : 0;

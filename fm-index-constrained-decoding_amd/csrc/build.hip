@@ -107,95 +107,6 @@ __global__ void __launch_bounds__(kThreads) k_chunk_scan(const uint64_t* __restr
   if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == kThreads - 1) *total = ex;
 }
 
-// ---- 16-ary wavelet matrix ------------------------------------------------
-// One wave per 192-digit rank block (3 chunks of 64 lanes).
-
-__device__ __forceinline__ uint32_t digit_at(const uint32_t* __restrict__ cur, uint64_t i, uint64_t n,
-                                             uint32_t shift) {
-  return i < n ? ((cur[i] >> shift) & 15u) : 16u;   // 16 = past the end
-}
-
-// per-block digit histogram, digit-major: hist[d * nblk + b]
-__global__ void __launch_bounds__(kThreads) k_hist16(const uint32_t* __restrict__ cur, uint64_t n,
-                                                    uint32_t shift, uint64_t* __restrict__ hist,
-                                                    uint64_t nblk) {
-  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (b >= nblk) return;
-  const uint32_t lane = lane_id();
-  uint32_t mine = 0;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const uint32_t d = digit_at(cur, b * kBlkDigits + (uint64_t)c * 64 + lane, n, shift);
-#pragma unroll
-    for (uint32_t dd = 0; dd < 16; ++dd) {
-      const uint32_t k = (uint32_t)__popcll(__ballot(d == dd));
-      if (lane == dd) mine += k;
-    }
-  }
-  if (lane < 16) hist[(uint64_t)lane * nblk + b] = mine;
-}
-
-// Write the rank block (header + packed digits), the superblock counts, and
-// stable-partition the level by digit: dest = base[d][b] + rank within block.
-__global__ void __launch_bounds__(kThreads) k_level16(const uint32_t* __restrict__ cur,
-                                                     uint32_t* __restrict__ nxt, uint64_t n,
-                                                     uint32_t shift, const uint64_t* __restrict__ base,
-                                                     uint64_t nblk, uint4* __restrict__ blocks,
-                                                     uint64_t* __restrict__ sbc, uint64_t nsb) {
-  const uint64_t b = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (b >= nblk) return;
-  const uint32_t lane = lane_id();
-  uint8_t* blk = reinterpret_cast<uint8_t*>(blocks + b * kBlkU4);
-  const uint64_t b_sb = (b / kSbBlocks) * kSbBlocks;
-  // header + superblock counts: lane d handles digit d
-  uint64_t my_base = 0;
-  if (lane < 16) {
-    my_base = base[(uint64_t)lane * nblk + b];
-    const uint64_t sb_start = base[(uint64_t)lane * nblk + b_sb];
-    reinterpret_cast<uint16_t*>(blk)[lane] = (uint16_t)(my_base - sb_start);
-    if (b == b_sb) sbc[(b / kSbBlocks) * kRadix + lane] = sb_start - base[(uint64_t)lane * nblk];
-  }
-  // payload: lane j < 48 packs digits 4j..4j+3 into two bytes
-  if (lane < 48) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint32_t d = digit_at(cur, b * kBlkDigits + 4 * lane + t, n, shift);
-      v |= (d & 15u) << (4 * t);
-    }
-    reinterpret_cast<uint16_t*>(blk + 32)[lane] = (uint16_t)v;
-  }
-  // partition
-  uint32_t run = 0;   // lane d: digits d seen so far in this block
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const uint64_t i = b * kBlkDigits + (uint64_t)c * 64 + lane;
-    const bool valid = i < n;
-    const uint32_t v = valid ? cur[i] : 0u;
-    const uint32_t d = valid ? ((v >> shift) & 15u) : 16u;
-    uint64_t same = __ballot(valid);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint64_t bt = __ballot((d >> t) & 1u);
-      same &= ((d >> t) & 1u) ? bt : ~bt;
-    }
-    const uint32_t within = (uint32_t)__popcll(same & below);
-    const uint64_t bd = __shfl(my_base, (int)(d & 15u), 64);
-    const uint32_t rd = (uint32_t)__shfl((int)run, (int)(d & 15u), 64);
-    if (valid) nxt[bd + rd + within] = v;
-#pragma unroll
-    for (uint32_t dd = 0; dd < 16; ++dd) {
-      const uint32_t k = (uint32_t)__popcll(__ballot(d == dd));
-      if (lane == dd) run += k;
-    }
-  }
-}
-
-__global__ void k_gather_z(const uint64_t* __restrict__ base, uint64_t nblk, uint64_t* __restrict__ z) {
-  if (threadIdx.x < 16) z[threadIdx.x] = base[(uint64_t)threadIdx.x * nblk];
-}
-
 __global__ void k_max_sym(const uint32_t* __restrict__ a, uint64_t n, uint32_t* __restrict__ out) {
   uint32_t m = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -491,64 +402,16 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     set_error("symbol %u too large (max %d bits)", max_sym, kMaxLevels);
     return -1;
   }
-  const uint64_t K = 1ull << L;
-  const uint32_t NL = (L + 3) / 4;
-  const uint64_t nblk = n / kBlkDigits + 1;
-  const uint64_t nsb = nblk / kSbBlocks + 1;
-
-  // -- 16-ary wavelet matrix
-  uint4* wm = nullptr;
-  uint64_t* sbc = nullptr;
-  uint64_t* Zd = nullptr;
-  uint32_t *cur = nullptr, *nxt = nullptr;
-  uint64_t *hist = nullptr, *base = nullptr;
-  if (dmalloc(&wm, (size_t)NL * nblk * kBlkU4) || dmalloc(&sbc, (size_t)NL * nsb * kRadix) ||
-      dmalloc(&Zd, (size_t)NL * kRadix) || dmalloc(&cur, n) || dmalloc(&nxt, n) ||
-      dmalloc(&hist, nblk * kRadix) || dmalloc(&base, nblk * kRadix))
-    return -1;
-  FM_HIP(hipMemsetAsync(sbc, 0, (size_t)NL * nsb * kRadix * 8, s));
-  FM_HIP(hipMemcpyAsync(cur, d_bwt, n * 4, hipMemcpyDeviceToDevice, s));
-  const unsigned gblk = (unsigned)((nblk + kWaves - 1) / kWaves);
-  for (uint32_t lev = 0; lev < NL; ++lev) {
-    const uint32_t shift = 4 * (NL - 1 - lev);
-    k_hist16<<<gblk, kThreads, 0, s>>>(cur, n, shift, hist, nblk);
-    FM_HIP(hipGetLastError());
-    if (exclusive_scan_u64(hist, base, nblk * kRadix, s, nullptr)) return -1;
-    k_gather_z<<<1, 64, 0, s>>>(base, nblk, Zd + lev * kRadix);
-    k_level16<<<gblk, kThreads, 0, s>>>(cur, nxt, n, shift, base, nblk, wm + (uint64_t)lev * nblk * kBlkU4,
-                                        sbc + (uint64_t)lev * nsb * kRadix, nsb);
-    FM_HIP(hipGetLastError());
-    std::swap(cur, nxt);
+  h->n = n;
+  h->L = L;
+  h->max_sym = max_sym;
+  // -- the 2-level wavelet matrix, with C / sigma from its final order
+  {
+    const double t = build_clock();
+    if (device_build_w2(h, d_bwt, n, s)) return -1;
+    build_phase("2-level wavelet matrix", t, s);
   }
-  FM_HIP(hipStreamSynchronize(s));
-  FM_HIP(hipFree(hist));
-  FM_HIP(hipFree(base));
-  // -- C / D from the final order
-  uint64_t *S = nullptr, *E = nullptr, *cnt = nullptr, *C = nullptr;
-  int64_t* D = nullptr;
-  unsigned long long* d_sigma = nullptr;
-  if (dmalloc(&S, K) || dmalloc(&E, K) || dmalloc(&cnt, K + 1) || dmalloc(&C, K + 1) ||
-      dmalloc(&D, K) || dmalloc(&d_sigma, 1))
-    return -1;
-  FM_HIP(hipMemsetAsync(S, 0, K * 8, s));
-  FM_HIP(hipMemsetAsync(E, 0, K * 8, s));
-  FM_HIP(hipMemsetAsync(cnt, 0, (K + 1) * 8, s));
-  FM_HIP(hipMemsetAsync(d_sigma, 0, 8, s));
-  k_bounds<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 20), kThreads, 0, s>>>(cur, n, S,
-                                                                                                     E);
-  k_counts<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(S, E, K, cnt, d_sigma);
-  if (exclusive_scan_u64(cnt, C, K + 1, s, nullptr)) return -1;
-  k_dtable<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(C, S, K, D);
-  FM_HIP(hipGetLastError());
-  unsigned long long sigma = 0;
-  FM_HIP(hipMemcpyAsync(&sigma, d_sigma, 8, hipMemcpyDeviceToHost, s));
-  FM_HIP(hipStreamSynchronize(s));
-  FM_HIP(hipFree(S));
-  FM_HIP(hipFree(E));
-  FM_HIP(hipFree(cnt));
-  FM_HIP(hipFree(d_sigma));
-  FM_HIP(hipFree(cur));
-  FM_HIP(hipFree(nxt));
+  uint64_t* C = h->C;
 
   // -- range bitmaps
   // Base block of the aligned bitmap hierarchy.  A decode step never reads the
@@ -594,29 +457,11 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   }
   FM_HIP(hipStreamSynchronize(s));
 
-  h->n = n;
-  h->L = L;
-  h->NL = NL;
-  h->max_sym = max_sym;
-  h->sigma = sigma;
-  h->wm = wm;
-  h->sb = sbc;
-  h->Z = Zd;
-  h->C = C;
-  h->D = D;
   h->bm = bm;
   h->bm_full = bm_full;
-  h->wm_bytes = (uint64_t)NL * (nblk * 128 + nsb * kRadix * 8);
   h->bm_bytes = total_words * 4;
-  DevView& v = h->view;
-  v = DevView{};
+  DevView& v = h->view;   // (device_build_w2 set C, D2 and the levels)
   v.n = n;
-  v.nblk = nblk;
-  v.nsb = nsb;
-  v.wm = wm;
-  v.sb = sbc;
-  v.Z = Zd;
-  v.D = D;
   v.C = C;
   v.bwt = d_bwt;
   v.bm = bm;
@@ -626,7 +471,6 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     v.bm_count[j] = bm_count[j];
   }
   v.L = L;
-  v.NL = NL;
   v.max_sym = max_sym;
   v.bm_words = words;
   v.bm_levels = bm_levels;
@@ -650,9 +494,6 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
     v.bm_follow = fb;
   }
   double t = build_clock();
-  if (device_build_w2(h, d_bwt, n, s)) return -1;
-  build_phase("2-level wavelet matrix", t, s);
-  t = build_clock();
   if (device_build_lfe(h, d_bwt, n, s)) return -1;
   build_phase("E array", t, s);
   t = build_clock();
@@ -671,11 +512,13 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   return 0;
 }
 
-// 2-level wavelet matrix over the BWT for the LF path (see W2Level).  Level l
-// holds the sequence stably partitioned by the digits of levels < l (a stable
-// radix sort by each digit's bit range); after the last level every symbol c
-// occupies one run starting at S2[c], so LF(i, c) = descent + C[c] - S2[c].
+// 2-level wavelet matrix over the BWT (see W2Level).  Level l holds the
+// sequence stably partitioned by the digits of levels < l (a stable radix sort
+// by each digit's bit range); after the last level every symbol c occupies one
+// run [S2[c], E2[c]), which gives C (the runs' lengths, scanned) and
+// LF(i, c) = descent + C[c] - S2[c].  Resets h->view and sets C, D2, sigma.
 int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) {
+  h->view = DevView{};
   const uint32_t L = h->L;
   const uint32_t NL2 = (L + 8) / 9;
   if (NL2 > (uint32_t)kW2MaxLevels) {
@@ -745,19 +588,31 @@ int device_build_w2(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream_t s) 
   FM_HIP(hipFree(total));
   FM_HIP(hipFree(sbtot));
   FM_HIP(hipFree(nxt));
-  // S2 / D2 from the final order
+  // S2 / C / D2 from the final order
   const uint64_t K = 1ull << L;
-  uint64_t *S = nullptr, *E = nullptr;
-  if (dmalloc(&S, K) || dmalloc(&E, K) || dmalloc(&h->D2, K)) return -1;
+  uint64_t *S = nullptr, *E = nullptr, *cnt = nullptr;
+  unsigned long long* d_sigma = nullptr;
+  if (dmalloc(&S, K) || dmalloc(&E, K) || dmalloc(&cnt, K + 1) || dmalloc(&h->C, K + 1) || dmalloc(&h->D2, K) ||
+      dmalloc(&d_sigma, 1))
+    return -1;
   FM_HIP(hipMemsetAsync(S, 0, K * 8, s));
   FM_HIP(hipMemsetAsync(E, 0, K * 8, s));
+  FM_HIP(hipMemsetAsync(cnt, 0, (K + 1) * 8, s));
+  FM_HIP(hipMemsetAsync(d_sigma, 0, 8, s));
   k_bounds<<<(unsigned)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1u << 20), kThreads, 0, s>>>(cur, n, S,
                                                                                                      E);
+  k_counts<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(S, E, K, cnt, d_sigma);
+  if (exclusive_scan_u64(cnt, h->C, K + 1, s, nullptr)) return -1;
   k_dtable<<<(unsigned)((K + kThreads - 1) / kThreads), kThreads, 0, s>>>(h->C, S, K, h->D2);
   FM_HIP(hipGetLastError());
+  unsigned long long sigma = 0;
+  FM_HIP(hipMemcpyAsync(&sigma, d_sigma, 8, hipMemcpyDeviceToHost, s));
   FM_HIP(hipStreamSynchronize(s));
+  h->sigma = sigma;
   FM_HIP(hipFree(S));
   FM_HIP(hipFree(E));
+  FM_HIP(hipFree(cnt));
+  FM_HIP(hipFree(d_sigma));
   FM_HIP(hipFree(cur));
   h->view.D2 = h->D2;
   h->view.NL2 = NL2;

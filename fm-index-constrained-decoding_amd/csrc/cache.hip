@@ -74,8 +74,10 @@ __device__ uint64_t cache_id_thread(const DevView& v, uint64_t lo, uint64_t hi) 
 
 // Insert the children of a batch of cached parents (k_distinct output: row r's
 // k[r] symbols, counts and child starts at off[r]) into the transition table.
-// One workgroup per parent; a slot is claimed by CAS on its first word; a key
-// whose home run of kTransProbe slots is full is left out (the decode step then
+// One workgroup per parent; a key goes to the emptier of its two buckets (fill
+// counts in `fill`, read without synchronisation: a stale read only makes the
+// choice less even), its slot claimed by an atomic increment of that bucket's
+// count; a key finding both buckets full is left out (the decode step then
 // takes the wavelet-matrix descent for it).
 __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t* __restrict__ plo,
                                                       const uint64_t* __restrict__ phi,
@@ -85,6 +87,7 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
                                                       const uint64_t* __restrict__ cnt,
                                                       const uint64_t* __restrict__ child, uint64_t m,
                                                       uint64_t* __restrict__ tab, uint64_t cap,
+                                                      uint32_t* __restrict__ fill,
                                                       unsigned long long* __restrict__ stats) {
   const uint64_t r = blockIdx.x;
   if (r >= m) return;
@@ -104,16 +107,21 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
     const uint64_t w0 = lo | (c << kTransSymShift);
     const uint64_t w1 = hi | ((clo & ((1ull << 30) - 1)) << kTransSymShift);
     const uint64_t w2 = (clo >> 30) | (cw << 4) | (aux << 38);
-    uint64_t slot = trans_home(lo, hi, c, cap);
+    const TransHome th = trans_home(lo, hi, c, cap);
+    const uint64_t ba = th.a / kTransBucket, bb = th.b / kTransBucket;
+    const bool a_first = __hip_atomic_load(fill + ba, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
+                         __hip_atomic_load(fill + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool done = false;
-    for (uint32_t d = 0; d < kTransProbe && !done; ++d) {
-      unsigned long long* p = reinterpret_cast<unsigned long long*>(tab + 3 * slot);
-      if (atomicCAS(p, (unsigned long long)kTransEmpty, (unsigned long long)w0) == kTransEmpty) {
-        tab[3 * slot + 1] = w1;
-        tab[3 * slot + 2] = w2;
+    for (uint32_t t = 0; t < 2 && !done; ++t) {
+      const uint64_t bk = (t == 0) == a_first ? ba : bb;
+      const uint32_t k = atomicAdd(fill + bk, 1u);
+      if (k < kTransBucket) {
+        uint64_t* p = tab + 3 * (bk * kTransBucket + k);
+        p[0] = w0;
+        p[1] = w1;
+        p[2] = w2;
         done = true;
       }
-      if (++slot == cap) slot = 0;
     }
     if (done) ++ins; else ++drop;
   }
@@ -125,6 +133,8 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
 // would exceed the trans_mb budget -- only the cached ones), built on the GPU from
 // two k_distinct passes over the cached parents: one to count the entries,
 // one to insert them.
+constexpr double kTransLoad = 0.85;
+
 int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>& nodes, hipStream_t s) {
   DevView& v = h->view;
   v.trans_cap = 0;
@@ -150,7 +160,7 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   hi.reserve(kChunkRows);
   off.reserve(kChunkRows + 1);
   // parents: every cached range but the root (whose LF step is the C lookup)
-  auto pass = [&](uint64_t min_count, uint64_t* tab, uint64_t cap, uint64_t& total,
+  auto pass = [&](uint64_t min_count, uint64_t* tab, uint64_t cap, uint32_t* d_fill, uint64_t& total,
                   unsigned long long* d_stats) -> int {
     total = 0;
     for (size_t i0 = 1; i0 < nodes.size();) {
@@ -176,7 +186,7 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
         return -1;
       if (tab) {
         k_trans_insert<<<(unsigned)m, 256, 0, s>>>(v, d_lo.p, d_hi.p, d_off.p, d_k.p, d_syms.p, d_cnt.p,
-                                                   d_child.p, m, tab, cap, d_stats);
+                                                   d_child.p, m, tab, cap, d_fill, d_stats);
         FM_HIP(hipGetLastError());
         FM_HIP(hipStreamSynchronize(s));   // the host staging vectors are refilled next chunk
       } else {
@@ -189,42 +199,46 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
     }
     return 0;
   };
-  uint64_t min_count = mode >= 2 ? 1 : v.cache_min;
+  uint64_t min_count = mode >= 2 ? (uint64_t)std::max(1, h->opts.trans_min) : v.cache_min;
   uint64_t entries = 0;
   double t = build_clock();
-  if (pass(min_count, nullptr, 0, entries, nullptr)) return -1;
+  if (pass(min_count, nullptr, 0, nullptr, entries, nullptr)) return -1;
   build_phase("transitions: count pass", t, s);
-  uint64_t cap = std::max<uint64_t>(1024, entries + entries / 2 + entries / 4);   // load <= 0.57
-  if (cap * 24 > budget && min_count == 1) {   // over budget: the cached children only
+  // buckets of 8 slots at load <= kTransLoad (two-choice: fmidx_internal.h)
+  auto slots_for = [](uint64_t e) {
+    const uint64_t nb = std::max<uint64_t>(128, (uint64_t)((double)e / (kTransLoad * kTransBucket)) + 1);
+    return nb * kTransBucket;
+  };
+  uint64_t cap = slots_for(entries);
+  if (cap * 24 > budget && min_count < v.cache_min) {   // over budget: the cached children only
     min_count = v.cache_min;
-    if (pass(min_count, nullptr, 0, entries, nullptr)) return -1;
-    cap = std::max<uint64_t>(1024, 2 * entries);
+    if (pass(min_count, nullptr, 0, nullptr, entries, nullptr)) return -1;
+    cap = slots_for(entries);
   }
   if (entries == 0 || cap * 24 > budget) return 0;
   uint64_t* tab = nullptr;
-  // kTransPad slots past the end mirror slots [0, kTransPad) (filled after the
-  // insert), so a probe run can be read as one contiguous span without wrapping
-  if (hipMalloc(reinterpret_cast<void**>(&tab), (cap + kTransPad) * 24) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&tab), cap * 24) != hipSuccess) {
     (void)hipGetLastError();
     return 0;   // no room: the descent serves every step
   }
-  FM_HIP(hipMemsetAsync(tab, 0xFF, (cap + kTransPad) * 24, s));
+  FM_HIP(hipMemsetAsync(tab, 0xFF, cap * 24, s));
   DBuf<unsigned long long> d_stats;
-  if (d_stats.alloc(2)) {
+  DBuf<uint32_t> d_fill;   // per-bucket fill counts, for the insert only
+  if (d_stats.alloc(2) || d_fill.alloc(cap / kTransBucket)) {
     (void)hipFree(tab);
     return -1;
   }
   FM_HIP(hipMemsetAsync(d_stats.p, 0, 16, s));
+  FM_HIP(hipMemsetAsync(d_fill.p, 0, cap / kTransBucket * 4, s));
   uint64_t dummy = 0;
   t = build_clock();
-  if (pass(min_count, tab, cap, dummy, d_stats.p)) {
+  if (pass(min_count, tab, cap, d_fill.p, dummy, d_stats.p)) {
     (void)hipFree(tab);
     return -1;
   }
   build_phase("transitions: insert pass", t, s);
   unsigned long long st[2] = {0, 0};
   FM_HIP(hipMemcpy(st, d_stats.p, 16, hipMemcpyDeviceToHost));
-  FM_HIP(hipMemcpyAsync(tab + 3 * cap, tab, kTransPad * 24, hipMemcpyDeviceToDevice, s));
   FM_HIP(hipStreamSynchronize(s));
   h->trans_tab = tab;
   h->trans_entries = st[0];

@@ -3,21 +3,14 @@
 //
 // Layout (all resident in HBM, built once per index):
 //
-//   wm      16-ary wavelet matrix over the BWT: NL = ceil(L/4) digit levels
-//           (L = bit width of the largest symbol; 17 -> 5 levels for a 128k
-//           vocabulary + SHIFT), level 0 = the most significant 4-bit digit.
-//           Level l is an array of 128-byte rank blocks: 16 x uint16 counts
-//           of each digit before the block (relative to its superblock) + 96
-//           bytes = 192 packed 4-bit digits.  rank_d(i) = one block line + one
-//           superblock count; an LF step is NL dependent round trips instead
-//           of the 17 of a binary wavelet tree/matrix.
-//   sb      per level and superblock (341 blocks = 65472 digits) the absolute
-//           count of each digit before it (16 x uint64).
-//   Z       per level, Z[l][d] = number of digits < d in that level (the start
-//           of digit d's partition in the next level).
-//   D       D[c] = C[c] - S[c] as int64, where C[c] is the FM-index C array and
-//           S[c] the start of symbol c in the wavelet matrix's final order, so
-//           LF(i, c) = desc_c(i) + D[c] (desc = the NL-level descent).
+//   w2      2-level wavelet matrix over the BWT (W2Level below): digits of
+//           <= 9 bits, 17 = 9 + 8 for a 128k vocabulary + SHIFT, so an LF step
+//           is 2 dependent rank round trips (a binary wavelet tree: 17).  Level
+//           l is an array of 1024-digit rank blocks (per-digit uint16 header +
+//           the digits as uint8 / uint16), with per-superblock (2^16 digits)
+//           absolute counts and Z[l][d] = digits < d in that level.
+//   D2      D2[c] = C[c] - S2[c] as int64 (S2[c] = start of symbol c in the
+//           matrix's final order), so LF(i, c) = desc_c(i) + D2[c].
 //   C       C[0 .. 2^L] (C[c+1]-C[c] = occurrences of c).
 //   bwt     the BWT as plain uint32 symbols (streamed for narrow ranges).
 //   bm      range-presence bitmaps: level j holds one bitmap of W bits for each
@@ -34,11 +27,6 @@ namespace fmidx {
 
 constexpr int kMaxSymBits = 26;        // 2^26 symbol table; token ids + 10 need 18 at most
 constexpr int kMaxLevels = kMaxSymBits;
-constexpr int kRadix = 16;             // 4-bit digits
-constexpr int kMaxDigitLevels = (kMaxSymBits + 3) / 4;
-constexpr int kBlkDigits = 192;        // digits per 128-B rank block
-constexpr int kBlkU4 = 8;              // uint4 per rank block
-constexpr int kSbBlocks = 341;         // blocks per superblock (65472 digits < 2^16)
 constexpr int kMaxBmLevels = 24;
 // 2-level wavelet matrix (the LF path): digits of <= 9 bits, so L <= 18 bits
 // in 2 levels (17 = 9 + 8 for a 128k vocabulary + SHIFT), <= 27 in 3.
@@ -69,12 +57,6 @@ struct W2Level {
 // Everything a kernel needs, passed by value as a kernel argument.
 struct DevView {
   uint64_t n;                 // BWT length (corpus tokens + 1 sentinel)
-  uint64_t nblk;              // rank blocks per level = n / 192 + 1
-  uint64_t nsb;               // superblocks per level = nblk / 341 + 1
-  const uint4* wm;            // NL * nblk * 8 uint4
-  const uint64_t* sb;         // NL * nsb * 16
-  const uint64_t* Z;          // NL * 16
-  const int64_t* D;           // [2^L]
   const uint64_t* C;          // [2^L + 1]
   const uint32_t* bwt;        // [n], or null once E holds the symbols (bwt_sym)
   const uint32_t* bm;         // bitmap hierarchy
@@ -101,7 +83,6 @@ struct DevView {
   const int64_t* D2;          // D2[c] = C[c] - S2[c] (S2 = start of c in its final order)
   uint32_t NL2;               // its levels (0 = not built)
   uint32_t L;                 // symbol bits
-  uint32_t NL;                // digit levels
   uint32_t max_sym;           // largest symbol value present
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
@@ -165,10 +146,9 @@ __device__ __forceinline__ uint32_t bwt_sym(const DevView& v, uint64_t i) {
 // hot field at kernel entry issues all those loads together, up front.
 #define FM_PRELOAD_VIEW(v)                                                                                 \
   do {                                                                                                     \
-    asm volatile("" ::"s"((v).n), "s"((v).nblk), "s"((v).nsb), "s"((v).wm), "s"((v).sb), "s"((v).Z),      \
-                 "s"((v).D), "s"((v).C));                                                                  \
+    asm volatile("" ::"s"((v).n), "s"((v).C));                                                             \
     asm volatile("" ::"s"((v).bwt), "s"((v).bm), "s"((v).bm_full), "s"((v).bm_follow),                     \
-                 "s"((v).bm_count[0]), "s"((v).L), "s"((v).NL), "s"((v).max_sym), "s"((v).bm_words),       \
+                 "s"((v).bm_count[0]), "s"((v).L), "s"((v).max_sym), "s"((v).bm_words),                    \
                  "s"((v).bm_levels), "s"((v).bm_log2));                                                    \
     asm volatile("" ::"s"((v).D2), "s"((v).NL2), "s"((v).cache_bm), "s"((v).cache_tab),                   \
                  "s"((v).cache_mask), "s"((v).cache_min), "s"((v).E), "s"((v).E2), "s"((v).trans_tab),                  \
@@ -178,73 +158,6 @@ __device__ __forceinline__ uint32_t bwt_sym(const DevView& v, uint64_t i) {
     asm volatile("" ::"s"((v).w2[1].blocks), "s"((v).w2[1].sb), "s"((v).w2[1].Z), "s"((v).w2[1].blk_bytes), \
                  "s"((v).w2[1].bits), "s"((v).w2[1].shift));                                               \
   } while (0)
-
-// ---------------------------------------------------------------------------
-// occurrences of digit d among the first m (<= 16) nibbles of w
-__device__ __forceinline__ uint32_t nib_count(uint64_t w, uint32_t d, uint32_t m) {
-  const uint64_t ones = 0x1111111111111111ull;
-  const uint64_t x = w ^ (ones * d);
-  const uint64_t nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & ones;
-  const uint64_t mk = (m >= 16) ? ~0ull : ((1ull << (4 * m)) - 1);
-  return (uint32_t)__popcll(~nz & ones & mk);
-}
-
-__device__ __forceinline__ uint32_t u4_get(const uint4& x, uint32_t i) {
-  return i == 0 ? x.x : (i == 1 ? x.y : (i == 2 ? x.z : x.w));
-}
-
-__device__ __forceinline__ uint32_t digit_of(uint32_t c, uint32_t NL, uint32_t lev) {
-  return (c >> (4 * (NL - 1 - lev))) & 15u;
-}
-
-// Contribution of one uint4 (slot q of a rank block) to rank_d(k-th digit):
-// slots 0,1 hold the 16 uint16 header counts, slots 2..7 32 digits each.
-__device__ __forceinline__ uint32_t block_part(const uint4& x, uint32_t q, uint32_t d, uint32_t k) {
-  if (q < 2) {
-    if ((d >> 3) != q) return 0;
-    const uint32_t w = u4_get(x, (d & 7) >> 1);
-    return (d & 1) ? (w >> 16) : (w & 0xFFFFu);
-  }
-  const uint32_t s = 32 * (q - 2);
-  const uint32_t m = k > s ? min(32u, k - s) : 0u;
-  const uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32);
-  const uint64_t hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  return nib_count(lo, d, min(16u, m)) + nib_count(hi, d, m > 16 ? m - 16 : 0u);
-}
-
-__device__ __forceinline__ const uint4* rank_block(const DevView& v, uint32_t lev, uint64_t b) {
-  return v.wm + ((uint64_t)lev * v.nblk + b) * kBlkU4;
-}
-
-__device__ __forceinline__ const uint64_t* sb_row(const DevView& v, uint32_t lev, uint64_t b) {
-  return v.sb + ((uint64_t)lev * v.nsb + b / kSbBlocks) * kRadix;
-}
-
-// rank_d(i) at level lev by one thread (0 <= i <= n).
-__device__ __forceinline__ uint64_t rank16(const DevView& v, uint32_t lev, uint64_t i, uint32_t d) {
-  const uint64_t b = i / kBlkDigits;
-  const uint32_t k = (uint32_t)(i - b * kBlkDigits);
-  const uint4* blk = rank_block(v, lev, b);
-  uint4 x[kBlkU4];
-#pragma unroll
-  for (int q = 0; q < kBlkU4; ++q) x[q] = blk[q];
-  uint64_t cnt = sb_row(v, lev, b)[d];
-#pragma unroll
-  for (uint32_t q = 0; q < kBlkU4; ++q) cnt += block_part(x[q], q, d, k);
-  return cnt;
-}
-
-// Full NL-level descent of both endpoints by one thread (no early exit).
-__device__ __forceinline__ void descend_full(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
-  for (uint32_t lev = 0; lev < v.NL; ++lev) {
-    const uint32_t d = digit_of(c, v.NL, lev);
-    const uint64_t z = v.Z[lev * kRadix + d];
-    const uint64_t rl = rank16(v, lev, l, d);
-    const uint64_t rr = rank16(v, lev, r, d);
-    l = z + rl;
-    r = z + rr;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Buffer descriptor over [base, base + bytes) from wave-uniform values.
@@ -340,6 +253,44 @@ __device__ __forceinline__ uint64_t rank_w2_at(const uint8_t* blocks, const uint
 
 __device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
   return rank_w2_at(L.blocks, L.sb, L.blk_bytes, L.bits, i, d, q);
+}
+
+// rank_d(i) of one level by ONE thread (the block's first i mod 1024 digits
+// streamed 16 B at a time): the host API's scalar step and the few keys the
+// transition table left out, never a batched path.
+__device__ __forceinline__ uint64_t rank_w2_thread(const W2Level& L, uint64_t i, uint32_t d) {
+  const uint64_t b = i >> kW2BlkLog2;
+  const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
+  const uint8_t* base = L.blocks + b * L.blk_bytes;
+  const uint32_t R = 1u << L.bits;
+  uint64_t cnt = L.sb[(i >> kW2SbLog2) * R + d] + reinterpret_cast<const uint16_t*>(base)[d];
+  const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R);
+  const uint32_t per = L.bits > 8 ? 8u : 16u;   // digits per 16 B
+  for (uint32_t j0 = 0; j0 < k; j0 += per) {
+    const uint4 x = p[j0 / per];
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const bool wide = L.bits > 8;
+      const uint32_t dig = wide ? (w[(j >> 1) & 3] >> (16 * (j & 1))) & 0xFFFFu : (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      cnt += ((!wide || j < 8) && j0 + j < k && dig == d) ? 1u : 0u;
+    }
+  }
+  return cnt;
+}
+
+// LF of both ends of [l, r) by symbol c (every level of the 2-level matrix) by
+// one thread: [C[c] + rank_c(l), C[c] + rank_c(r)).
+__device__ __forceinline__ void descend_w2_thread(const DevView& v, uint32_t c, uint64_t& l, uint64_t& r) {
+  for (uint32_t lev = 0; lev < v.NL2; ++lev) {
+    const W2Level& L = v.w2[lev];
+    const uint32_t d = (c >> L.shift) & ((1u << L.bits) - 1u);
+    const uint64_t z = L.Z[d];
+    l = z + rank_w2_thread(L, l, d);
+    r = z + rank_w2_thread(L, r, d);
+  }
+  l = (uint64_t)((int64_t)l + v.D2[c]);
+  r = (uint64_t)((int64_t)r + v.D2[c]);
 }
 
 // LF step of a narrow range by a whole wave: E[lo, hi) is scanned (8 entries
@@ -458,8 +409,14 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
   return cache_hash(lo ^ (c * 0xD6E8FEB86659FD93ull), hi + c);
 }
 
-// Transition slot (24 B, linear probing, every key within kTransProbe slots
-// of its home; keys that do not fit are left out and take the descent):
+// Transition slot (24 B) in buckets of kTransBucket slots, two-choice
+// hashing: a key sits in one of the 8 slots of its bucket A or of its bucket B
+// (k_trans_insert fills the emptier of the two; a key finding both full is
+// left out and takes the descent).  A bucket is 192 B (64-B aligned: two 128-B
+// lines), so a probe reads the same 16 slots / 384 B / 4 lines as a 16-slot
+// linear-probing run did, while the table runs at load 0.85 with about as few
+// left-out keys as linear probing had at 0.57 (0.15 % vs 0.12 % simulated;
+// C3: 45.2 -> 30.4 GiB).
 //   w0 = plo | c << 34                       (empty: ~0)
 //   w1 = phi | (clo & (2^30 - 1)) << 34
 //   w2 = clo >> 30 | cw << 4 | aux << 38      aux: 0, cache id + 1 of the child,
@@ -467,16 +424,31 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
 constexpr uint32_t kTransSymShift = 34;
 constexpr uint64_t kMask34 = (1ull << 34) - 1;
 constexpr uint64_t kTransOne = 1ull << 25;
-constexpr uint32_t kTransProbe = 16;
-constexpr uint64_t kTransPad = 32;   // slots after the table's end mirroring its first kTransPad (cache.hip)
+constexpr uint32_t kTransBucket = 8;
+constexpr uint32_t kTransProbe = 2 * kTransBucket;   // a key's candidate slots: bucket A's, then bucket B's
 constexpr uint64_t kTransEmpty = ~0ull;
 
-__host__ __device__ __forceinline__ uint64_t trans_home(uint64_t lo, uint64_t hi, uint64_t c, uint64_t cap) {
+__host__ __device__ __forceinline__ uint64_t mul_hi64(uint64_t a, uint64_t b) {
 #ifdef __HIP_DEVICE_COMPILE__
-  return __umul64hi(trans_hash(lo, hi, c), cap);
+  return __umul64hi(a, b);
 #else
-  return (uint64_t)(((unsigned __int128)trans_hash(lo, hi, c) * cap) >> 64);
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
 #endif
+}
+
+struct TransHome {
+  uint64_t a, b;   // first slots of the key's two buckets (cap = the table's slots, a multiple of 8)
+};
+__host__ __device__ __forceinline__ TransHome trans_home(uint64_t lo, uint64_t hi, uint64_t c, uint64_t cap) {
+  const uint64_t h = trans_hash(lo, hi, c);
+  uint64_t g = (h ^ (h >> 31)) * 0x94D049BB133111EBull;   // a second, independent bucket index
+  g ^= g >> 29;
+  const uint64_t nb = cap / kTransBucket;
+  return TransHome{mul_hi64(h, nb) * kTransBucket, mul_hi64(g, nb) * kTransBucket};
+}
+// candidate k (0 .. kTransProbe - 1) of a key
+__host__ __device__ __forceinline__ uint64_t trans_slot(const TransHome& t, uint32_t k) {
+  return k < kTransBucket ? t.a + k : t.b + (k - kTransBucket);
 }
 
 // The LF step of the batched kernels, by all 64 lanes of a wave (uniform
@@ -527,15 +499,14 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   const uint32_t q = lane & 31u;
   const bool side = lane >= 32;
   const uint64_t c = (uint64_t)sym;
-  // (1) transition probe of a cached range: 16 slots x 3 words, one word per
-  // lane 0-47; lanes 48-63 read the parent's own home run in the range cache
+  // (1) transition probe of a cached range: its 16 candidate slots x 3 words,
+  // one word per lane 0-47; lanes 48-63 read the parent's own home run in the range cache
   // (8 slots x 2 words), in the same round trip
   const bool probe = v.trans_cap && hi - lo >= v.cache_min;
   const uint64_t key0 = lo | (c << kTransSymShift);
   uint64_t tw = kTransEmpty;
   if (probe && lane < 3 * kTransProbe) {
-    uint64_t slot = trans_home(lo, hi, c, v.trans_cap) + lane / 3;
-    if (slot >= v.trans_cap) slot -= v.trans_cap;
+    const uint64_t slot = trans_slot(trans_home(lo, hi, c, v.trans_cap), lane / 3);
     tw = v.trans_tab[3 * slot + lane % 3];
   } else if (probe && v.cache_mask) {
     const uint32_t k = lane - 3 * kTransProbe;
@@ -640,6 +611,7 @@ struct BuildOpts {
   int32_t keep_bwt = 0;         // keep the plain BWT although E holds its symbols
   int32_t follow_bitmaps = 0;   // per-symbol C-block bitmaps
   int32_t bm_log2 = -1;         // aligned bitmap block; -1: by n
+  int32_t trans_min = 1;        // transitions = 2: the children of >= trans_min occurrences
   uint64_t cache_min = 4096;    // range-bitmap cache threshold (rows)
   uint64_t cache_mb = 48ull << 10;
   uint64_t trans_mb = 72ull << 10;
@@ -680,12 +652,7 @@ struct Index {
   uint64_t sigma = 0;            // distinct symbols in the BWT
   uint64_t max_sym = 0;
   uint32_t L = 0;
-  uint32_t NL = 0;
   // device allocations
-  uint4* wm = nullptr;
-  uint64_t* sb = nullptr;
-  uint64_t* Z = nullptr;
-  int64_t* D = nullptr;
   uint64_t* C = nullptr;
   uint32_t* bwt = nullptr;        // freed after the build when E holds the symbols
   uint32_t* bwt_view = nullptr;   // materialised on request (fm_device_bwt) when bwt is freed
@@ -710,7 +677,7 @@ struct Index {
   uint32_t* sa_samp = nullptr;
   uint64_t* isa_samp = nullptr;
   uint64_t samp_bytes = 0;
-  uint64_t wm_bytes = 0, bm_bytes = 0, follow_bytes = 0, w2_bytes = 0;
+  uint64_t bm_bytes = 0, follow_bytes = 0, w2_bytes = 0;
   SampleView samples() const { return SampleView{mark, mark_cnt, sa_samp, isa_samp}; }
   // grow-only workspace for batched traversals
   void* ws = nullptr;

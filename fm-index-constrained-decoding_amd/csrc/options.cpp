@@ -47,6 +47,7 @@ bool set_build(BuildOpts& o, const std::string& k, long long x) {
   else if (k == "keep_bwt") o.keep_bwt = (int32_t)x;
   else if (k == "follow_bitmaps") o.follow_bitmaps = (int32_t)x;
   else if (k == "bm_log2") o.bm_log2 = (int32_t)x;
+  else if (k == "trans_min") o.trans_min = (int32_t)x;
   else if (k == "cache_min") o.cache_min = (uint64_t)x;
   else if (k == "cache_mb") o.cache_mb = (uint64_t)x;
   else if (k == "trans_mb") o.trans_mb = (uint64_t)x;
@@ -83,8 +84,8 @@ bool check_tuning(const Tuning& t) {
     set_error("tuning: dec_threads must be 0, 256, 512 or 1024");
     return false;
   }
-  if (t.lf_work < -1 || t.lf_work > 2) {
-    set_error("tuning: lf_work must be -1 (by row count), 0, 1 or 2");
+  if (t.lf_work < -1 || t.lf_work > 3) {
+    set_error("tuning: lf_work must be -1 (by row count), 0, 1, 2 or 3");
     return false;
   }
   if (t.sa_chunk < 1024) {

@@ -91,32 +91,31 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
 constexpr uint64_t kPackMax = 128;
 
 // Transition probe of a wave's cached rows eight at a time (8 lanes per row):
-// the row's 16-slot run as four 16-B loads per lane (128 B contiguous per
-// row and instruction) staged through LDS, and (CE) the range's own
+// the row's two 192-B buckets as three 16-B loads per lane (128 B contiguous
+// per row and instruction) staged through LDS, and (CE) the range's own
 // range-cache run alongside.  Used by get_range (group_step<P8>) and the
 // opt-in LF sweep (k_lf_sweep).
 constexpr uint32_t kProbeLanes = 8;
 constexpr uint32_t kProbeRows = 64 / kProbeLanes;
-constexpr uint32_t kProbeChunks = 32;   // 16-B chunks staged per probe row (a 16-slot run spans <= 25)
+constexpr uint32_t kProbeChunks = 24;   // 16-B chunks staged per probe row (two buckets of 12)
 
 // Transition probe of up to eight rows (8 lanes each; row k of the batch =
 // the wave's lane src[k], src < 0: none) -- loads only; probe_finish consumes.
 struct ProbeLoads {
-  uint4 c0, c1, c2, c3;   // 16-B chunks sl, sl + 8, sl + 16, sl + 24 of the row's run
+  uint4 c0, c1, c2;       // 16-B chunks sl, sl + 8, sl + 16 of the row's 24 (bucket A's 12, then B's)
   uint4 ce;               // the range's own range-cache slot sl
 };
 template <bool CE = true>
 __device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, uint64_t h, uint64_t c) {
   const uint32_t sl = (threadIdx.x & 63u) % kProbeLanes;
-  const uint64_t home = trans_home(l, h, c, v.trans_cap);
-  // the run's bytes [24 home, 24 home + 384) as 16-B chunks from c0; the table
-  // carries kTransPad mirrored slots past its end, so nothing wraps
-  const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab) + ((24 * home) >> 4) + sl;
+  const TransHome th = trans_home(l, h, c, v.trans_cap);
+  // chunk i < 12 of bucket A at 24 a / 16 + i, chunk i >= 12 of bucket B
+  const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab);
+  const uint64_t ca = (24 * th.a) >> 4, cb = ((24 * th.b) >> 4) - 12;
   ProbeLoads p;
-  p.c0 = tt[0];
-  p.c1 = tt[kProbeLanes];
-  p.c2 = tt[2 * kProbeLanes];
-  p.c3 = tt[3 * kProbeLanes];
+  p.c0 = tt[ca + sl];                                                        // chunks 0 .. 7
+  p.c1 = tt[sl < 4 ? ca + 8 + sl : cb + 8 + sl];                             // 8 .. 15
+  p.c2 = tt[cb + 16 + sl];                                                   // 16 .. 23
   // the range's own range-cache run (8 slots, one per lane)
   if (CE) {
     const uint64_t cs = (cache_hash(l, h) + sl) & v.cache_mask;
@@ -135,14 +134,12 @@ __device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint6
                                             uint64_t& chi, uint64_t& pid1) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
-  const uint64_t home = trans_home(l, h, c, v.trans_cap);
   uint4* sr = s_run + seg * kProbeChunks + sl;
   sr[0] = p.c0;
   sr[kProbeLanes] = p.c1;
   sr[2 * kProbeLanes] = p.c2;
-  sr[3 * kProbeLanes] = p.c3;
   __builtin_amdgcn_wave_barrier();
-  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]) + ((24 * home) & 15) / 8;
+  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]);   // the 16 candidates
   const uint64_t key0 = l | (c << kTransSymShift);
   bool hit = false;
   uint64_t w1 = 0, w2 = 0;
@@ -238,11 +235,10 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     // unconditional loads (slot 0 for rows that do not probe; C[0..2] when
     // the index has no transition table)
     const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;
-    const uint64_t home = probe ? trans_home(l, h, c, v.trans_cap) : 0;
+    const TransHome th = probe ? trans_home(l, h, c, v.trans_cap) : TransHome{0, 0};
 #pragma unroll
     for (int k = 0; k < 16 / G; ++k) {
-      uint64_t slot_k = probe ? home + j * (16 / G) + k : 0;
-      if (slot_k >= v.trans_cap) slot_k -= v.trans_cap;
+      const uint64_t slot_k = probe ? trans_slot(th, j * (16 / G) + k) : 0;
 #pragma unroll
       for (int w = 0; w < 3; ++w) pw[3 * k + w] = tt[3 * slot_k + w];
     }
@@ -392,8 +388,7 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
       const uint64_t qc = act ? (uint64_t)qs : 0;
       const bool qscan = act && v.E && qh - ql <= 128;
       const bool qprobe = act && !qscan && v.trans_cap && qh - ql >= v.cache_min;
-      uint64_t slot = qprobe ? trans_home(ql, qh, qc, v.trans_cap) + sl : 0;
-      if (slot >= v.trans_cap) slot -= v.trans_cap;
+      const uint64_t slot = qprobe ? trans_slot(trans_home(ql, qh, qc, v.trans_cap), sl) : 0;
       const uint64_t p0 = tt[3 * slot], p1 = tt[3 * slot + 1], p2 = tt[3 * slot + 2];
       uint64_t qe[8];
 #pragma unroll
@@ -910,6 +905,249 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_tail(DevView v, const LfWork*
   }
 }
 
+// ------------------------------------------------------------ class-list LF
+// Throughput form of fm_lf_step_batch (lf_work 3): every row's work is done by
+// lanes shaped for it, and no row waits behind another row's chain.
+//   k_lf_class  one lane per row, no wide-row code (few VGPRs: the whole
+//               launch's waves resident at once): reset / dead rows, the full
+//               range (C lookup) and every range of <= kOwnScan rows -- the
+//               lane loads its own E[lo, hi) (a one-row range, 71 % of a
+//               decode trace's rows, is ONE 8-B load: one request) -- are
+//               settled and written; every other row is appended to one of
+//               three class lists (one atomic per class per workgroup):
+//                 P  cached ranges (>= cache_min rows): transition probes,
+//                 S  ranges of kOwnScan+1 .. kSmallScan rows: E scans,
+//                 W  the rest: E scans of <= 512 rows, 2-level descents;
+//   k_lf_lists  persistent waves over the lists: P eight rows per round trip
+//               (probe_issue / probe_finish: 8 lanes per row, LDS-staged
+//               buckets, the range's own cache run alongside; a miss -- a key
+//               the table left out, or an uncached range -- takes the descent
+//               started with the range's bitmap word), S eight rows per round
+//               trip (8 lanes x 8 entries per row), W one row per wave
+//               (lf_step_tail).
+// Lists are split into kWorkRegions regions by appending workgroup, as the
+// worklist sweep's are.  Every row is written exactly once, so in-place
+// launches stay correct.
+constexpr uint64_t kOwnScan = 8;
+constexpr uint64_t kSmallScan = 64;
+constexpr uint32_t kLfClasses = 3;   // P, S, W
+#ifndef FMIDX_LIST_WAVES
+#define FMIDX_LIST_WAVES 4096
+#endif
+constexpr uint64_t kListWaves = FMIDX_LIST_WAVES;   // k_lf_lists' persistent waves (a multiple of 4 x kWorkRegions)
+
+#ifndef FMIDX_CLASS_WGS
+#define FMIDX_CLASS_WGS 0
+#endif
+constexpr uint64_t kClassWgs = FMIDX_CLASS_WGS;   // k_lf_class workgroups (0: one per 256 rows)
+
+__global__ void __launch_bounds__(kLfThreads) k_lf_class(DevView v, const int64_t* __restrict__ tok, int64_t shift,
+                                                        int64_t reset_below, const uint64_t* lo_in,
+                                                        const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                                                        uint64_t m, LfWork* __restrict__ lt,
+                                                        uint32_t* __restrict__ cnt, uint64_t cap) {
+  __shared__ uint32_t s_n[2][kLfClasses][kLfThreads / 64];   // by iteration parity
+  __shared__ uint32_t s_base[2][kLfClasses];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  // workgroup-strided over 256-row blocks, the next block's row state loaded
+  // while this block's E entries are in flight
+  uint64_t blk = blockIdx.x;
+  uint64_t i = blk * kLfThreads + threadIdx.x;
+  int64_t t = (int64_t)row_load_u64(tok, m, i < m ? i : m - 1);
+  uint64_t l = row_load_u64(lo_in, m, i < m ? i : m - 1);
+  uint64_t h = row_load_u64(hi_in, m, i < m ? i : m - 1);
+  for (uint32_t par = 0; blk * kLfThreads < m; blk += gridDim.x, par ^= 1u) {   // workgroup-uniform
+    // (no early exit: every wave of the workgroup reaches the append's barriers)
+    const uint64_t ni = (blk + gridDim.x) * kLfThreads + threadIdx.x;
+    const uint64_t nii = ni < m ? ni : m - 1;
+    const int64_t tn = (int64_t)row_load_u64(tok, m, nii);
+    const uint64_t ln = row_load_u64(lo_in, m, nii), hn = row_load_u64(hi_in, m, nii);
+    const bool valid = i < m;
+    if (h > v.n) h = v.n;
+    const int64_t sym = t + shift;
+    const bool reset = valid && t < reset_below;
+    const bool live = valid && !reset;
+    const bool dead = live && (l >= h || sym < 0 || (uint64_t)sym > v.max_sym);
+    const bool full = live && !dead && l == 0 && h == v.n;
+    const bool step = live && !dead && !full;
+    const uint64_t w = step ? h - l : 0;
+    const bool own = step && v.E && w <= kOwnScan;
+    const bool probe = step && !own && v.trans_cap && w >= v.cache_min;
+    const bool small = step && !own && !probe && v.E && w <= kSmallScan;
+    const bool wide = step && !own && !probe && !small;
+    const uint64_t c = (uint64_t)sym;
+    const uint64_t cf = full ? c : 0;   // the others all read C[0..1]: one shared line
+    const uint64_t ca = v.C[cf], cb = v.C[cf + 1];
+    // the lane's own E entries: as many loads as the wave's widest own row needs
+    // (wave-uniform; one for a wave of one-row ranges), clamped, unconditional
+    uint32_t wmax = (uint32_t)(own ? w : 0);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, d, 64));
+    uint64_t fmin = ~0ull, fmax = 0;
+#ifdef FMIDX_CLASS_SKIP_E   // measurement variant: every own load reads E[0] (the skeleton's cost)
+    const uint64_t eb = 0, el = 0;
+#else
+    const uint64_t eb = own ? l : 0, el = own ? w - 1 : 0;
+#endif
+    if (wmax <= 1) {
+      const uint64_t x = v.E ? v.E[eb] : 0;
+      if (own && (x >> kESymShift) == c) fmin = fmax = x & kELfMask;
+    } else {
+      uint64_t x[kOwnScan];
+#pragma unroll
+      for (uint32_t k = 0; k < kOwnScan; ++k) x[k] = v.E[eb + (k < el ? k : el)];
+#pragma unroll
+      for (uint32_t k = 0; k < kOwnScan; ++k) {
+        if (own && k <= el && (x[k] >> kESymShift) == c) {
+          const uint64_t f = x[k] & kELfMask;
+          fmin = f < fmin ? f : fmin;
+          fmax = f > fmax ? f : fmax;
+        }
+      }
+    }
+    if (valid && !(probe || small || wide)) {
+      uint64_t nl = 0, nh = 0;
+      if (reset) {
+        nh = v.n;
+      } else if (full) {
+        nl = ca < cb ? ca : 0;
+        nh = ca < cb ? cb : 0;
+      } else if (own && fmin != ~0ull) {
+        nl = fmin;
+        nh = fmax + 1;
+      }
+      lo_out[i] = nl;
+      hi_out[i] = nh;
+    }
+    // ---- the lists: one atomic per class per workgroup and block
+    const uint64_t bp = __ballot(probe), bs = __ballot(small), bw = __ballot(wide);
+    if (lane == 0) {
+      s_n[par][0][wv] = (uint32_t)__popcll(bp);
+      s_n[par][1][wv] = (uint32_t)__popcll(bs);
+      s_n[par][2][wv] = (uint32_t)__popcll(bw);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const uint32_t r = (uint32_t)(blk % kWorkRegions);
+    if (threadIdx.x < kLfClasses) {
+      uint32_t tot = 0;
+      for (uint32_t q = 0; q < kLfThreads / 64; ++q) tot += s_n[par][threadIdx.x][q];
+      s_base[par][threadIdx.x] = tot ? atomicAdd(&cnt[threadIdx.x * kWorkRegions + r], tot) : 0u;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (probe || small || wide) {
+      const uint32_t k = probe ? 0u : (small ? 1u : 2u);
+      const uint64_t bk = probe ? bp : (small ? bs : bw);
+      uint32_t pos = s_base[par][k];
+      for (uint32_t q = 0; q < wv; ++q) pos += s_n[par][k][q];
+      pos += (uint32_t)__popcll(bk & ((1ull << lane) - 1));
+      lt[((uint64_t)k * kWorkRegions + r) * cap + pos] = LfWork{l, h, c, i};
+    }
+    i = ni;
+    t = tn;
+    l = ln;
+    h = hn;
+  }
+}
+
+__global__ void __launch_bounds__(kLfThreads) k_lf_lists(DevView v, const LfWork* __restrict__ lt,
+                                                        const uint32_t* __restrict__ cnt, uint64_t cap,
+                                                        uint64_t* lo_out, uint64_t* hi_out,
+                                                        uint32_t waves_per_region) {
+  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
+  const uint32_t r = (uint32_t)(wave % kWorkRegions);
+  const uint64_t j0 = wave / kWorkRegions;
+  const uint64_t stride = waves_per_region;
+  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
+  const uint64_t np = cnt[0 * kWorkRegions + r], ns = cnt[1 * kWorkRegions + r], nw = cnt[2 * kWorkRegions + r];
+  const LfWork* P = lt + (uint64_t)(0 * kWorkRegions + r) * cap;
+  const LfWork* S = lt + (uint64_t)(1 * kWorkRegions + r) * cap;
+  const LfWork* Wl = lt + (uint64_t)(2 * kWorkRegions + r) * cap;
+  // every class's first items in one round trip; each loop loads its next
+  // item(s) before stepping the current ones
+  const auto pick = [](const LfWork* L, uint64_t n, uint64_t k) { return L[k < n ? k : 0]; };
+  LfWork xp = pick(P, np, j0 * kProbeRows + seg);
+  LfWork xs = pick(S, ns, j0 * 8 + seg);
+  LfWork xw = pick(Wl, nw, j0);
+  // ---- P: eight cached ranges per round trip
+  for (uint64_t b = j0; b * kProbeRows < np; b += stride) {   // wave-uniform
+    const bool act = b * kProbeRows + seg < np;
+    const LfWork x = xp;
+    xp = pick(P, np, (b + stride) * kProbeRows + seg);
+    const ProbeLoads pld = probe_issue<true>(v, x.l, x.h, x.sym);
+    bool hit;
+    uint64_t clo, chi, pid1;
+    probe_finish<true>(v, x.l, x.h, x.sym, act, pld, s_run[wv], hit, clo, chi, pid1);
+    if (act && hit && sl == 0) {
+      lo_out[x.row] = clo;
+      hi_out[x.row] = chi;
+    }
+    // misses (left-out keys, uncached ranges): the descent, one row at a time
+    uint64_t mb = __ballot(act && !hit && sl == 0);
+    while (mb) {
+      const int src = __ffsll((long long)mb) - 1;
+      mb &= mb - 1;
+      uint64_t ml = __shfl(x.l, src, 64), mh = __shfl(x.h, src, 64);
+      const uint64_t mc = __shfl(x.sym, src, 64), mp = __shfl(pid1, src, 64), mr = __shfl(x.row, src, 64);
+      const uint32_t* pw = mp ? v.cache_bm + (mp - 1) * v.bm_words + ((uint32_t)mc >> 5)
+                              : reinterpret_cast<const uint32_t*>(v.C);
+      const uint32_t pword = mp ? *pw : ~0u;
+      lf_step_tail(v, mc, pword, ml, mh);
+      if (lane == 0) {
+        lo_out[mr] = ml;
+        hi_out[mr] = mh;
+      }
+    }
+  }
+  // ---- S: eight ranges of <= kSmallScan rows per round trip, 8 lanes x 8 entries each
+  for (uint64_t b = j0; b * 8 < ns; b += stride) {   // wave-uniform
+    const bool act = b * 8 + seg < ns;
+    const LfWork x = xs;
+    xs = pick(S, ns, (b + stride) * 8 + seg);
+    const uint64_t last = x.h - 1;
+    uint64_t e[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint64_t idx = x.l + sl + 8 * k;
+      e[k] = v.E[idx < x.h ? idx : last];
+    }
+    uint64_t fmin = ~0ull, fmax = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint64_t idx = x.l + sl + 8 * k;
+      if (idx < x.h && (e[k] >> kESymShift) == x.sym) {
+        const uint64_t f = e[k] & kELfMask;
+        fmin = f < fmin ? f : fmin;
+        fmax = f > fmax ? f : fmax;
+      }
+    }
+#pragma unroll
+    for (int d = 1; d < (int)kProbeLanes; d <<= 1) {
+      const uint64_t a = __shfl_xor(fmin, d, 64), z = __shfl_xor(fmax, d, 64);
+      fmin = a < fmin ? a : fmin;
+      fmax = z > fmax ? z : fmax;
+    }
+    if (act && sl == 0) {
+      lo_out[x.row] = fmin != ~0ull ? fmin : 0;
+      hi_out[x.row] = fmin != ~0ull ? fmax + 1 : 0;
+    }
+  }
+  // ---- W: one row per wave
+  for (uint64_t j = j0; j < nw; j += stride) {   // wave-uniform
+    const LfWork x = xw;
+    xw = pick(Wl, nw, j + stride);
+    uint64_t l = x.l, h = x.h;
+    lf_step_tail(v, x.sym, ~0u, l, h);
+    if (lane == 0) {
+      lo_out[x.row] = l;
+      hi_out[x.row] = h;
+    }
+  }
+}
+
 // [sdsl] backward_search on an inclusive range with unsigned wrap-around.
 __device__ void sdsl_backward_search(const DevView& v, uint64_t c, uint64_t l, uint64_t r,
                                      uint64_t& lr, uint64_t& rr) {
@@ -922,10 +1160,9 @@ __device__ void sdsl_backward_search(const DevView& v, uint64_t c, uint64_t l, u
   uint64_t pl = l > v.n ? v.n : l;
   uint64_t pr = r + 1;
   if (pr > v.n) pr = v.n;
-  descend_full(v, (uint32_t)c, pl, pr);
-  const int64_t d = v.D[c];
-  lr = (uint64_t)((int64_t)pl + d);
-  rr = (uint64_t)((int64_t)pr + d) - 1;
+  descend_w2_thread(v, (uint32_t)c, pl, pr);
+  lr = pl;
+  rr = pr - 1;
 }
 
 __global__ void k_step_raw(DevView v, uint64_t sym, uint64_t low, uint64_t high, uint64_t* out) {
@@ -984,18 +1221,26 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* lds /*[
   return base + x - v;
 }
 
-// interval_symbols with counts: level-synchronous BFS over the 16-ary
-// wavelet matrix, one workgroup per row; children are appended in digit
-// order so the final frontier is in ascending symbol order.  Each frontier
-// node is expanded by 4 lanes, lane j ranking digits 4j..4j+3 at both
-// endpoints (the 4 lanes read the same two rank blocks: one coalesced
-// request), 64 nodes per workgroup round; a thread holds 8 ranks instead of
-// all 32 (no register spills), and a block-wide scan of the per-lane child
-// counts in (node, digit) order gives every child its output slot.
-// min_count > 1 prunes every prefix node holding fewer occurrences (so only
-// symbols occurring >= min_count times are reported, in O(width / min_count)
-// space); child_lo, when given, receives LF(lo, c) = C[c] + rank_c(lo) of
-// every reported symbol (the child range is [child_lo, child_lo + count)).
+// interval_symbols with counts: a level-synchronous BFS over the 2-level
+// wavelet matrix, one workgroup (4 waves) per row.  A frontier node (a range
+// of level l's sequence) is expanded by ONE wave into all R = 2^bits digit
+// children at once: rank_d at both ends for every d = superblock count + block
+// header + the digits before the end in its block, the last counted into an
+// LDS histogram (lane j takes digits [16 j, 16 j + 16) of each end's block) --
+// one round trip per node, 2 levels for a 17-bit alphabet (the 16-ary matrix
+// this replaced took 5 levels of 16-way expansion and 14 GiB at C3).  Lane j
+// owns digits [j R/64, (j+1) R/64) (or digit j when R < 64), so a wave scan of
+// the per-lane child counts orders a node's children by digit; the four waves
+// take consecutive nodes and a 4-entry LDS scan orders those.  Children are
+// appended in (node, digit) order, so the final frontier is in ascending
+// symbol order.  min_count > 1 prunes every prefix node holding fewer
+// occurrences (only symbols occurring >= min_count times are reported, in
+// O(width / min_count) space); child_lo, when given, receives LF(lo, c) =
+// C[c] + rank_c(lo) of every reported symbol (the child range is
+// [child_lo, child_lo + count)).
+constexpr uint32_t kDistWaves = 4;
+constexpr uint32_t kDistMaxR = 512;   // digits of <= 9 bits (device_build_w2)
+
 __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __restrict__ lo_a,
                                                  const uint64_t* __restrict__ hi_a, uint64_t m,
                                                  const uint64_t* __restrict__ cap_off,
@@ -1005,6 +1250,8 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
                                                  uint64_t min_count, uint64_t* __restrict__ child_lo,
                                                  bool cached_path) {
   __shared__ uint32_t wave_tot[4];
+  __shared__ uint32_t s_hist[kDistWaves][2][kDistMaxR];
+  __shared__ uint32_t s_cnt[kDistWaves];
   const uint64_t row = blockIdx.x;
   if (row >= m) return;
   uint64_t lo = lo_a[row], hi = hi_a[row];
@@ -1058,66 +1305,114 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     apre[0] = 0;
   }
   __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   uint64_t fc = 1;
   bool overflow = false;
-  const uint32_t d0 = 4 * (threadIdx.x & 3u);   // this lane's digits d0 .. d0 + 3
-  for (uint32_t lev = 0; lev < v.NL; ++lev) {
-    uint64_t zd[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) zd[j] = v.Z[lev * kRadix + d0 + j];
+  for (uint32_t lev = 0; lev < v.NL2; ++lev) {
+    const W2Level& L = v.w2[lev];
+    const uint32_t bits = L.bits, R = 1u << bits;
+    const uint32_t per = R >= 64 ? R / 64 : 1u;   // digits per lane
+    const uint32_t d0 = R >= 64 ? lane * per : lane;
+    const bool lane_on = d0 < R;
     uint64_t out = 0;
-    for (uint64_t t0 = 0; t0 < fc; t0 += 64) {
-      const uint64_t i = t0 + (threadIdx.x >> 2);
-      uint64_t cl[4] = {0, 0, 0, 0}, ch[4] = {0, 0, 0, 0};
-      uint32_t p = 0, nchild = 0;
-      if (i < fc) {
+    for (uint64_t t0 = 0; t0 < fc; t0 += kDistWaves) {   // workgroup-uniform
+      const uint64_t i = t0 + wv;
+      const bool node = i < fc;
+      for (uint32_t d = lane; d < R; d += 64) {
+        s_hist[wv][0][d] = 0;
+        s_hist[wv][1][d] = 0;
+      }
+      __syncthreads();
+      uint32_t p = 0;
+      uint64_t sbv[2][8];
+      uint32_t hdr[2][8];
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+          sbv[e][u] = 0;
+          hdr[e][u] = 0;
+        }
+      if (node) {
         p = apre[i];
-        const uint64_t il = alo[i], ih = ahi[i];
-        const uint64_t bl = il / kBlkDigits, bh = ih / kBlkDigits;
-        const uint32_t kl = (uint32_t)(il - bl * kBlkDigits), kh = (uint32_t)(ih - bh * kBlkDigits);
-        const uint4* xl = rank_block(v, lev, bl);
-        const uint4* xh = rank_block(v, lev, bh);
-        uint4 a[kBlkU4], b[kBlkU4];
 #pragma unroll
-        for (int q = 0; q < kBlkU4; ++q) {
-          a[q] = xl[q];
-          b[q] = xh[q];
-        }
-        const uint64_t* sl = sb_row(v, lev, bl);
-        const uint64_t* sh = sb_row(v, lev, bh);
+        for (int e = 0; e < 2; ++e) {
+          const uint64_t x = e ? ahi[i] : alo[i];
+          const uint32_t k = (uint32_t)(x & (kW2Blk - 1));
+          const uint8_t* blk = L.blocks + (x >> kW2BlkLog2) * L.blk_bytes;
+          const uint64_t* sbp = L.sb + (x >> kW2SbLog2) * R;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          cl[j] = sl[d0 + j];
-          ch[j] = sh[d0 + j];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-          for (uint32_t q = 0; q < kBlkU4; ++q) {
-            cl[j] += block_part(a[q], q, d0 + j, kl);
-            ch[j] += block_part(b[q], q, d0 + j, kh);
-          }
-          nchild += (ch[j] >= cl[j] + min_count) ? 1u : 0u;
-        }
-      }
-      uint32_t tot;
-      uint64_t pos = out + block_scan_u32(nchild, wave_tot, tot);
-      if (nchild) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (ch[j] >= cl[j] + min_count) {
-            if (pos < cap) {
-              blo[pos] = zd[j] + cl[j];
-              bhi[pos] = zd[j] + ch[j];
-              bpre[pos] = (p << 4) | (d0 + j);
+          for (uint32_t u = 0; u < 8; ++u) {
+            if (lane_on && u < per) {
+              sbv[e][u] = sbp[d0 + u];
+              hdr[e][u] = reinterpret_cast<const uint16_t*>(blk)[d0 + u];
             }
-            ++pos;
+          }
+          // the digits before the end in its block: lane j counts [16 j, 16 j + 16)
+          const uint32_t j0 = 16 * lane;
+          if (j0 < k) {
+            uint32_t w[8];
+            if (bits > 8) {
+              const uint4* q = reinterpret_cast<const uint4*>(blk + 2 * R) + 2 * lane;
+              const uint4 x0 = q[0], x1 = q[1];
+              w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+              w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+            } else {
+              const uint4 x0 = reinterpret_cast<const uint4*>(blk + 2 * R)[lane];
+              w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+              w[4] = w[5] = w[6] = w[7] = 0;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j) {
+              const uint32_t dig = bits > 8 ? (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu
+                                            : (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+              if (j0 + j < k) atomicAdd(&s_hist[wv][e][dig], 1u);
+            }
           }
         }
       }
-      out += tot;
+      __syncthreads();
+      uint64_t ra[8], rb[8];
+      uint32_t nchild = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const bool on = node && lane_on && u < per;
+        ra[u] = on ? sbv[0][u] + hdr[0][u] + s_hist[wv][0][d0 + u] : 0;
+        rb[u] = on ? sbv[1][u] + hdr[1][u] + s_hist[wv][1][d0 + u] : 0;
+        nchild += (on && rb[u] >= ra[u] + min_count) ? 1u : 0u;
+      }
+      // the node's children in digit order (wave scan), the nodes in wave order
+      uint32_t inc = nchild;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+      if (lane == 63) s_cnt[wv] = inc;
+      __syncthreads();
+      uint64_t pos = out + inc - nchild, all = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kDistWaves; ++w) {
+        const uint32_t cw = s_cnt[w];
+        pos += w < wv ? cw : 0u;
+        all += cw;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        const bool on = node && lane_on && u < per;
+        if (on && rb[u] >= ra[u] + min_count) {
+          if (pos < cap) {
+            const uint64_t z = L.Z[d0 + u];
+            blo[pos] = z + ra[u];
+            bhi[pos] = z + rb[u];
+            bpre[pos] = (p << bits) | (d0 + u);
+          }
+          ++pos;
+        }
+      }
+      out += all;
+      __syncthreads();   // s_hist / s_cnt are reused by the next nodes
     }
-    __syncthreads();
     if (out > cap) {
       overflow = true;
       break;
@@ -1128,6 +1423,8 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
     t = alo; alo = blo; blo = t;
     t = ahi; ahi = bhi; bhi = t;
     tp = apre; apre = bpre; bpre = tp;
+    __threadfence_block();
+    __syncthreads();   // this level's frontier writes before the next level reads them
   }
   if (overflow) {
     if (threadIdx.x == 0) k_out[row] = ~0ull;
@@ -1136,7 +1433,7 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
   for (uint64_t i = threadIdx.x; i < fc; i += 256) {
     syms[base + i] = apre[i];
     counts[base + i] = ahi[i] - alo[i];
-    if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D[apre[i]]);
+    if (child_lo) child_lo[base + i] = (uint64_t)((int64_t)alo[i] + v.D2[apre[i]]);
   }
   if (threadIdx.x == 0) k_out[row] = fc;
 }
@@ -1145,18 +1442,20 @@ __global__ void __launch_bounds__(256) k_distinct(DevView v, const uint64_t* __r
 // its symbols are the set bits of its cached bitmap, already in ascending
 // order, and the count of symbol c is the width of the child range the
 // transition table holds for (range, c) -- or, for a key the table left out,
-// the width of the 16-ary descent of both ends.  A row is split over
+// the width of the wavelet-matrix descent of both ends.  A row is split over
 // kDcChunks workgroups of 256 words (8192 symbols); a workgroup's output
 // offset is the popcount of the bitmap words before its chunk.  Only for
 // min_count == 1 with a transition table (not while the table is being built).
 constexpr uint32_t kDcWords = 256;
 
-// the child of (lo, hi) by symbol c: from slot `slot` + d of its probe run on
-// (the caller has checked the first `d0` slots)
-__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint64_t slot,
-                                         uint32_t d0, uint64_t& clo, uint64_t& cnt) {
+// the child of (lo, hi) by symbol c: a scan of its candidate slots from
+// candidate d0 on (the caller has checked the others)
+__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint32_t d0,
+                                         uint64_t& clo, uint64_t& cnt) {
   const uint64_t key0 = lo | ((uint64_t)c << kTransSymShift);
+  const TransHome th = trans_home(lo, hi, c, v.trans_cap);
   for (uint32_t d = d0; d < kTransProbe; ++d) {
+    const uint64_t slot = trans_slot(th, d);
     const uint64_t w0 = v.trans_tab[3 * slot], w1 = v.trans_tab[3 * slot + 1];
     if (w0 == key0 && (w1 & kMask34) == hi) {
       const uint64_t w2 = v.trans_tab[3 * slot + 2];
@@ -1164,12 +1463,15 @@ __device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t
       cnt = (w2 >> 4) & kMask34;
       return;
     }
-    if (w0 == kTransEmpty) break;     // slots are claimed first-empty-from-home and never freed
-    if (++slot == v.trans_cap) slot = 0;
+    // a bucket fills from its first slot and is never emptied: an empty slot ends it
+    if (w0 == kTransEmpty) {
+      if (d >= kTransBucket) break;
+      d = kTransBucket - 1;
+    }
   }
   uint64_t pl = lo, pr = hi;           // a key the table left out: the descent
-  descend_full(v, c, pl, pr);
-  clo = (uint64_t)((int64_t)pl + v.D[c]);
+  descend_w2_thread(v, c, pl, pr);
+  clo = pl;
   cnt = pr - pl;
 }
 
@@ -1230,17 +1532,14 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
         cs[u] = 0;
       }
     }
-    // the first two slots of every symbol's probe run, issued together
-    // (linear probing at load <= 0.57: most keys sit in one of them)
-    uint64_t sl0[4], q[4][6];
+    // the first slot of both buckets of every symbol, issued together
+    uint64_t q[4][6];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool pr = !fullr && u < nb;
-      uint64_t a = pr ? trans_home(lo, hi, cs[u], v.trans_cap) : 0;
-      uint64_t b = a + 1 == v.trans_cap ? 0 : a + 1;
-      sl0[u] = a;
+      const TransHome th = pr ? trans_home(lo, hi, cs[u], v.trans_cap) : TransHome{0, 0};
+      const uint64_t a = th.a, b = th.b;
       const uint64_t* tt = pr ? v.trans_tab : v.C;   // C[0..2]: a valid dummy address
-      if (!pr) a = b = 0;
 #pragma unroll
       for (int w = 0; w < 3; ++w) {
         q[u][w] = tt[3 * a + w];
@@ -1262,15 +1561,13 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
           } else if (q[u][3] == key0 && (q[u][4] & kMask34) == hi) {
             clo = (q[u][4] >> kTransSymShift) | ((q[u][5] & 0xFu) << 30);
             cnt = (q[u][5] >> 4) & kMask34;
-          } else if (q[u][0] == kTransEmpty || q[u][3] == kTransEmpty) {
+          } else if (q[u][0] == kTransEmpty && q[u][3] == kTransEmpty) {
             uint64_t pl = lo, pr2 = hi;    // not in the table (left out): the descent
-            descend_full(v, cs[u], pl, pr2);
-            clo = (uint64_t)((int64_t)pl + v.D[cs[u]]);
+            descend_w2_thread(v, cs[u], pl, pr2);
+            clo = pl;
             cnt = pr2 - pl;
           } else {
-            uint64_t s2 = sl0[u] + 2;
-            if (s2 >= v.trans_cap) s2 -= v.trans_cap;
-            child_of(v, lo, hi, cs[u], s2, 2, clo, cnt);
+            child_of(v, lo, hi, cs[u], 0, clo, cnt);
           }
         }
         if (pos - base < cap) {
@@ -1370,6 +1667,7 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
+  bool lists;         // k_lf_class + k_lf_lists (lf_work 3) when a workspace is given
   uint64_t sweep_min; // work_inline from this many rows (lf_work -1: lf_sweep_min; 2: min_rows)
   bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
@@ -1388,6 +1686,7 @@ LfTuning load_lf_tuning() {
   const bool autow = p.lf_work < 0;
   t.work = p.lf_work == 1;
   t.work_inline = autow || p.lf_work == 2;
+  t.lists = p.lf_work == 3;
   t.sweep_min = autow ? p.lf_sweep_min : 0;
   t.search_p8 = p.search_p8 != 0;
   return t;
@@ -1404,6 +1703,7 @@ bool lf_gprobe() { return lf_tuning().gprobe; }
 bool lf_quad() { return lf_tuning().quad; }
 bool lf_split() { return lf_tuning().split; }
 bool lf_work() { return lf_tuning().work; }
+bool lf_lists() { return lf_tuning().lists; }
 
 // worklist geometry for m rows: entries per region, sweep-1 waves
 uint64_t lf_work_cap(uint64_t m) {
@@ -1416,6 +1716,8 @@ uint64_t lf_work_cap(uint64_t m) {
 void reload_lf_tuning() { lf_tuning() = load_lf_tuning(); }
 
 size_t lf_ws_bytes(uint64_t m) {
+  if (m > lf_tuning().min_rows && lf_lists())
+    return kLfClasses * kWorkRegions * (lf_work_cap(m) * sizeof(LfWork) + 4);
   return m > lf_tuning().min_rows && lf_work() ? kWorkRegions * lf_work_cap(m) * sizeof(LfWork) + kWorkRegions * 4 : 0;
 }
 
@@ -1428,6 +1730,19 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
     const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
     k_lf_sweep<true><<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, nullptr,
                                                nullptr, 0);
+    FM_HIP(hipGetLastError());
+    return 0;
+  }
+  if (ws && m > lf_tuning().min_rows && lf_lists()) {
+    const uint64_t cap = lf_work_cap(m);
+    LfWork* lt = reinterpret_cast<LfWork*>(ws);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lt + kLfClasses * kWorkRegions * cap);
+    FM_HIP(hipMemsetAsync(cnt, 0, kLfClasses * kWorkRegions * 4, s));
+    const uint64_t nblk = (m + kLfThreads - 1) / kLfThreads;
+    const unsigned g1 = (unsigned)(kClassWgs ? std::min<uint64_t>(nblk, kClassWgs) : nblk);
+    k_lf_class<<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, lt, cnt, cap);
+    const uint32_t q = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kListWaves / kWorkRegions, cap));
+    k_lf_lists<<<q * kWorkRegions / (kLfThreads / 64), kLfThreads, 0, s>>>(v, lt, cnt, cap, lo_out, hi_out, q);
     FM_HIP(hipGetLastError());
     return 0;
   }

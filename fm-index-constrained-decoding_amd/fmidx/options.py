@@ -27,7 +27,7 @@ class BuildOptions(ctypes.Structure):
     """fm_build_options."""
     _fields_ = [("size", c_uint32), ("profile", c_int32), ("transitions", c_int32), ("lf_e", c_int32),
                 ("lf_e2", c_int32), ("probe_first", c_int32), ("keep_bwt", c_int32), ("follow_bitmaps", c_int32),
-                ("bm_log2", c_int32), ("reserved", c_int32), ("cache_min", c_uint64), ("cache_mb", c_uint64),
+                ("bm_log2", c_int32), ("trans_min", c_int32), ("cache_min", c_uint64), ("cache_mb", c_uint64),
                 ("trans_mb", c_uint64), ("gpu_sort_min", c_uint64)]
 
     def as_dict(self) -> dict:

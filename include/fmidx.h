@@ -56,7 +56,7 @@ void fm_destroy(fm_index* h);
  * counterpart: sdsl's csa_wt_int<> has one layout, fm_index.hpp:36).  Set on
  * a handle before any fm_initialize* (or give it to fm_load_ex); the values
  * in force are fm_get_build_options'.  fm_build_options_init fills a profile:
- *   FM_PROFILE_DEFAULT -- every structure (117.9 GiB at n = 4.5e9, V = 128256;
+ *   FM_PROFILE_DEFAULT -- every structure (89.1 GiB at n = 4.5e9, V = 128256;
  *     13.8 us per cold B = 256 decode step);
  *   FM_PROFILE_COMPACT -- transitions to cached children only, no E array,
  *     the transition probe issued with the descent (54.3 GiB there, +24 % cold).
@@ -76,7 +76,7 @@ typedef struct fm_build_options {
   int32_t keep_bwt;         /* 1: keep the plain BWT although E holds its symbols */
   int32_t follow_bitmaps;   /* 1: a bitmap per symbol of its C-block (0: the range cache holds the wide ones) */
   int32_t bm_log2;          /* aligned bitmap block, log2 rows; -1: by n (16 from 2^31 rows, 14 from 2^26, 12 below) */
-  int32_t reserved;
+  int32_t trans_min;        /* transitions = 2: only the children of >= trans_min occurrences (1); <= 0: the profile's */
   uint64_t cache_min;       /* range-bitmap cache: every SA range of >= cache_min rows reachable from the root (4096) */
   uint64_t cache_mb;        /* its budget, MiB (48 GiB) */
   uint64_t trans_mb;        /* the transition table's budget, MiB (72 GiB; past it: cached children only) */
@@ -99,7 +99,8 @@ typedef struct fm_tuning {
   uint32_t reserved;
   uint64_t lf_group_min;    /* grouped LF / get_range kernels above this many rows (8192) */
   int32_t lf_work;          /* -1: the in-wave sweep from lf_sweep_min rows, else the grouped kernel; 0 grouped only;
-                               1 sweep + worklist tail; 2 in-wave sweep whenever grouped */
+                               1 sweep + worklist tail; 2 in-wave sweep whenever grouped; 3 class lists
+                               (k_lf_class + k_lf_lists) */
   int32_t lf_gprobe;        /* groups of >= 4 lanes probe the transition table themselves (1) */
   int32_t lf_quad;          /* two-lane LF launches settle wide rows four at a time first (1) */
   int32_t lf_split;         /* two-pass LF launch, cheap rows then wide rows (0: measured slower) */
@@ -533,8 +534,9 @@ int fm_processor_shard_finish(const fm_prep_config* cfg, const fm_processor_args
 
 /* ---- introspection (bench / roofline accounting) ----------------------- */
 
-/* Digit levels of the 16-ary wavelet matrix (one dependent rank round trip
- * each per LF step), bytes of each device structure. */
+/* Digit levels of the wavelet matrix (the 2-level one: one dependent rank
+ * round trip each per LF step) and its bytes, bytes of the plain BWT (0 once
+ * E holds the symbols) and of the bitmaps, the aligned bitmap block. */
 int fm_stats(const fm_index* h, uint64_t* levels, uint64_t* wm_bytes, uint64_t* bwt_bytes,
              uint64_t* bitmap_bytes, uint64_t* bitmap_block);
 
@@ -545,7 +547,7 @@ int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint
                 uint64_t* cache_bytes, uint64_t* cache_min);
 
 /* Transition table of the cached ranges (cached parent, symbol) -> child range:
- * entries inserted, entries left out (probe window full; those steps take the
+ * entries inserted, entries left out (both buckets full; those steps take the
  * wavelet-matrix descent) and bytes in HBM. */
 int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes);
 

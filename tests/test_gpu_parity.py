@@ -271,7 +271,7 @@ _GROUPED_VARIANTS = [{}, {"lf_group": 1}, {"lf_quad": 0}, {"lf_split": 1},
                      {"lf_group": 8, "search_group": 8, "lf_gprobe": 1},
                      {"lf_group": 16, "search_group": 16},
                      {"lf_group": 64, "search_group": 64}]
-_LF_VARIANTS = _GROUPED_VARIANTS + [{"lf_work": 0}, {"lf_work": 1}, {"lf_work": 2}, {"search_p8": 0}]
+_LF_VARIANTS = _GROUPED_VARIANTS + [{"lf_work": 0}, {"lf_work": 1}, {"lf_work": 2}, {"lf_work": 3}, {"search_p8": 0}]
 
 
 @pytest.mark.parametrize("variant", _LF_VARIANTS, ids=lambda v: "-".join(f"{k}{x}" for k, x in v.items()) or "default")
@@ -851,13 +851,32 @@ def _device_u8(ptr, nbytes, owner):
     return torch.as_tensor(_V(), device=torch.device("cuda", 0))
 
 
+def _trans_home(lo, hi, c, cap):
+    """trans_home (csrc/fmidx_internal.h) in Python integers: the first slots of
+    a key's two buckets."""
+    M = (1 << 64) - 1
+
+    def cache_hash(a, b):
+        x = ((a * 0x9E3779B97F4A7C15) & M) ^ (((b + 0x632BE59BD9B4E019) & M) * 0xC2B2AE3D27D4EB4F & M)
+        x ^= x >> 29
+        x = (x * 0xBF58476D1CE4E5B9) & M
+        return x ^ (x >> 32)
+
+    h = cache_hash(lo ^ ((c * 0xD6E8FEB86659FD93) & M), (hi + c) & M)
+    g = ((h ^ (h >> 31)) * 0x94D049BB133111EB) & M
+    g ^= g >> 29
+    nb = cap // 8
+    return ((h * nb) >> 64) * 8, ((g * nb) >> 64) * 8
+
+
 def test_device_structs(dev):
     """fm_device_struct (the bench's gather ceilings over the index's own
     allocations) reports each structure's pointer and size, and the structures
     are what the kernels assume: E[i] = LF(i) | BWT[i] << 36 with LF the
     stable order of the BWT by symbol (LF(i) = C[BWT[i]] + rank), and the
-    transition table's kTransPad (32) slots past its end mirror its first 32
-    (csrc/cache.hip), so a probe run is read without wrapping."""
+    transition table is 8-slot buckets of 24-B slots, each filled from its
+    first slot, with every key in one of its two buckets (trans_home,
+    csrc/fmidx_internal.h)."""
     import torch
 
     docs = markov_docs(11, 300, 200, 120)
@@ -876,9 +895,19 @@ def test_device_structs(dev):
     order = torch.argsort(bwt, stable=True)
     assert torch.equal(lf[order], torch.arange(n, device=dev))
     p2, b2 = ours.device_struct(2)
-    assert p2 and b2 > 0 and b2 % 24 == 0
-    tab = _device_u8(p2, b2 + 32 * 24, ours)
-    assert torch.equal(tab[b2:], tab[:32 * 24])
+    assert p2 and b2 > 0 and b2 % 192 == 0
+    tab = _device_u8(p2, b2, ours).view(torch.int64).cpu().numpy().view(np.uint64).reshape(-1, 8, 3)
+    nb = tab.shape[0]
+    empty = tab[:, :, 0] == np.uint64(2**64 - 1)
+    assert not (empty[:, :-1] & ~empty[:, 1:]).any()          # filled from the first slot
+    m34 = (1 << 34) - 1
+    keys = 0
+    for b, k in zip(*np.nonzero(~empty)):
+        w0, w1 = int(tab[b, k, 0]), int(tab[b, k, 1])
+        ha, hb = _trans_home(w0 & m34, w1 & m34, w0 >> 34, 8 * nb)
+        assert 8 * b in (ha, hb)
+        keys += 1
+    assert keys == ours.stats()["trans_entries"]
     for w in (3, 4):
         p, b = ours.device_struct(w)
         assert p and b > 0

@@ -6,6 +6,9 @@ final states against the trace and every step's mask against the first
 library's (saved masks), and prints one JSON line per library.
 
 usage: python tools/ab_decode.py [--tokens 4.5e9] [--reps 7] lib_a.so lib_b.so ...
+A library argument may carry build options for its process:
+lib.so@trans_min=2,lf_e=0 (FMIDX_BUILD_OPTIONS); the line then reports the
+index's device bytes and transition-table counts too.
 """
 import argparse
 import json
@@ -70,7 +73,13 @@ def child(args):
         same = bool(np.array_equal(np.load(ref), m))
     else:
         np.save(ref, m)
-    print(json.dumps({"lib": os.environ.get("FMIDX_LIB"), "cold_us": sorted(cold), "warm_us": sorted(warm),
+    try:
+        st = fm.stats()
+    except AttributeError:     # a library older than the stats it asks for
+        st = {"device_bytes": 0, "trans_bytes": 0, "trans_entries": -1, "trans_dropped": -1}
+    print(json.dumps({"lib": os.environ.get("FMIDX_LIB"), "build_options": os.environ.get("FMIDX_BUILD_OPTIONS", ""),
+                      "device_gib": st["device_bytes"] / 2**30, "trans_gib": st["trans_bytes"] / 2**30,
+                      "trans_entries": st["trans_entries"], "trans_dropped": st["trans_dropped"], "cold_us": sorted(cold), "warm_us": sorted(warm),
                       "cold_median": float(np.median(cold)), "warm_median": float(np.median(warm)),
                       "trace_ok": ok, "mask_equal_first_lib": same}), flush=True)
 
@@ -80,7 +89,7 @@ def main():
     ap.add_argument("--tokens", type=float, default=4.5e9)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=7)
-    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "ab"))
+    ap.add_argument("--out", default="/tmp/ab_decode")   # the saved mask: box-local
     ap.add_argument("--child", action="store_true")
     ap.add_argument("libs", nargs="*")
     args = ap.parse_args()
@@ -93,7 +102,10 @@ def main():
         os.remove(ref)
     rc = 0
     for lib in args.libs:
+        lib, _, opts = lib.partition("@")
         env = dict(os.environ, FMIDX_LIB=os.path.abspath(lib))
+        if opts:
+            env["FMIDX_BUILD_OPTIONS"] = opts
         r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--child", "--tokens", str(args.tokens),
                             "--batch", str(args.batch), "--reps", str(args.reps), "--out", args.out], env=env)
         rc = rc or r.returncode

@@ -3,8 +3,9 @@ index: the call the reference's processors make every decode step
 (get_distinct_count_multi over the B rows' ranges, index.py:161-174).
 
 For B = 256 rows of the bench's decode trace at several steps: the device
-launch alone (fm_distinct_count_batch: 16-ary wavelet BFS, one workgroup per
-range), and the SWIG-surface call end to end (fm_distinct_count_multi: launch +
+launch alone (fm_distinct_count_batch: cached ranges from their bitmaps and
+the transition table, the rest by the 2-level wavelet-matrix BFS, one workgroup
+per range), and the SWIG-surface call end to end (fm_distinct_count_multi: launch +
 device compaction + copy + Python tuples), against oracle/cpu_ref's
 sdsl-faithful distinct_count (the reference's algorithm, sigma-sized scratch per
 call) on one thread and on all cores.  Results must agree exactly.
