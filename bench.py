@@ -288,6 +288,26 @@ def gather_ceiling(dev, nbytes=8 << 30):
             best = ms if best is None else min(best, ms)
         rates[name] = threads // lpl * loads * line / (best * 1e-3) / 1e9
     gbs = max(rates["lane_64B"], rates["coop4_64B"])
+    # the same shapes at the rank launch's size and temperature: ~1M requests
+    # (2^19 pairs make ~1.07M) in ONE launch right after a 1 GiB eviction --
+    # what a short cold gather kernel reaches, ramp and drain included
+    flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+    for mode in (4, 3):
+        name, lpl, line = GATHER_MODES[mode]
+        thr = (1 << 20) * lpl // 8
+        ts = []
+        for _ in range(3):
+            flush.add_(1)
+            torch.cuda.synchronize()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            check(lib().fm_probe_gather(buf.data_ptr(), nbytes, mode, 8, thr, sink.data_ptr(), stream), "probe")
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        rates[name + "_1M_cold"] = thr // lpl * 8 * line / (float(np.median(ts)) * 1e-3) / 1e9
+    del flush
     hops, chains = 4000, 256
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
@@ -1462,6 +1482,9 @@ def main():
     req_ceiling = max(gm.get("coop8_128B", 0) / 128, gm.get("coop4_64B", 0) / 64,
                       gm.get("lane_8B", 0) / 8)          # G requests/s (GB/s / B per request)
     result["rank"]["request_ceiling_G_per_s"] = req_ceiling
+    # the same at the launch's own size, cold (gather_ceiling: ~1M requests after an eviction)
+    req_ceiling_1m = max(gm.get("coop8_128B_1M_cold", 0) / 128, gm.get("lane_8B_1M_cold", 0) / 8)
+    result["rank"]["request_ceiling_1M_cold_G_per_s"] = req_ceiling_1m
     # the rank figure comes from this bench's own 2^19-pair launch (pmc_req_c3.json, counted over the
     # same command) when that file has it, else from tools/probe_rank.py's launch of the same shape
     have_c3_rank = False
@@ -1500,6 +1523,7 @@ def main():
                 rate = req / (us * 1e-6) / 1e9
                 result["rank"]["request_rate_G_per_s"] = rate
                 result["rank"]["frac_of_request_ceiling"] = rate / req_ceiling if req_ceiling else None
+                result["rank"]["frac_of_request_ceiling_1M_cold"] = rate / req_ceiling_1m if req_ceiling_1m else None
         except Exception as e:
             result[where]["pmc_requests_source"] = f"unreadable: {e!r}"
     if cpu_leg:

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--lf-work", type=int, default=3)
     ap.add_argument("--rows", type=int, default=65536, help="trace rows (pairs = 8 x rows)")
     ap.add_argument("--compare", default="", help="also the 'all' set under these lf_work values, e.g. -1,0")
+    ap.add_argument("--split", type=int, default=0, help="also the 'all' set as this many parts on as many streams")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     fm, text, bwt, _ = bench.build_index(int(4.5e9), 128256, 20250905, dev)
@@ -73,6 +74,33 @@ def main():
                 ts.append(a.elapsed_time(b) * 1e3)
         res[f"all_lf_work{lw}"] = {"cold_us": float(np.median(ts[1:])),
                                    "exact": bool(torch.equal(o1, ref[0]) and torch.equal(o2, ref[1]))}
+    if args.split > 1:
+        K = args.split
+        parts = torch.tensor_split(torch.arange(tok.numel(), device=dev), K)
+        ins = [(tok[p].contiguous(), lo[p].contiguous(), hi[p].contiguous()) for p in parts]
+        outs = [(torch.empty_like(x[1]), torch.empty_like(x[2])) for x in ins]
+        streams = [torch.cuda.Stream(dev) for _ in range(K)]
+        for lw in (args.lf_work, 0):
+            ts = []
+            with tuning(lf_work=lw):
+                for _ in range(4):
+                    flush.add_(1)
+                    torch.cuda.synchronize()
+                    a = torch.cuda.Event(enable_timing=True)
+                    b = torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    cur = torch.cuda.current_stream(dev)
+                    for (t_, l_, h_), (o1, o2), st in zip(ins, outs, streams):
+                        st.wait_stream(cur)
+                        with torch.cuda.stream(st):
+                            fm.lf_step_batch(t_, l_, h_, bench.SHIFT, lo_out=o1, hi_out=o2, reset_below=0)
+                    for st in streams:
+                        cur.wait_stream(st)
+                    b.record()
+                    torch.cuda.synchronize()
+                    ts.append(a.elapsed_time(b) * 1e3)
+            ok = all(torch.equal(o[0], ref[0][p]) and torch.equal(o[1], ref[1][p]) for o, p in zip(outs, parts))
+            res[f"all_split{K}_lf_work{lw}"] = {"cold_us": float(np.median(ts[1:])), "exact": bool(ok)}
     print(json.dumps(res), flush=True)
 
 
