@@ -297,8 +297,10 @@ def gather_ceiling(dev, nbytes=8 << 30):
         thr = (1 << 20) * lpl // 8
         ts = []
         for _ in range(3):
-            flush.add_(1)
+            # enqueued behind the eviction while it runs (as the rank legs' timed() queued=True):
+            # the events bracket the gather kernel, not the host's launch latency
             torch.cuda.synchronize()
+            flush.add_(1)
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record()
@@ -1168,15 +1170,22 @@ def main():
     def evict():
         flush.add_(1)
 
-    def timed(graph, reps=1, reset=False, cold=False):
+    def timed(graph, reps=1, reset=False, cold=False, queued=False):
+        # queued (one-launch graphs, the rank legs): the replay is enqueued behind the
+        # eviction while the GPU is still busy with it, so the events bracket the
+        # kernel itself and not the host's graph-launch latency (~10 us, which a
+        # 20-step replay spreads over its steps but a one-launch replay would carry whole)
         ts = []
         for _ in range(reps):
             if reset:
                 lo.copy_(state_lo)
                 hi.copy_(state_hi)
+            if queued:
+                torch.cuda.synchronize()
             if cold:
                 evict()
-            torch.cuda.synchronize()
+            if not queued:
+                torch.cuda.synchronize()
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record()
@@ -1200,12 +1209,12 @@ def main():
     g_lfbig = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g_lfbig):
         fm.lf_step_batch(all_tok, all_lo, all_hi, SHIFT, lo_out=big_lo, hi_out=big_hi, reset_below=0)
-    lfbig_cold = timed(g_lfbig, 3, cold=True)
+    lfbig_cold = timed(g_lfbig, 3, cold=True, queued=True)
     rs_olo, rs_ohi = torch.empty_like(rs_lo), torch.empty_like(rs_hi)
     g_rs = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g_rs):
         fm.lf_step_batch(rs_tok, rs_lo, rs_hi, SHIFT, lo_out=rs_olo, hi_out=rs_ohi, reset_below=0)
-    rs_cold = timed(g_rs, 3, cold=True)
+    rs_cold = timed(g_rs, 3, cold=True, queued=True)
     rs_ok = bool(torch.equal(rs_olo, rs_ref[0]) and torch.equal(rs_ohi, rs_ref[1]))
     r2 = None
     if r2_tok is not None:
@@ -1213,7 +1222,7 @@ def main():
         g_r2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_r2):
             fm.lf_step_batch(r2_tok, r2_lo, r2_hi, SHIFT, lo_out=r2_olo, hi_out=r2_ohi, reset_below=0)
-        r2_cold = timed(g_r2, 3, cold=True)
+        r2_cold = timed(g_r2, 3, cold=True, queued=True)
         r2_warm = timed(g_r2, 3)
         r2 = {"rows": int(r2_tok.numel()), "avg_launch_us_cold": float(np.median(r2_cold)) * 1e3,
               "avg_launch_us_warm": float(np.median(r2_warm)) * 1e3,

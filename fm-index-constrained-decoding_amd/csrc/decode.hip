@@ -60,6 +60,10 @@ __host__ __device__ constexpr uint32_t win_words(uint64_t sw) { return (uint32_t
 #define FMIDX_EARLY_ZERO_WIDTH 64   // measurement variant (make variant VFLAGS=-DFMIDX_EARLY_ZERO_WIDTH=512)
 #endif
 constexpr uint64_t kEarlyZeroWidth = FMIDX_EARLY_ZERO_WIDTH;   // rows this narrow get their zeros written up front
+#ifndef FMIDX_EZ_SLEEP
+#define FMIDX_EZ_SLEEP 0   // measurement variant: s_sleep (x 64 clocks) between a thread's early zero stores
+#endif
+constexpr int kEzSleep = FMIDX_EZ_SLEEP;
 constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
 constexpr uint32_t kPayMagic = 0x58534D46u;    // the shard payload's magic (csrc/shard.hip)
 constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144
@@ -465,6 +469,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // waiting for them -- wave 0 (LF + plan) must stay store-free.
   if (early_zero && threadIdx.x >= kEzFirst) {
     for (uint64_t k = threadIdx.x - kEzFirst; k < nch; k += kDecThreads - kEzFirst) {
+      if (kEzSleep && k >= kDecThreads - kEzFirst) __builtin_amdgcn_s_sleep(kEzSleep);
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
         store4(orsrc, (uint32_t)(k * 4), 0u);

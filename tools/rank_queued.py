@@ -1,0 +1,169 @@
+"""Where the cold cost of the rank (LF) launch and of the decode step goes.
+
+Builds the bench's C3 index and times, each with the replay enqueued behind
+the work that precedes it (so the events bracket the kernels, not the host's
+graph-launch latency):
+  * the LF launch over 2^19 and 2^21 (state, token) pairs of a decode trace,
+    for every LF variant (tuning lf_work 0 grouped, 2 in-wave sweep, 3 class
+    lists), in three temperatures:
+      cold     -- after the bench's 1 GiB eviction;
+      ptewarm  -- after the eviction, then random 8-B reads spread over every
+                  index structure (warms the page-table lines / TLB, but hits
+                  none of the pairs' lines except by chance);
+      warm     -- back-to-back with the same launch;
+  * the fused decode step (K = 20 steps in one graph, the bench's trace) in
+    the same three temperatures;
+  * the 1M-request random-gather ceiling (8-B words, 128-B lines) over a fresh
+    8 GiB buffer and over E, cold and ptewarm.
+usage: python tools/rank_queued.py [--tokens 4.5e9] [--out file.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "fm-index-constrained-decoding_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from fmidx._lib import check, lib  # noqa: E402
+from fmidx.options import set_tuning  # noqa: E402
+from fmidx.synth import decode_trace  # noqa: E402
+
+SHIFT = bench.SHIFT
+STRUCTS = {0: "bwt", 1: "E", 2: "trans", 3: "cache_bm", 4: "w2_level0"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=float, default=4.5e9)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    V = 128256
+    fm, text, bwt, _ = bench.build_index(int(args.tokens), V, 20250905, dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sink = torch.zeros(1024, dtype=torch.int64, device=dev)
+    flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+    structs = [(STRUCTS[w],) + tuple(fm.device_struct(w)) for w in STRUCTS]
+    structs = [s for s in structs if s[1] and s[2] >= (1 << 20)]
+
+    def ptewarm():
+        # 2^19 random 8-B reads over every structure: every 2 MB page touched many times
+        for _, ptr, nbytes in structs:
+            check(lib().fm_probe_gather(ptr, nbytes, 4, 8, 1 << 16, sink.data_ptr(), stream), "probe")
+
+    def timed(launch, temp, reps):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            if temp == "warm":
+                launch()            # the previous replay warms, and keeps the GPU busy while we enqueue
+            else:
+                flush.add_(1)
+                if temp == "ptewarm":
+                    ptewarm()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            launch()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+        return ts
+
+    res = {"tokens": int(args.tokens), "structs": {s[0]: s[2] / 2**30 for s in structs}}
+    # ---- rank launches
+    pairs = {}
+    for log2, rows in ((19, 65536), (21, 4 * 65536)):
+        tok, lo, hi, ref = bench.rank_pairs(fm, text, bwt, V, 20250905 + 17 + log2, dev, rows=rows)
+        pairs[log2] = (tok, lo, hi, ref)
+    trace = decode_trace(fm, text, bwt, 256, V, 25, 20250905, dev)
+    del text
+    torch.cuda.empty_cache()
+    res["rank"] = []
+    for work in (0, 2, 3):
+        try:
+            old = set_tuning(lf_work=work)
+        except Exception as e:
+            res["rank"].append({"lf_work": work, "error": repr(e)})
+            continue
+        for log2, (tok, lo, hi, ref) in pairs.items():
+            olo, ohi = torch.empty_like(lo), torch.empty_like(hi)
+            try:
+                g = torch.cuda.CUDAGraph()
+                fm.lf_step_batch(tok, lo, hi, SHIFT, lo_out=olo, hi_out=ohi, reset_below=0)   # workspace, outside capture
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g):
+                    fm.lf_step_batch(tok, lo, hi, SHIFT, lo_out=olo, hi_out=ohi, reset_below=0)
+                e = {"lf_work": work, "pairs_log2": log2}
+                for temp in ("cold", "ptewarm", "warm"):
+                    ts = timed(g.replay, temp, args.reps)
+                    e[temp + "_us"] = sorted(ts)
+                    e[temp + "_median_us"] = float(np.median(ts))
+                e["exact"] = bool(torch.equal(olo, ref[0]) and torch.equal(ohi, ref[1]))
+                del g
+            except Exception as ex:
+                e = {"lf_work": work, "pairs_log2": log2, "error": repr(ex)}
+            res["rank"].append(e)
+            print(json.dumps(e), flush=True)
+        set_tuning(old)
+    # ---- the decode step, K = 20 in one graph
+    tokens, init, lo_hist, hi_hist, _ = trace
+    W, K, B = 5, 20, 256
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    lo, hi = init[0].clone(), init[1].clone()
+    for s in range(W):
+        fm.decode_step(tokens[s], lo, hi, mask, V, SHIFT, reset_below=0)
+    st_lo, st_hi = lo.clone(), hi.clone()
+    bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(K):
+            src, dst = bufs[i % 2], bufs[(i + 1) % 2]
+            fm.decode_step(tokens[W + i], src[0], src[1], mask, V, SHIFT, reset_below=0,
+                           lo_out=dst[0], hi_out=dst[1])
+
+    def dec():
+        lo.copy_(st_lo)
+        hi.copy_(st_hi)
+        g.replay()
+
+    e = {"decode_K": K}
+    for temp in ("cold", "ptewarm", "warm"):
+        ts = [t / K for t in timed(dec, temp, args.reps)]   # (the state reset copies are in the window: < 0.1 us/step)
+        e[temp + "_us_per_step"] = sorted(ts)
+        e[temp + "_median_us_per_step"] = float(np.median(ts))
+    fin = bufs[K % 2]
+    e["trace_ok"] = bool(torch.equal(fin[0], lo_hist[W + K - 1]) and torch.equal(fin[1], hi_hist[W + K - 1]))
+    res["decode"] = e
+    print(json.dumps(e), flush=True)
+    # ---- 1M-request gather ceilings
+    fresh = torch.randint(0, 1 << 62, ((8 << 30) // 8,), dtype=torch.int64, device=dev)
+    targets = [("fresh_8GiB", fresh.data_ptr(), fresh.numel() * 8)] + [s for s in structs if s[0] == "E"]
+    res["gather_1M"] = []
+    for name, ptr, nbytes in targets:
+        for mode in (4, 3):
+            gname, lpl, line = bench.GATHER_MODES[mode]
+            thr = (1 << 20) * lpl // 8
+
+            def launch():
+                check(lib().fm_probe_gather(ptr, nbytes, mode, 8, thr, sink.data_ptr(), stream), "probe")
+
+            e = {"target": name, "shape": gname}
+            for temp in ("cold", "ptewarm", "warm"):
+                ts = timed(launch, temp, args.reps)
+                e[temp + "_median_us"] = float(np.median(ts))
+                e[temp + "_G_req_per_s"] = (1 << 20) / (float(np.median(ts)) * 1e-6) / 1e9
+            res["gather_1M"].append(e)
+            print(json.dumps(e), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
