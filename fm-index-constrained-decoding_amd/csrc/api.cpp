@@ -233,6 +233,17 @@ int grow_dscratch(fm_index* h, size_t bytes) {
   return 0;
 }
 
+// Whether `s` is capturing into a graph.  The handle's workspace is not
+// captured: a graph would bake in the pointer of a buffer a later call may
+// free and regrow, and the event hand-off between its uses (ws_acquire /
+// ws_release) crosses the capture boundary.  (A round-5 run of a workspace
+// LF launch inside a captured graph faulted the GPU.)
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
+  return st != hipStreamCaptureStatusNone;
+}
+
 // Workspace of k_distinct (under h->mu): wait for its previous use -- on any
 // stream -- before `s` touches it; growing it waits on the host first.
 int ws_acquire(fm_index* h, hipStream_t s, size_t bytes) {
@@ -1167,7 +1178,8 @@ int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_
   FM_GUARD(h);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t wsb = fmidx::lf_ws_bytes(m);
-  if (!wsb) return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s);
+  // the worklist variant needs the workspace: under capture the launch takes the workspace-free kernels
+  if (!wsb || capturing(s)) return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s);
   std::lock_guard<std::mutex> lk(h->mu);     // the workspace and its event are shared (ws_acquire)
   if (ws_acquire(h, s, wsb)) return -1;
   const int rc = fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s,
@@ -1233,6 +1245,10 @@ int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d
   FM_GUARD(h);
   std::lock_guard<std::mutex> lk(h->mu);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (capturing(s)) {
+    set_error("fm_distinct_count_batch: not capturable (it uses the handle's workspace); launch it eagerly");
+    return -1;
+  }
   if (ws_acquire(h, s, fmidx::distinct_ws_bytes(total_cap))) return -1;
   if (fmidx::launch_distinct(h->idx.view, d_lo, d_hi, m, d_cap_off, d_syms, d_counts, d_k, h->idx.ws, total_cap, s))
     return -1;

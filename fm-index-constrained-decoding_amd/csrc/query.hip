@@ -905,248 +905,12 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_tail(DevView v, const LfWork*
   }
 }
 
-// ------------------------------------------------------------ class-list LF
-// Throughput form of fm_lf_step_batch (lf_work 3): every row's work is done by
-// lanes shaped for it, and no row waits behind another row's chain.
-//   k_lf_class  one lane per row, no wide-row code (few VGPRs: the whole
-//               launch's waves resident at once): reset / dead rows, the full
-//               range (C lookup) and every range of <= kOwnScan rows -- the
-//               lane loads its own E[lo, hi) (a one-row range, 71 % of a
-//               decode trace's rows, is ONE 8-B load: one request) -- are
-//               settled and written; every other row is appended to one of
-//               three class lists (one atomic per class per workgroup):
-//                 P  cached ranges (>= cache_min rows): transition probes,
-//                 S  ranges of kOwnScan+1 .. kSmallScan rows: E scans,
-//                 W  the rest: E scans of <= 512 rows, 2-level descents;
-//   k_lf_lists  persistent waves over the lists: P eight rows per round trip
-//               (probe_issue / probe_finish: 8 lanes per row, LDS-staged
-//               buckets, the range's own cache run alongside; a miss -- a key
-//               the table left out, or an uncached range -- takes the descent
-//               started with the range's bitmap word), S eight rows per round
-//               trip (8 lanes x 8 entries per row), W one row per wave
-//               (lf_step_tail).
-// Lists are split into kWorkRegions regions by appending workgroup, as the
-// worklist sweep's are.  Every row is written exactly once, so in-place
-// launches stay correct.
-constexpr uint64_t kOwnScan = 8;
-constexpr uint64_t kSmallScan = 64;
-constexpr uint32_t kLfClasses = 3;   // P, S, W
-#ifndef FMIDX_LIST_WAVES
-#define FMIDX_LIST_WAVES 4096
-#endif
-constexpr uint64_t kListWaves = FMIDX_LIST_WAVES;   // k_lf_lists' persistent waves (a multiple of 4 x kWorkRegions)
-
-#ifndef FMIDX_CLASS_WGS
-#define FMIDX_CLASS_WGS 0
-#endif
-constexpr uint64_t kClassWgs = FMIDX_CLASS_WGS;   // k_lf_class workgroups (0: one per 256 rows)
-
-__global__ void __launch_bounds__(kLfThreads) k_lf_class(DevView v, const int64_t* __restrict__ tok, int64_t shift,
-                                                        int64_t reset_below, const uint64_t* lo_in,
-                                                        const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
-                                                        uint64_t m, LfWork* __restrict__ lt,
-                                                        uint32_t* __restrict__ cnt, uint64_t cap) {
-  __shared__ uint32_t s_n[2][kLfClasses][kLfThreads / 64];   // by iteration parity
-  __shared__ uint32_t s_base[2][kLfClasses];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
-  // workgroup-strided over 256-row blocks, the next block's row state loaded
-  // while this block's E entries are in flight
-  uint64_t blk = blockIdx.x;
-  uint64_t i = blk * kLfThreads + threadIdx.x;
-  int64_t t = (int64_t)row_load_u64(tok, m, i < m ? i : m - 1);
-  uint64_t l = row_load_u64(lo_in, m, i < m ? i : m - 1);
-  uint64_t h = row_load_u64(hi_in, m, i < m ? i : m - 1);
-  for (uint32_t par = 0; blk * kLfThreads < m; blk += gridDim.x, par ^= 1u) {   // workgroup-uniform
-    // (no early exit: every wave of the workgroup reaches the append's barriers)
-    const uint64_t ni = (blk + gridDim.x) * kLfThreads + threadIdx.x;
-    const uint64_t nii = ni < m ? ni : m - 1;
-    const int64_t tn = (int64_t)row_load_u64(tok, m, nii);
-    const uint64_t ln = row_load_u64(lo_in, m, nii), hn = row_load_u64(hi_in, m, nii);
-    const bool valid = i < m;
-    if (h > v.n) h = v.n;
-    const int64_t sym = t + shift;
-    const bool reset = valid && t < reset_below;
-    const bool live = valid && !reset;
-    const bool dead = live && (l >= h || sym < 0 || (uint64_t)sym > v.max_sym);
-    const bool full = live && !dead && l == 0 && h == v.n;
-    const bool step = live && !dead && !full;
-    const uint64_t w = step ? h - l : 0;
-    const bool own = step && v.E && w <= kOwnScan;
-    const bool probe = step && !own && v.trans_cap && w >= v.cache_min;
-    const bool small = step && !own && !probe && v.E && w <= kSmallScan;
-    const bool wide = step && !own && !probe && !small;
-    const uint64_t c = (uint64_t)sym;
-    const uint64_t cf = full ? c : 0;   // the others all read C[0..1]: one shared line
-    const uint64_t ca = v.C[cf], cb = v.C[cf + 1];
-    // the lane's own E entries: as many loads as the wave's widest own row needs
-    // (wave-uniform; one for a wave of one-row ranges), clamped, unconditional
-    uint32_t wmax = (uint32_t)(own ? w : 0);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, d, 64));
-    uint64_t fmin = ~0ull, fmax = 0;
-#ifdef FMIDX_CLASS_SKIP_E   // measurement variant: every own load reads E[0] (the skeleton's cost)
-    const uint64_t eb = 0, el = 0;
-#else
-    const uint64_t eb = own ? l : 0, el = own ? w - 1 : 0;
-#endif
-    if (wmax <= 1) {
-      const uint64_t x = v.E ? v.E[eb] : 0;
-      if (own && (x >> kESymShift) == c) fmin = fmax = x & kELfMask;
-    } else {
-      uint64_t x[kOwnScan];
-#pragma unroll
-      for (uint32_t k = 0; k < kOwnScan; ++k) x[k] = v.E[eb + (k < el ? k : el)];
-#pragma unroll
-      for (uint32_t k = 0; k < kOwnScan; ++k) {
-        if (own && k <= el && (x[k] >> kESymShift) == c) {
-          const uint64_t f = x[k] & kELfMask;
-          fmin = f < fmin ? f : fmin;
-          fmax = f > fmax ? f : fmax;
-        }
-      }
-    }
-    if (valid && !(probe || small || wide)) {
-      uint64_t nl = 0, nh = 0;
-      if (reset) {
-        nh = v.n;
-      } else if (full) {
-        nl = ca < cb ? ca : 0;
-        nh = ca < cb ? cb : 0;
-      } else if (own && fmin != ~0ull) {
-        nl = fmin;
-        nh = fmax + 1;
-      }
-      lo_out[i] = nl;
-      hi_out[i] = nh;
-    }
-    // ---- the lists: one atomic per class per workgroup and block
-    const uint64_t bp = __ballot(probe), bs = __ballot(small), bw = __ballot(wide);
-    if (lane == 0) {
-      s_n[par][0][wv] = (uint32_t)__popcll(bp);
-      s_n[par][1][wv] = (uint32_t)__popcll(bs);
-      s_n[par][2][wv] = (uint32_t)__popcll(bw);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const uint32_t r = (uint32_t)(blk % kWorkRegions);
-    if (threadIdx.x < kLfClasses) {
-      uint32_t tot = 0;
-      for (uint32_t q = 0; q < kLfThreads / 64; ++q) tot += s_n[par][threadIdx.x][q];
-      s_base[par][threadIdx.x] = tot ? atomicAdd(&cnt[threadIdx.x * kWorkRegions + r], tot) : 0u;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (probe || small || wide) {
-      const uint32_t k = probe ? 0u : (small ? 1u : 2u);
-      const uint64_t bk = probe ? bp : (small ? bs : bw);
-      uint32_t pos = s_base[par][k];
-      for (uint32_t q = 0; q < wv; ++q) pos += s_n[par][k][q];
-      pos += (uint32_t)__popcll(bk & ((1ull << lane) - 1));
-      lt[((uint64_t)k * kWorkRegions + r) * cap + pos] = LfWork{l, h, c, i};
-    }
-    i = ni;
-    t = tn;
-    l = ln;
-    h = hn;
-  }
-}
-
-__global__ void __launch_bounds__(kLfThreads) k_lf_lists(DevView v, const LfWork* __restrict__ lt,
-                                                        const uint32_t* __restrict__ cnt, uint64_t cap,
-                                                        uint64_t* lo_out, uint64_t* hi_out,
-                                                        uint32_t waves_per_region) {
-  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint64_t wave = ((uint64_t)blockIdx.x * kLfThreads + threadIdx.x) >> 6;
-  const uint32_t r = (uint32_t)(wave % kWorkRegions);
-  const uint64_t j0 = wave / kWorkRegions;
-  const uint64_t stride = waves_per_region;
-  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
-  const uint64_t np = cnt[0 * kWorkRegions + r], ns = cnt[1 * kWorkRegions + r], nw = cnt[2 * kWorkRegions + r];
-  const LfWork* P = lt + (uint64_t)(0 * kWorkRegions + r) * cap;
-  const LfWork* S = lt + (uint64_t)(1 * kWorkRegions + r) * cap;
-  const LfWork* Wl = lt + (uint64_t)(2 * kWorkRegions + r) * cap;
-  // every class's first items in one round trip; each loop loads its next
-  // item(s) before stepping the current ones
-  const auto pick = [](const LfWork* L, uint64_t n, uint64_t k) { return L[k < n ? k : 0]; };
-  LfWork xp = pick(P, np, j0 * kProbeRows + seg);
-  LfWork xs = pick(S, ns, j0 * 8 + seg);
-  LfWork xw = pick(Wl, nw, j0);
-  // ---- P: eight cached ranges per round trip
-  for (uint64_t b = j0; b * kProbeRows < np; b += stride) {   // wave-uniform
-    const bool act = b * kProbeRows + seg < np;
-    const LfWork x = xp;
-    xp = pick(P, np, (b + stride) * kProbeRows + seg);
-    const ProbeLoads pld = probe_issue<true>(v, x.l, x.h, x.sym);
-    bool hit;
-    uint64_t clo, chi, pid1;
-    probe_finish<true>(v, x.l, x.h, x.sym, act, pld, s_run[wv], hit, clo, chi, pid1);
-    if (act && hit && sl == 0) {
-      lo_out[x.row] = clo;
-      hi_out[x.row] = chi;
-    }
-    // misses (left-out keys, uncached ranges): the descent, one row at a time
-    uint64_t mb = __ballot(act && !hit && sl == 0);
-    while (mb) {
-      const int src = __ffsll((long long)mb) - 1;
-      mb &= mb - 1;
-      uint64_t ml = __shfl(x.l, src, 64), mh = __shfl(x.h, src, 64);
-      const uint64_t mc = __shfl(x.sym, src, 64), mp = __shfl(pid1, src, 64), mr = __shfl(x.row, src, 64);
-      const uint32_t* pw = mp ? v.cache_bm + (mp - 1) * v.bm_words + ((uint32_t)mc >> 5)
-                              : reinterpret_cast<const uint32_t*>(v.C);
-      const uint32_t pword = mp ? *pw : ~0u;
-      lf_step_tail(v, mc, pword, ml, mh);
-      if (lane == 0) {
-        lo_out[mr] = ml;
-        hi_out[mr] = mh;
-      }
-    }
-  }
-  // ---- S: eight ranges of <= kSmallScan rows per round trip, 8 lanes x 8 entries each
-  for (uint64_t b = j0; b * 8 < ns; b += stride) {   // wave-uniform
-    const bool act = b * 8 + seg < ns;
-    const LfWork x = xs;
-    xs = pick(S, ns, (b + stride) * 8 + seg);
-    const uint64_t last = x.h - 1;
-    uint64_t e[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint64_t idx = x.l + sl + 8 * k;
-      e[k] = v.E[idx < x.h ? idx : last];
-    }
-    uint64_t fmin = ~0ull, fmax = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint64_t idx = x.l + sl + 8 * k;
-      if (idx < x.h && (e[k] >> kESymShift) == x.sym) {
-        const uint64_t f = e[k] & kELfMask;
-        fmin = f < fmin ? f : fmin;
-        fmax = f > fmax ? f : fmax;
-      }
-    }
-#pragma unroll
-    for (int d = 1; d < (int)kProbeLanes; d <<= 1) {
-      const uint64_t a = __shfl_xor(fmin, d, 64), z = __shfl_xor(fmax, d, 64);
-      fmin = a < fmin ? a : fmin;
-      fmax = z > fmax ? z : fmax;
-    }
-    if (act && sl == 0) {
-      lo_out[x.row] = fmin != ~0ull ? fmin : 0;
-      hi_out[x.row] = fmin != ~0ull ? fmax + 1 : 0;
-    }
-  }
-  // ---- W: one row per wave
-  for (uint64_t j = j0; j < nw; j += stride) {   // wave-uniform
-    const LfWork x = xw;
-    xw = pick(Wl, nw, j + stride);
-    uint64_t l = x.l, h = x.h;
-    lf_step_tail(v, x.sym, ~0u, l, h);
-    if (lane == 0) {
-      lo_out[x.row] = l;
-      hi_out[x.row] = h;
-    }
-  }
-}
+// (A class-list form of this launch -- k_lf_class settling the one-row / <= 8-row
+// rows lane by lane and appending the rest to three per-class lists for a
+// persistent k_lf_lists -- was measured in round 5: exact eagerly, no faster
+// (37 + 40 us of kernel time against the grouped kernel's 69-71 at 2^19 pairs,
+// profiles/r05_rank/), and a run of it inside a captured graph faulted the GPU,
+// so it was removed; it is in the history, tuning lf_work 3.)
 
 // [sdsl] backward_search on an inclusive range with unsigned wrap-around.
 __device__ void sdsl_backward_search(const DevView& v, uint64_t c, uint64_t l, uint64_t r,
@@ -1667,7 +1431,6 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
-  bool lists;         // k_lf_class + k_lf_lists (lf_work 3) when a workspace is given
   uint64_t sweep_min; // work_inline from this many rows (lf_work -1: lf_sweep_min; 2: min_rows)
   bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
@@ -1686,7 +1449,6 @@ LfTuning load_lf_tuning() {
   const bool autow = p.lf_work < 0;
   t.work = p.lf_work == 1;
   t.work_inline = autow || p.lf_work == 2;
-  t.lists = p.lf_work == 3;
   t.sweep_min = autow ? p.lf_sweep_min : 0;
   t.search_p8 = p.search_p8 != 0;
   return t;
@@ -1703,7 +1465,6 @@ bool lf_gprobe() { return lf_tuning().gprobe; }
 bool lf_quad() { return lf_tuning().quad; }
 bool lf_split() { return lf_tuning().split; }
 bool lf_work() { return lf_tuning().work; }
-bool lf_lists() { return lf_tuning().lists; }
 
 // worklist geometry for m rows: entries per region, sweep-1 waves
 uint64_t lf_work_cap(uint64_t m) {
@@ -1716,8 +1477,6 @@ uint64_t lf_work_cap(uint64_t m) {
 void reload_lf_tuning() { lf_tuning() = load_lf_tuning(); }
 
 size_t lf_ws_bytes(uint64_t m) {
-  if (m > lf_tuning().min_rows && lf_lists())
-    return kLfClasses * kWorkRegions * (lf_work_cap(m) * sizeof(LfWork) + 4);
   return m > lf_tuning().min_rows && lf_work() ? kWorkRegions * lf_work_cap(m) * sizeof(LfWork) + kWorkRegions * 4 : 0;
 }
 
@@ -1730,19 +1489,6 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
     const unsigned g1 = (unsigned)((m + kLfThreads - 1) / kLfThreads);
     k_lf_sweep<true><<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, nullptr,
                                                nullptr, 0);
-    FM_HIP(hipGetLastError());
-    return 0;
-  }
-  if (ws && m > lf_tuning().min_rows && lf_lists()) {
-    const uint64_t cap = lf_work_cap(m);
-    LfWork* lt = reinterpret_cast<LfWork*>(ws);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(lt + kLfClasses * kWorkRegions * cap);
-    FM_HIP(hipMemsetAsync(cnt, 0, kLfClasses * kWorkRegions * 4, s));
-    const uint64_t nblk = (m + kLfThreads - 1) / kLfThreads;
-    const unsigned g1 = (unsigned)(kClassWgs ? std::min<uint64_t>(nblk, kClassWgs) : nblk);
-    k_lf_class<<<g1, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, lt, cnt, cap);
-    const uint32_t q = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kListWaves / kWorkRegions, cap));
-    k_lf_lists<<<q * kWorkRegions / (kLfThreads / 64), kLfThreads, 0, s>>>(v, lt, cnt, cap, lo_out, hi_out, q);
     FM_HIP(hipGetLastError());
     return 0;
   }

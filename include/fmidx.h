@@ -99,8 +99,8 @@ typedef struct fm_tuning {
   uint32_t reserved;
   uint64_t lf_group_min;    /* grouped LF / get_range kernels above this many rows (8192) */
   int32_t lf_work;          /* -1: the in-wave sweep from lf_sweep_min rows, else the grouped kernel; 0 grouped only;
-                               1 sweep + worklist tail; 2 in-wave sweep whenever grouped; 3 class lists
-                               (k_lf_class + k_lf_lists) */
+                               1 sweep + worklist tail (not inside a captured graph: the grouped kernel
+                               there); 2 in-wave sweep whenever grouped */
   int32_t lf_gprobe;        /* groups of >= 4 lanes probe the transition table themselves (1) */
   int32_t lf_quad;          /* two-lane LF launches settle wide rows four at a time first (1) */
   int32_t lf_split;         /* two-pass LF launch, cheap rows then wide rows (0: measured slower) */
@@ -272,7 +272,7 @@ int fm_decode_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, in
  * CSR slots d_cap_off[i] .. d_cap_off[i+1] (capacity, caller-computed as
  * min(hi-lo, sigma) prefix sums; total_cap = d_cap_off[m] known on the host);
  * the number written per row goes to d_k (UINT64_MAX = capacity overflow).
- * Grows the handle's workspace on first use (not graph-capturable then). */
+ * Uses the handle's shared workspace: refused (-1) on a capturing stream. */
 int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
                             const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
                             uint64_t* d_counts, uint64_t* d_k, void* stream);

@@ -37,7 +37,7 @@ def test_tuning_set_get_and_restore():
         t = get_tuning().as_dict()
         assert (t["lf_group"], t["dec_threads"], t["lf_work"]) == (4, 512, 2)
     assert get_tuning().as_dict() == before
-    for bad in ({"lf_group": 3}, {"dec_threads": 300}, {"lf_work": 5}, {"sa_chunk": 10}):
+    for bad in ({"lf_group": 3}, {"dec_threads": 300}, {"lf_work": 3}, {"sa_chunk": 10}):
         with pytest.raises(FMIndexError):
             set_tuning(**bad)
     assert get_tuning().as_dict() == before

@@ -4,8 +4,8 @@ Builds the bench's C3 index and times, each with the replay enqueued behind
 the work that precedes it (so the events bracket the kernels, not the host's
 graph-launch latency):
   * the LF launch over 2^19 and 2^21 (state, token) pairs of a decode trace,
-    for every LF variant (tuning lf_work 0 grouped, 2 in-wave sweep, 3 class
-    lists), in three temperatures:
+    for the LF variants (tuning lf_work 0 grouped, 2 in-wave sweep) in three
+    temperatures:
       cold     -- after the bench's 1 GiB eviction;
       ptewarm  -- after the eviction, then random 8-B reads spread over every
                   index structure (warms the page-table lines / TLB, but hits
@@ -85,7 +85,7 @@ def main():
     del text
     torch.cuda.empty_cache()
     res["rank"] = []
-    for work in (0, 2, 3):
+    for work in (0, 2):
         try:
             old = set_tuning(lf_work=work)
         except Exception as e:
