@@ -64,7 +64,7 @@ def main():
         if kind in ("rmw", "rmw+read"):
             flush.add_(1)
         if kind in ("read", "rmw+read"):
-            torch.sum(flush, dtype=torch.int64, out=acc)
+            torch.sum(flush, 0, dtype=torch.int64, out=acc)
 
     def timed(replay, kind, per):
         lo.copy_(st_lo)
