@@ -827,7 +827,11 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   tail = tail || (probe && !probed);
   if (INLINE) {
     // the wave's tail rows one at a time by the whole wave (lf_step_tail), then every row is written
+#ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
+    uint64_t tb = 0;
+#else
     uint64_t tb = __ballot(tail);
+#endif
     while (tb) {
       const int src = __ffsll((long long)tb) - 1;
       tb &= tb - 1;

@@ -67,12 +67,14 @@ def main():
             torch.sum(flush, 0, dtype=torch.int64, out=acc)
 
     def timed(replay, kind, per):
-        lo.copy_(st_lo)
-        hi.copy_(st_hi)
         if kind == "warm":
+            lo.copy_(st_lo)
+            hi.copy_(st_hi)
             replay()
         else:
             evict(kind)
+        lo.copy_(st_lo)     # the decode graph always starts from the trace's state
+        hi.copy_(st_hi)
         torch.cuda.synchronize()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)

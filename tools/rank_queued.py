@@ -6,7 +6,8 @@ graph-launch latency):
   * the LF launch over 2^19 and 2^21 (state, token) pairs of a decode trace,
     for the LF variants (tuning lf_work 0 grouped, 2 in-wave sweep) in three
     temperatures:
-      cold     -- after the bench's 1 GiB eviction;
+      cold     -- after the bench's 1 GiB eviction and a 1 GiB read pass (no dirty
+                  lines of the eviction left for the timed kernel to write back);
       ptewarm  -- after the eviction, then random 8-B reads spread over every
                   index structure (warms the page-table lines / TLB, but hits
                   none of the pairs' lines except by chance);
@@ -41,6 +42,8 @@ def main():
     ap.add_argument("--tokens", type=float, default=4.5e9)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="")
+    ap.add_argument("--works", default="0,2", help="LF variants (tuning lf_work) to time")
+    ap.add_argument("--rank-only", action="store_true", help="only the rank launches")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     V = 128256
@@ -48,6 +51,7 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     sink = torch.zeros(1024, dtype=torch.int64, device=dev)
     flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+    acc = torch.zeros((), dtype=torch.int64, device=dev)
     structs = [(STRUCTS[w],) + tuple(fm.device_struct(w)) for w in STRUCTS]
     structs = [s for s in structs if s[1] and s[2] >= (1 << 20)]
 
@@ -63,7 +67,10 @@ def main():
             if temp == "warm":
                 launch()            # the previous replay warms, and keeps the GPU busy while we enqueue
             else:
+                # a clean eviction: the read-modify-write, then a read-only pass that writes its
+                # dirty lines back before the timed kernel (profiles/r05_evict/)
                 flush.add_(1)
+                torch.sum(flush, 0, dtype=torch.int64, out=acc)
                 if temp == "ptewarm":
                     ptewarm()
             a = torch.cuda.Event(enable_timing=True)
@@ -75,17 +82,18 @@ def main():
             ts.append(a.elapsed_time(b) * 1e3)
         return ts
 
-    res = {"tokens": int(args.tokens), "structs": {s[0]: s[2] / 2**30 for s in structs}}
+    res = {"tokens": int(args.tokens), "lib": os.environ.get("FMIDX_LIB", ""),
+           "structs": {s[0]: s[2] / 2**30 for s in structs}}
     # ---- rank launches
     pairs = {}
-    for log2, rows in ((19, 65536), (21, 4 * 65536)):
-        tok, lo, hi, ref = bench.rank_pairs(fm, text, bwt, V, 20250905 + 17 + log2, dev, rows=rows)
+    for log2, rows, seed in ((19, 65536, 20250905 + 17), (21, 4 * 65536, 20250905 + 19)):   # the bench's pairs
+        tok, lo, hi, ref = bench.rank_pairs(fm, text, bwt, V, seed, dev, rows=rows)
         pairs[log2] = (tok, lo, hi, ref)
     trace = decode_trace(fm, text, bwt, 256, V, 25, 20250905, dev)
     del text
     torch.cuda.empty_cache()
     res["rank"] = []
-    for work in (0, 2):
+    for work in (int(x) for x in args.works.split(",") if x.strip()):
         try:
             old = set_tuning(lf_work=work)
         except Exception as e:
@@ -111,6 +119,11 @@ def main():
             res["rank"].append(e)
             print(json.dumps(e), flush=True)
         set_tuning(old)
+    if args.rank_only:
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     # ---- the decode step, K = 20 in one graph
     tokens, init, lo_hist, hi_hist, _ = trace
     W, K, B = 5, 20, 256
