@@ -292,6 +292,7 @@ def gather_ceiling(dev, nbytes=8 << 30):
     # (2^19 pairs make ~1.07M) in ONE launch right after a 1 GiB eviction --
     # what a short cold gather kernel reaches, ramp and drain included
     flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+    flush_acc = torch.zeros((), dtype=torch.int64, device=dev)
     for mode in (4, 3):
         name, lpl, line = GATHER_MODES[mode]
         thr = (1 << 20) * lpl // 8
@@ -301,6 +302,7 @@ def gather_ceiling(dev, nbytes=8 << 30):
             # the events bracket the gather kernel, not the host's launch latency
             torch.cuda.synchronize()
             flush.add_(1)
+            torch.sum(flush, 0, dtype=torch.int64, out=flush_acc)   # the rank legs' clean eviction
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record()
@@ -1166,15 +1168,23 @@ def main():
     # 1 GiB read-modify-write (4x the 256 MB MALL, far beyond L2) right before
     # it evicts whatever earlier replays (or the trace generation) left there.
     flush = torch.zeros(1 << 28, dtype=torch.int32, device=dev)
+    flush_acc = torch.zeros((), dtype=torch.int64, device=dev)
 
-    def evict():
+    def evict(clean=False):
         flush.add_(1)
+        if clean:
+            # then a 1 GiB read-only pass: the read-modify-write's dirty lines are written back
+            # before the timed kernel instead of by its own traffic (profiles/r05_evict/: a 2^19-pair
+            # LF launch 78.8 us after the read-modify-write alone, 71.0 after both)
+            torch.sum(flush, 0, dtype=torch.int64, out=flush_acc)
 
     def timed(graph, reps=1, reset=False, cold=False, queued=False):
         # queued (one-launch graphs, the rank legs): the replay is enqueued behind the
         # eviction while the GPU is still busy with it, so the events bracket the
         # kernel itself and not the host's graph-launch latency (~10 us, which a
-        # 20-step replay spreads over its steps but a one-launch replay would carry whole)
+        # 20-step replay spreads over its steps but a one-launch replay would carry
+        # whole); its eviction is the clean one (evict(clean=True)), since without the
+        # host's gap the kernel would otherwise start while the eviction's dirty lines drain
         ts = []
         for _ in range(reps):
             if reset:
@@ -1183,7 +1193,7 @@ def main():
             if queued:
                 torch.cuda.synchronize()
             if cold:
-                evict()
+                evict(clean=queued)
             if not queued:
                 torch.cuda.synchronize()
             a = torch.cuda.Event(enable_timing=True)
@@ -1324,7 +1334,7 @@ def main():
         r2["rank_GBps"] = r2["alg_bytes_per_launch"] / (r2["avg_launch_us_cold"] * 1e-6) / 1e9
         r2["frac_of_peak"] = r2["rank_GBps"] / HBM_PEAK_GBS
         r2["lf_steps_per_s"] = r2["rows"] / (r2["avg_launch_us_cold"] * 1e-6)
-        r2["kernel"] = "k_lf_sweep<true> (in-wave tail rows), chosen by the library from 2^20 rows"
+        r2["kernel"] = "k_lf_sweep<true> (in-wave tail rows), chosen by the library from 2^19 rows"
         log(f"rank at 2^21 pairs: {r2['avg_launch_us_cold']:.1f}us cold ({r2['avg_launch_us_warm']:.1f} warm), "
             f"{r2['rank_GBps']:.0f} GB/s, {r2['lf_steps_per_s'] / 1e9:.1f} G steps/s, exact {r2['matches_decode_kernel']}")
     gather_gbs, chase_ns, gather_modes = (None, None, None)
@@ -1497,10 +1507,15 @@ def main():
     # the rank figure comes from this bench's own 2^19-pair launch (pmc_req_c3.json, counted over the
     # same command) when that file has it, else from tools/probe_rank.py's launch of the same shape
     have_c3_rank = False
+
+    def rank_2_19(r):
+        # a 2^19-row LF launch (grouped kernel or in-wave sweep): 8.4 MB of new states written
+        # (the 2^21 launch writes 33.5 MB, the by-path launches less)
+        return ("k_lf_group" in r["kernel"] or "k_lf_sweep" in r["kernel"]) and 8e6 <= r.get("write_bytes", 0) < 2e7
+
     try:
         with open(os.path.join(REPO, "profiles", "pmc_req_c3.json")) as f:
-            have_c3_rank = any("k_lf_group" in r["kernel"] and r.get("write_bytes", 0) >= 8e6
-                               for r in json.load(f)["dispatches"])
+            have_c3_rank = any(rank_2_19(r) for r in json.load(f)["dispatches"])
     except (OSError, ValueError, KeyError):
         pass
     for name, where in ((("pmc_req_c3.json" if have_c3_rank else "pmc_req_rank.json"), "rank"),
@@ -1515,7 +1530,7 @@ def main():
                 result[where]["pmc_requests_source"] = f"none: profiles/{name} was counted on lib {t.get('lib_sha16')}"
                 continue
             if where == "rank":      # the 2^19-row launches (the by-path launches write less)
-                rows = [r for r in t["dispatches"] if "k_lf_group" in r["kernel"] and r.get("write_bytes", 0) >= 8e6]
+                rows = [r for r in t["dispatches"] if rank_2_19(r)]
             else:                    # the uint8 decode launches of the C3 bench (B = 256)
                 rows = [r for r in t["dispatches"] if "k_decode<false, true" in r["kernel"]]
             if not rows:

@@ -1422,10 +1422,12 @@ __global__ void __launch_bounds__(256) k_csr_pairs(const uint64_t* __restrict__ 
 //  * lf_work: 0 = the grouped kernel only, 1 / 2 = the worklist sweeps
 //    above (k_lf_sweep + k_lf_tail, or tail rows in-wave); -1 = chosen by
 //    the launch's row count: the in-wave sweep from lf_sweep_min rows
-//    (default 2^20), the grouped kernel below.  Measured on the C3 index, cold
+//    (default 2^19), the grouped kernel below.  Measured on the C3 index, cold
 //    / warm us (profiles/r03_rank/worklist/): 2^19 pairs 71.8 / 60.9 grouped vs
 //    76.6 / 47.7 in-wave; 2^20 126.6 / 109.5 vs 123.0 / 77.6; 2^21 216.4 / 202.4
-//    vs 177.6 / 140.2 -- the in-wave sweep wins cold from 2^20 rows on.
+//    vs 177.6 / 140.2; round 5, after an eviction that leaves no dirty lines
+//    (profiles/r05_rank_temp/): 2^19 72.9 / 63.7 vs 63.1 / 51.5, 2^21 207.3 /
+//    205.3 vs 142.8 / 140.5 -- the in-wave sweep from 2^19 rows.
 struct LfTuning {
   uint32_t G;
   uint32_t Gs;   // get_range

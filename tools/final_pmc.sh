@@ -16,9 +16,9 @@ if [ "$2" = a ]; then
   timeout -k 10 400 bash tools/pmc_traffic.sh "$O/pmc_c3" > "$O/pmc_c3.log" 2>&1
   timeout -k 10 200 bash tools/pmc_rank.sh "$O/pmc_rank" > "$O/pmc_rank.log" 2>&1
 else
-  PASS_TIMEOUT=120 timeout -k 10 700 bash tools/pmc_req.sh "$O/req_c3" "k_decode|k_lf_group" \
+  PASS_TIMEOUT=120 timeout -k 10 700 bash tools/pmc_req.sh "$O/req_c3" "k_decode|k_lf_group|k_lf_sweep" \
       python3 bench.py --no-cpu --no-c4 --no-gather --eager-replay > "$O/req_c3.log" 2>&1
-  PASS_TIMEOUT=90 timeout -k 10 450 bash tools/pmc_req.sh "$O/req_rank" "k_lf_group" \
+  PASS_TIMEOUT=90 timeout -k 10 450 bash tools/pmc_req.sh "$O/req_rank" "k_lf_group|k_lf_sweep" \
       python3 tools/probe_rank.py --rows-log2 19 --patterns 1024 --by-path --out "$O/req_rank/probe.json" \
       > "$O/req_rank.log" 2>&1
 fi
