@@ -255,6 +255,60 @@ __device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32
   return rank_w2_at(L.blocks, L.sb, L.blk_bytes, L.bits, i, d, q);
 }
 
+// The same rank by 16 lanes (q = lane & 15): lane q covers digits [64 q, 64 q
+// + 64) of the block, i.e. twice rank_w2_at's loads per lane, so that a wave
+// ranks four positions at once (two rows' ends: the LF sweep's paired descents).
+__device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
+  const uint64_t b = i >> kW2BlkLog2;
+  const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
+  const uint8_t* base = L.blocks + b * L.blk_bytes;
+  const uint32_t R = 1u << L.bits;
+  const uint64_t sbv = L.sb[(i >> kW2SbLog2) * R + d];
+  const uint32_t hdr = reinterpret_cast<const uint16_t*>(base)[d];
+  const uint32_t first = 64 * q;   // first digit of this lane
+  uint32_t cnt = 0;
+  if (L.bits > 8) {
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 8 * q;
+    uint4 x[8] = {};
+    if (first < k) {   // one guard for all eight loads (see rank_w2_at)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = p[u];
+    }
+    const uint32_t dd = d | (d << 16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t j0 = first + 8 * u;
+      const uint32_t nv = j0 < k ? min(8u, k - j0) : 0u;
+      cnt += eq16_count(x[u].x, dd, nv >= 2 ? 3u : (nv >= 1 ? 1u : 0u));
+      cnt += eq16_count(x[u].y, dd, nv >= 4 ? 3u : (nv >= 3 ? 1u : 0u));
+      cnt += eq16_count(x[u].z, dd, nv >= 6 ? 3u : (nv >= 5 ? 1u : 0u));
+      cnt += eq16_count(x[u].w, dd, nv >= 8 ? 3u : (nv >= 7 ? 1u : 0u));
+    }
+  } else {
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
+    uint4 x[4] = {};
+    if (first < k) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = p[u];
+    }
+    const uint32_t dd = d * 0x01010101u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j0 = first + 16 * u;
+      const uint32_t nv = j0 < k ? min(16u, k - j0) : 0u;
+      cnt += eq8_count(x[u].x, dd, nv >= 4 ? 4u : nv);
+      cnt += eq8_count(x[u].y, dd, nv >= 8 ? 4u : (nv > 4 ? nv - 4 : 0u));
+      cnt += eq8_count(x[u].z, dd, nv >= 12 ? 4u : (nv > 8 ? nv - 8 : 0u));
+      cnt += eq8_count(x[u].w, dd, nv >= 16 ? 4u : (nv > 12 ? nv - 12 : 0u));
+    }
+  }
+  cnt += __shfl_xor(cnt, 1, 64);
+  cnt += __shfl_xor(cnt, 2, 64);
+  cnt += __shfl_xor(cnt, 4, 64);
+  cnt += __shfl_xor(cnt, 8, 64);
+  return sbv + hdr + cnt;
+}
+
 // rank_d(i) of one level by ONE thread (the block's first i mod 1024 digits
 // streamed 16 B at a time): the host API's scalar step and the few keys the
 // transition table left out, never a batched path.

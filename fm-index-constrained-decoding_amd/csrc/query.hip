@@ -687,6 +687,50 @@ __device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint3
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
+// The 2-level descent of TWO ranges at once, one per half-wave (lanes 0-31:
+// row A, 32-63: row B; within a half, 16 lanes rank the lower end and 16 the
+// upper, rank_w2_q16): the LF sweep's tail rows in pairs, so a wave waits one
+// descent's round trips for two rows.  Inputs uniform within each half (lo <
+// hi <= n, not the full range, sym valid); pword as for lf_step_tail -- a
+// symbol the range lacks makes the row empty, and when every active row of the
+// wave lacks its symbol the second level is skipped.  act = false: the half's
+// result is unspecified (its inputs must still be a valid range).
+__device__ __forceinline__ void lf_descend_pair(const DevView& v, bool act, uint64_t c, uint32_t pword, uint64_t& lo,
+                                                uint64_t& hi) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 15u;
+  const bool side = ((lane >> 4) & 1u) != 0;
+  const uint32_t c32 = (uint32_t)c;
+  const int64_t dd = v.D2[c32];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  uint64_t pos = side ? hi : lo;
+  const bool absent = !((pword >> (c32 & 31u)) & 1u);
+#pragma unroll 1
+  for (int l = 0; l < (int)v.NL2; ++l) {
+    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    const uint64_t r = rank_w2_q16(v.w2[l], pos, d, q);
+    pos = z[l] + r;
+    if (l == 0 && __all(absent || !act)) break;   // wave-uniform
+  }
+  const uint64_t other = __shfl_xor(pos, 16, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (absent || l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
+#ifndef FMIDX_SWEEP_PAIR_TAIL
+#define FMIDX_SWEEP_PAIR_TAIL 1   // measurement variant 0: the tail rows one at a time (round 3-5's form)
+#endif
+constexpr int kTailPass = 8;      // 64-entry passes per round trip of the tail rows' packed E scan
+
 // occupancy experiments (make qvariant VFLAGS=-DFMIDX_SWEEP_WPE=6): waves per SIMD forced on the sweep
 #ifndef FMIDX_SWEEP_WPE
 #define FMIDX_SWEEP_WPE 0
@@ -826,6 +870,90 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   }
   tail = tail || (probe && !probed);
   if (INLINE) {
+#if FMIDX_SWEEP_PAIR_TAIL
+    // The wave's tail rows (1.8 per wave on a decode trace: 0.8 E scans of 65..512 rows, 1.0
+    // descents; round 5: 37 % of the sweep's time at 2^19 pairs went to them, stepped one at a
+    // time), then every row is written:
+    //  (1) every E-scan tail of the wave in ONE packed scan (their entries end to end over the
+    //      wave, kTailPass passes per round trip), not one lf_step_fast round trip per row;
+    //  (2) the descents two at a time, one per half-wave (lf_descend_pair).
+    const bool t1 = tail && v.E && h - l <= kENarrow;
+    {
+      const uint32_t cnt1 = t1 ? (uint32_t)(h - l) : 0u;
+      uint32_t inc1 = cnt1;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc1, d, 64);
+        if (lane >= (uint32_t)d) inc1 += y;
+      }
+      const uint32_t excl1 = inc1 - cnt1;
+      const uint32_t total1 = __shfl(inc1, 63, 64);
+      for (uint32_t t0 = 0; t0 < total1; t0 += 64 * kTailPass) {   // wave-uniform
+        uint64_t xs[kTailPass], cs[kTailPass];
+        uint32_t rs[kTailPass];
+#pragma unroll
+        for (int k = 0; k < kTailPass; ++k) {
+          const uint32_t e = t0 + 64u * k + lane;
+          uint32_t r = 0;   // the last row whose offset is <= e (rows of no entries are never it)
+#pragma unroll
+          for (int st = 32; st > 0; st >>= 1) {
+            const uint32_t x = __shfl(excl1, (int)(r + st), 64);
+            if (x <= e) r += st;
+          }
+          const uint64_t base = __shfl(l, (int)r, 64);
+          const uint32_t off = e - __shfl(excl1, (int)r, 64);
+          cs[k] = __shfl(c, (int)r, 64);
+          xs[k] = v.E[e < total1 ? base + off : 0];   // unconditional (a surplus lane reads E[0])
+          rs[k] = e < total1 ? r : ~0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kTailPass; ++k) {
+          if (rs[k] != ~0u && (xs[k] >> kESymShift) == cs[k]) {
+            atomicMin(&s_mm[wv][0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+            atomicMax(&s_mm[wv][1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+          }
+        }
+      }
+      if (total1) {   // wave-uniform; the slots of these rows were untouched by the narrow scan
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t f0 = s_mm[wv][0][lane], f1 = s_mm[wv][1][lane];
+        if (t1) {
+          nl = f0 != ~0ull ? f0 : 0;
+          nh = f0 != ~0ull ? f1 + 1 : 0;
+        }
+      }
+    }
+#ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
+    uint64_t tb = 0;
+#else
+    uint64_t tb = __ballot(tail && !t1);
+#endif
+    while (tb) {   // wave-uniform
+      const int sa = __ffsll((long long)tb) - 1;
+      tb &= tb - 1;
+      const int sb = tb ? __ffsll((long long)tb) - 1 : -1;
+      if (tb) tb &= tb - 1;
+      const int src = lane < 32 ? sa : sb;
+      const bool act = src >= 0;
+      const int s_ = act ? src : sa;   // an idle half repeats row A (valid inputs), its result unused
+      uint64_t tl = __shfl(l, s_, 64), th = __shfl(h, s_, 64);
+      const uint64_t tc = __shfl(c, s_, 64), tp = __shfl(pid1, s_, 64);
+      const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5)
+                              : reinterpret_cast<const uint32_t*>(v.C);
+      const uint32_t pword = tp ? *pw : ~0u;
+      lf_descend_pair(v, act, tc, pword, tl, th);
+      const uint64_t al = __shfl(tl, 0, 64), ah = __shfl(th, 0, 64);
+      const uint64_t bl = __shfl(tl, 32, 64), bh = __shfl(th, 32, 64);
+      if ((int)lane == sa) {
+        nl = al;
+        nh = ah;
+      }
+      if ((int)lane == sb) {
+        nl = bl;
+        nh = bh;
+      }
+    }
+#else
     // the wave's tail rows one at a time by the whole wave (lf_step_tail), then every row is written
 #ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
     uint64_t tb = 0;
@@ -846,6 +974,7 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
         nh = th;
       }
     }
+#endif
     if (valid) {
       lo_out[i] = nl;
       hi_out[i] = nh;
