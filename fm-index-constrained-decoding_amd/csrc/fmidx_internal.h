@@ -255,58 +255,80 @@ __device__ __forceinline__ uint64_t rank_w2(const W2Level& L, uint64_t i, uint32
   return rank_w2_at(L.blocks, L.sb, L.blk_bytes, L.bits, i, d, q);
 }
 
+// the four 8-bit digits of a word equal to d, counting those whose bit is set in m (4 bits)
+__device__ __forceinline__ uint32_t eq8_count_mask(uint32_t x, uint32_t dd, uint32_t m) {
+  const uint32_t y = x ^ dd;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) c += ((m >> j) & 1u) && ((y >> (8 * j)) & 0xFFu) == 0;
+  return c;
+}
+
+// bits [max(lo - j0, 0), min(hi - j0, w)) of a w-digit chunk starting at block position j0
+__device__ __forceinline__ uint32_t chunk_mask(uint32_t j0, uint32_t w, uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo > j0 ? min(lo - j0, w) : 0u;
+  const uint32_t e = hi > j0 ? min(hi - j0, w) : 0u;
+  return a < e ? (((1u << e) - 1u) & ~((1u << a) - 1u)) : 0u;
+}
+
 // The same rank by 16 lanes (q = lane & 15): lane q covers digits [64 q, 64 q
-// + 64) of the block, i.e. twice rank_w2_at's loads per lane, so that a wave
-// ranks four positions at once (two rows' ends: the LF sweep's paired descents).
-__device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, uint32_t d, uint32_t q) {
+// + 64) of the block, twice rank_w2_at's loads per lane, so that a wave ranks
+// four positions at once (two rows' ends: the LF sweep's paired descents).  A
+// position past the block's middle is ranked from the NEXT block's start
+// (rank(i) = rank(start of block b + 1) - the matches in [i, end of block b)),
+// so at most half a block of digits is read per rank (n = BWT length: block b
+// + 1 exists while b < n / 1024).
+__device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, uint32_t d, uint32_t q, uint64_t n) {
   const uint64_t b = i >> kW2BlkLog2;
   const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
+  const bool back = k > (uint32_t)kW2Blk / 2 && b < (n >> kW2BlkLog2);
+  const uint64_t hb = back ? b + 1 : b;   // the block whose start rank is read
   const uint8_t* base = L.blocks + b * L.blk_bytes;
   const uint32_t R = 1u << L.bits;
-  const uint64_t sbv = L.sb[(i >> kW2SbLog2) * R + d];
-  const uint32_t hdr = reinterpret_cast<const uint16_t*>(base)[d];
+  const uint64_t sbv = L.sb[((hb << kW2BlkLog2) >> kW2SbLog2) * R + d];
+  const uint32_t hdr = reinterpret_cast<const uint16_t*>(L.blocks + hb * L.blk_bytes)[d];
   const uint32_t first = 64 * q;   // first digit of this lane
+  const uint32_t lo = back ? k : 0u, hi = back ? (uint32_t)kW2Blk : k;   // the block positions counted
+  const bool need = first < hi && first + 64 > lo;
   uint32_t cnt = 0;
   if (L.bits > 8) {
     const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 8 * q;
     uint4 x[8] = {};
-    if (first < k) {   // one guard for all eight loads (see rank_w2_at)
+    if (need) {   // one guard for all eight loads (see rank_w2_at)
 #pragma unroll
       for (int u = 0; u < 8; ++u) x[u] = p[u];
     }
     const uint32_t dd = d | (d << 16);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const uint32_t j0 = first + 8 * u;
-      const uint32_t nv = j0 < k ? min(8u, k - j0) : 0u;
-      cnt += eq16_count(x[u].x, dd, nv >= 2 ? 3u : (nv >= 1 ? 1u : 0u));
-      cnt += eq16_count(x[u].y, dd, nv >= 4 ? 3u : (nv >= 3 ? 1u : 0u));
-      cnt += eq16_count(x[u].z, dd, nv >= 6 ? 3u : (nv >= 5 ? 1u : 0u));
-      cnt += eq16_count(x[u].w, dd, nv >= 8 ? 3u : (nv >= 7 ? 1u : 0u));
+      const uint32_t m = chunk_mask(first + 8 * u, 8, lo, hi);   // digits of the chunk counted
+      cnt += eq16_count(x[u].x, dd, m & 3u);
+      cnt += eq16_count(x[u].y, dd, (m >> 2) & 3u);
+      cnt += eq16_count(x[u].z, dd, (m >> 4) & 3u);
+      cnt += eq16_count(x[u].w, dd, (m >> 6) & 3u);
     }
   } else {
     const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
     uint4 x[4] = {};
-    if (first < k) {
+    if (need) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) x[u] = p[u];
     }
     const uint32_t dd = d * 0x01010101u;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint32_t j0 = first + 16 * u;
-      const uint32_t nv = j0 < k ? min(16u, k - j0) : 0u;
-      cnt += eq8_count(x[u].x, dd, nv >= 4 ? 4u : nv);
-      cnt += eq8_count(x[u].y, dd, nv >= 8 ? 4u : (nv > 4 ? nv - 4 : 0u));
-      cnt += eq8_count(x[u].z, dd, nv >= 12 ? 4u : (nv > 8 ? nv - 8 : 0u));
-      cnt += eq8_count(x[u].w, dd, nv >= 16 ? 4u : (nv > 12 ? nv - 12 : 0u));
+      const uint32_t m = chunk_mask(first + 16 * u, 16, lo, hi);
+      cnt += eq8_count_mask(x[u].x, dd, m & 15u);
+      cnt += eq8_count_mask(x[u].y, dd, (m >> 4) & 15u);
+      cnt += eq8_count_mask(x[u].z, dd, (m >> 8) & 15u);
+      cnt += eq8_count_mask(x[u].w, dd, (m >> 12) & 15u);
     }
   }
   cnt += __shfl_xor(cnt, 1, 64);
   cnt += __shfl_xor(cnt, 2, 64);
   cnt += __shfl_xor(cnt, 4, 64);
   cnt += __shfl_xor(cnt, 8, 64);
-  return sbv + hdr + cnt;
+  return back ? sbv + hdr - cnt : sbv + hdr + cnt;
 }
 
 // rank_d(i) of one level by ONE thread (the block's first i mod 1024 digits

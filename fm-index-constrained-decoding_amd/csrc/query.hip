@@ -711,7 +711,7 @@ __device__ __forceinline__ void lf_descend_pair(const DevView& v, bool act, uint
 #pragma unroll 1
   for (int l = 0; l < (int)v.NL2; ++l) {
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    const uint64_t r = rank_w2_q16(v.w2[l], pos, d, q);
+    const uint64_t r = rank_w2_q16(v.w2[l], pos, d, q, v.n);
     pos = z[l] + r;
     if (l == 0 && __all(absent || !act)) break;   // wave-uniform
   }
@@ -877,6 +877,13 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
     //  (1) every E-scan tail of the wave in ONE packed scan (their entries end to end over the
     //      wave, kTailPass passes per round trip), not one lf_step_fast round trip per row;
     //  (2) the descents two at a time, one per half-wave (lf_descend_pair).
+    // a probe miss of a range whose bitmap is cached (pid1): the range's word for c, every such row
+    // of the wave at once and in the round trip of (1) -- a symbol the range lacks (nearly every
+    // miss: 0.15 % of the keys are left out of the table) settles the row as empty with no descent
+    const bool pm = tail && pid1 != 0;
+    const uint32_t* pwp = pm ? v.cache_bm + (pid1 - 1) * v.bm_words + ((uint32_t)c >> 5)
+                             : reinterpret_cast<const uint32_t*>(v.C);
+    const uint32_t pword_own = pm ? *pwp : ~0u;
     const bool t1 = tail && v.E && h - l <= kENarrow;
     {
       const uint32_t cnt1 = t1 ? (uint32_t)(h - l) : 0u;
@@ -926,7 +933,8 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
 #ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
     uint64_t tb = 0;
 #else
-    uint64_t tb = __ballot(tail && !t1);
+    const bool absent = pm && !((pword_own >> ((uint32_t)c & 31u)) & 1u);   // nl = nh = 0 already
+    uint64_t tb = __ballot(tail && !t1 && !absent);
 #endif
     while (tb) {   // wave-uniform
       const int sa = __ffsll((long long)tb) - 1;
@@ -937,11 +945,8 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
       const bool act = src >= 0;
       const int s_ = act ? src : sa;   // an idle half repeats row A (valid inputs), its result unused
       uint64_t tl = __shfl(l, s_, 64), th = __shfl(h, s_, 64);
-      const uint64_t tc = __shfl(c, s_, 64), tp = __shfl(pid1, s_, 64);
-      const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5)
-                              : reinterpret_cast<const uint32_t*>(v.C);
-      const uint32_t pword = tp ? *pw : ~0u;
-      lf_descend_pair(v, act, tc, pword, tl, th);
+      const uint64_t tc = __shfl(c, s_, 64);
+      lf_descend_pair(v, act, tc, __shfl(pword_own, s_, 64), tl, th);
       const uint64_t al = __shfl(tl, 0, 64), ah = __shfl(th, 0, 64);
       const uint64_t bl = __shfl(tl, 32, 64), bh = __shfl(th, 32, 64);
       if ((int)lane == sa) {

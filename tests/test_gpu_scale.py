@@ -271,6 +271,14 @@ def test_c3_grouped_lf_and_search(dev, c3):
     ol, oh = torch.empty_like(pl), torch.empty_like(ph)
     fm.lf_step_batch(t, pl, ph, SHIFT, lo_out=ol, hi_out=oh, reset_below=0)
     assert torch.equal(ol, lo_h[1:S].reshape(-1)) and torch.equal(oh, hi_h[1:S].reshape(-1))
+    # the in-wave sweep (the library's choice from 2^19 rows: packed tail E scans, paired
+    # descents with the two-sided block rank) on the same pairs, in place
+    from fmidx.options import tuning
+
+    with tuning(lf_work=2):
+        sl, sh_ = pl.clone(), ph.clone()
+        fm.lf_step_batch(t, sl, sh_, SHIFT, reset_below=0)
+    assert torch.equal(sl, lo_h[1:S].reshape(-1)) and torch.equal(sh_, hi_h[1:S].reshape(-1))
     sel = torch.randint(0, t.numel(), (512,), generator=g, device=dev)
     clo = pl[sel].cpu().numpy().astype(np.uint64)
     chi = ph[sel].cpu().numpy().astype(np.uint64)
