@@ -271,28 +271,35 @@ __device__ __forceinline__ uint32_t chunk_mask(uint32_t j0, uint32_t w, uint32_t
   return a < e ? (((1u << e) - 1u) & ~((1u << a) - 1u)) : 0u;
 }
 
-// The same rank by 16 lanes (q = lane & 15): lane q covers digits [64 q, 64 q
-// + 64) of the block, twice rank_w2_at's loads per lane, so that a wave ranks
-// four positions at once (two rows' ends: the LF sweep's paired descents).  A
-// position past the block's middle is ranked from the NEXT block's start
-// (rank(i) = rank(start of block b + 1) - the matches in [i, end of block b)),
-// so at most half a block of digits is read per rank (n = BWT length: block b
-// + 1 exists while b < n / 1024).
-__device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, uint32_t d, uint32_t q, uint64_t n) {
+// The same rank by 8 lanes (q = lane & 7), reading at most half a block: a
+// position in the block's first half counts the digits before it (rank(i) =
+// rank(block start) + matches in [block start, i)), one in its second half the
+// digits from it to the block's end (rank(i) = rank(next block's start) -
+// matches in [i, block end); for the last block, the level's total of d from
+// Z), so every rank reads <= 512 digits and lane q covers [base + 64 q, + 64)
+// of them -- the LF sweep ranks eight positions at once (four rows' ends).
+// (n = the level's length = the BWT length: block b + 1 exists while b < n / 1024.)
+__device__ __forceinline__ uint64_t rank_w2_q8(const W2Level& L, uint64_t i, uint32_t d, uint32_t q, uint64_t n) {
   const uint64_t b = i >> kW2BlkLog2;
   const uint32_t k = (uint32_t)(i & (kW2Blk - 1));
-  const bool back = k > (uint32_t)kW2Blk / 2 && b < (n >> kW2BlkLog2);
-  const uint64_t hb = back ? b + 1 : b;   // the block whose start rank is read
-  const uint8_t* base = L.blocks + b * L.blk_bytes;
   const uint32_t R = 1u << L.bits;
+  const bool back = k > (uint32_t)kW2Blk / 2;
+  const bool last = b >= (n >> kW2BlkLog2);   // no next block: the level's total of d instead
+  const uint64_t hb = (back && !last) ? b + 1 : b;   // the block whose start rank is read
+  const uint8_t* base = L.blocks + b * L.blk_bytes;
   const uint64_t sbv = L.sb[((hb << kW2BlkLog2) >> kW2SbLog2) * R + d];
   const uint32_t hdr = reinterpret_cast<const uint16_t*>(L.blocks + hb * L.blk_bytes)[d];
-  const uint32_t first = 64 * q;   // first digit of this lane
-  const uint32_t lo = back ? k : 0u, hi = back ? (uint32_t)kW2Blk : k;   // the block positions counted
+  // total of d in the level (Z[d + 1] - Z[d], n - Z[R - 1] for the last digit): only read for a
+  // second-half position of the last block; clamped loads of Z[d], Z[d + 1] otherwise unused
+  const uint64_t z0 = L.Z[d], z1 = L.Z[d + 1 < R ? d + 1 : d];
+  const uint64_t tot = (d + 1 < R ? z1 : n) - z0;
+  const uint32_t blk_end = last ? (uint32_t)(n & (kW2Blk - 1)) : (uint32_t)kW2Blk;
+  const uint32_t lo = back ? k : 0u, hi = back ? blk_end : k;   // the block positions counted
+  const uint32_t first = (back ? (uint32_t)kW2Blk / 2 : 0u) + 64 * q;
   const bool need = first < hi && first + 64 > lo;
   uint32_t cnt = 0;
   if (L.bits > 8) {
-    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 8 * q;
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + first / 8;
     uint4 x[8] = {};
     if (need) {   // one guard for all eight loads (see rank_w2_at)
 #pragma unroll
@@ -308,7 +315,7 @@ __device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, ui
       cnt += eq16_count(x[u].w, dd, (m >> 6) & 3u);
     }
   } else {
-    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + 4 * q;
+    const uint4* p = reinterpret_cast<const uint4*>(base + 2 * R) + first / 16;
     uint4 x[4] = {};
     if (need) {
 #pragma unroll
@@ -327,8 +334,8 @@ __device__ __forceinline__ uint64_t rank_w2_q16(const W2Level& L, uint64_t i, ui
   cnt += __shfl_xor(cnt, 1, 64);
   cnt += __shfl_xor(cnt, 2, 64);
   cnt += __shfl_xor(cnt, 4, 64);
-  cnt += __shfl_xor(cnt, 8, 64);
-  return back ? sbv + hdr - cnt : sbv + hdr + cnt;
+  if (!back) return sbv + hdr + cnt;
+  return (last ? tot : sbv + hdr) - cnt;
 }
 
 // rank_d(i) of one level by ONE thread (the block's first i mod 1024 digits

@@ -687,19 +687,20 @@ __device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint3
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
-// The 2-level descent of TWO ranges at once, one per half-wave (lanes 0-31:
-// row A, 32-63: row B; within a half, 16 lanes rank the lower end and 16 the
-// upper, rank_w2_q16): the LF sweep's tail rows in pairs, so a wave waits one
-// descent's round trips for two rows.  Inputs uniform within each half (lo <
-// hi <= n, not the full range, sym valid); pword as for lf_step_tail -- a
-// symbol the range lacks makes the row empty, and when every active row of the
-// wave lacks its symbol the second level is skipped.  act = false: the half's
-// result is unspecified (its inputs must still be a valid range).
-__device__ __forceinline__ void lf_descend_pair(const DevView& v, bool act, uint64_t c, uint32_t pword, uint64_t& lo,
+// The 2-level descent of FOUR ranges at once, one per quarter-wave (lanes
+// 16 r .. 16 r + 15: row r; within a quarter, 8 lanes rank the lower end and 8
+// the upper, rank_w2_q8 -- at most half a block of digits per rank): the LF
+// sweep's tail rows four at a time, so a wave waits one descent's round trips
+// for four rows.  Inputs uniform within each quarter (lo < hi <= n, not the
+// full range, sym valid); pword as for lf_step_tail -- a symbol the range lacks
+// makes the row empty, and when every active row of the wave lacks its symbol
+// the second level is skipped.  act = false: the quarter's result is
+// unspecified (its inputs must still be a valid range).
+__device__ __forceinline__ void lf_descend_quad(const DevView& v, bool act, uint64_t c, uint32_t pword, uint64_t& lo,
                                                 uint64_t& hi) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t q = lane & 15u;
-  const bool side = ((lane >> 4) & 1u) != 0;
+  const uint32_t q = lane & 7u;
+  const bool side = ((lane >> 3) & 1u) != 0;
   const uint32_t c32 = (uint32_t)c;
   const int64_t dd = v.D2[c32];
   uint64_t z[kW2MaxLevels];
@@ -711,11 +712,11 @@ __device__ __forceinline__ void lf_descend_pair(const DevView& v, bool act, uint
 #pragma unroll 1
   for (int l = 0; l < (int)v.NL2; ++l) {
     const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    const uint64_t r = rank_w2_q16(v.w2[l], pos, d, q, v.n);
+    const uint64_t r = rank_w2_q8(v.w2[l], pos, d, q, v.n);
     pos = z[l] + r;
     if (l == 0 && __all(absent || !act)) break;   // wave-uniform
   }
-  const uint64_t other = __shfl_xor(pos, 16, 64);
+  const uint64_t other = __shfl_xor(pos, 8, 64);
   const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
   if (absent || l2 >= h2) {
     lo = 0;
@@ -876,7 +877,7 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
     // time), then every row is written:
     //  (1) every E-scan tail of the wave in ONE packed scan (their entries end to end over the
     //      wave, kTailPass passes per round trip), not one lf_step_fast round trip per row;
-    //  (2) the descents two at a time, one per half-wave (lf_descend_pair).
+    //  (2) the descents four at a time, one per quarter-wave (lf_descend_quad).
     // a probe miss of a range whose bitmap is cached (pid1): the range's word for c, every such row
     // of the wave at once and in the round trip of (1) -- a symbol the range lacks (nearly every
     // miss: 0.15 % of the keys are left out of the table) settles the row as empty with no descent
@@ -936,26 +937,27 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
     const bool absent = pm && !((pword_own >> ((uint32_t)c & 31u)) & 1u);   // nl = nh = 0 already
     uint64_t tb = __ballot(tail && !t1 && !absent);
 #endif
-    while (tb) {   // wave-uniform
-      const int sa = __ffsll((long long)tb) - 1;
-      tb &= tb - 1;
-      const int sb = tb ? __ffsll((long long)tb) - 1 : -1;
-      if (tb) tb &= tb - 1;
-      const int src = lane < 32 ? sa : sb;
+    while (tb) {   // wave-uniform: up to four rows per round, quarter-wave r takes the r-th
+      int sv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sv[k] = tb ? __ffsll((long long)tb) - 1 : -1;
+        if (tb) tb &= tb - 1;
+      }
+      const uint32_t qw = lane >> 4;
+      const int src = qw == 0 ? sv[0] : (qw == 1 ? sv[1] : (qw == 2 ? sv[2] : sv[3]));
       const bool act = src >= 0;
-      const int s_ = act ? src : sa;   // an idle half repeats row A (valid inputs), its result unused
+      const int s_ = act ? src : sv[0];   // an idle quarter repeats the first row (valid inputs), its result unused
       uint64_t tl = __shfl(l, s_, 64), th = __shfl(h, s_, 64);
       const uint64_t tc = __shfl(c, s_, 64);
-      lf_descend_pair(v, act, tc, __shfl(pword_own, s_, 64), tl, th);
-      const uint64_t al = __shfl(tl, 0, 64), ah = __shfl(th, 0, 64);
-      const uint64_t bl = __shfl(tl, 32, 64), bh = __shfl(th, 32, 64);
-      if ((int)lane == sa) {
-        nl = al;
-        nh = ah;
-      }
-      if ((int)lane == sb) {
-        nl = bl;
-        nh = bh;
+      lf_descend_quad(v, act, tc, __shfl(pword_own, s_, 64), tl, th);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t rl = __shfl(tl, 16 * k, 64), rh = __shfl(th, 16 * k, 64);
+        if (sv[k] >= 0 && (int)lane == sv[k]) {
+          nl = rl;
+          nh = rh;
+        }
       }
     }
 #else

@@ -313,6 +313,68 @@ def test_grouped_lf_and_search_vs_oracle(dev, cache_min, variant):
         assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
 
 
+def test_lf_sweep_descents_vs_oracle(dev):
+    """The in-wave LF sweep's tail rows (lf_work 2: the library's kernel from
+    2^19 rows) on a corpus made for them: 17-bit symbols (a 9-bit first
+    wavelet level, i.e. uint16 digits), frequent tokens whose ranges are
+    wider than the sweep's E scans and narrower than the range cache (the
+    descents, four per wave round), ranges ending at n with n mod 1024 in the
+    block's second half (the half-block rank from the level's total), cached
+    ranges with probe misses (cache_min 64) -- against the oracle."""
+    import torch
+
+    from fmidx.options import tuning
+
+    rng = np.random.default_rng(41)
+
+    def doc():
+        ln = int(rng.integers(40, 160))
+        common = rng.integers(0, 24, ln)
+        rare = rng.integers(60000, 120000, ln)
+        return [int(x) for x in np.where(rng.random(ln) < 0.9, common, rare)]
+
+    docs = [doc() for _ in range(260)]
+    while True:   # n mod 1024 in the second half of the last rank block
+        n_est = sum(len(d) for d in docs) + 1   # T' + the sentinel
+        if 600 <= n_est % 1024 <= 1000:
+            break
+        docs.append(doc())
+    for cache_min in (None, 64):
+        ours = ours_index(docs, cache_min=cache_min)
+        ora = OracleIndex()
+        ora.initialize(docs, in_memory=True)
+        n = ours.size()
+        assert n == ora.size() and 600 <= n % 1024 <= 1000, n
+        F = [t for d in reversed(docs) for t in d]
+        m = 24001
+        pats, nxt = [], []
+        for i in range(m):
+            ln = int(rng.integers(0, 3))
+            s = int(rng.integers(0, len(F) - ln))
+            pats.append(list(F[s:s + ln]))
+            nxt.append(F[int(rng.integers(0, len(F)))] if rng.random() < 0.85 else int(rng.integers(0, 120000)))
+        want = [ora.get_range(p) if p else (0, n) for p in pats]
+        li = [w[0] for w in want]
+        hv = [w[1] for w in want]
+        hv[::7] = [n] * len(hv[::7])            # ranges ending at n: the last block's upper end
+        li[::7] = [max(0, n - int(rng.integers(513, 4000))) for _ in range(len(li[::7]))]
+        want_lf = []
+        for i in range(m):
+            a_, b_ = li[i], min(hv[i], n)
+            want_lf.append((0, 0) if a_ >= b_ else ora.backward_search_step(int(nxt[i]) + 10, a_, b_ - 1))
+        widths = np.array(hv) - np.array(li)
+        assert ((widths > 512) & (widths < 4096)).sum() > 2000
+        with tuning(lf_work=2):
+            lo_in = torch.tensor(li, dtype=torch.int64, device=dev)
+            hi_in = torch.tensor(hv, dtype=torch.int64, device=dev)
+            lo_out, hi_out = torch.empty_like(lo_in), torch.empty_like(hi_in)
+            ours.lf_step_batch(torch.tensor(nxt, dtype=torch.int64, device=dev), lo_in, hi_in, 10, lo_out=lo_out,
+                               hi_out=hi_out, reset_below=-(1 << 62))
+        got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
+        bad = [i for i in range(m) if got[i] != want_lf[i]]
+        assert not bad, [(i, int(nxt[i]), li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]]
+
+
 def test_workspace_launches_under_graph_capture(dev):
     """The handle's workspace is never captured into a graph: an LF launch
     whose variant needs it (lf_work 1, the worklist sweep) takes the
