@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--works", default="0,2", help="LF variants (tuning lf_work) to time")
     ap.add_argument("--rank-only", action="store_true", help="only the rank launches")
+    ap.add_argument("--sizes", default="19,21", help="log2 of the pairs per launch (2^19 / 2^21: the bench's pairs)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     V = 128256
@@ -86,8 +87,10 @@ def main():
            "structs": {s[0]: s[2] / 2**30 for s in structs}}
     # ---- rank launches
     pairs = {}
-    for log2, rows, seed in ((19, 65536, 20250905 + 17), (21, 4 * 65536, 20250905 + 19)):   # the bench's pairs
-        tok, lo, hi, ref = bench.rank_pairs(fm, text, bwt, V, seed, dev, rows=rows)
+    for log2 in (int(x) for x in args.sizes.split(",") if x.strip()):
+        # rows x 8 pairs; 2^19 and 2^21 are the bench's own pairs (seeds), the other sizes their own traces
+        seed = {19: 20250905 + 17, 21: 20250905 + 19}.get(log2, 20250905 + 100 + log2)
+        tok, lo, hi, ref = bench.rank_pairs(fm, text, bwt, V, seed, dev, rows=(1 << log2) // 8)
         pairs[log2] = (tok, lo, hi, ref)
     trace = decode_trace(fm, text, bwt, 256, V, 25, 20250905, dev)
     del text
