@@ -1338,7 +1338,7 @@ def main():
         r2["rank_GBps"] = r2["alg_bytes_per_launch"] / (r2["avg_launch_us_cold"] * 1e-6) / 1e9
         r2["frac_of_peak"] = r2["rank_GBps"] / HBM_PEAK_GBS
         r2["lf_steps_per_s"] = r2["rows"] / (r2["avg_launch_us_cold"] * 1e-6)
-        r2["kernel"] = "k_lf_sweep<true> (in-wave tail rows), chosen by the library from 2^19 rows"
+        r2["kernel"] = "k_lf_sweep<true> (in-wave tail rows), chosen by the library from 2^18 rows"
         log(f"rank at 2^21 pairs: {r2['avg_launch_us_cold']:.1f}us cold ({r2['avg_launch_us_warm']:.1f} warm), "
             f"{r2['rank_GBps']:.0f} GB/s, {r2['lf_steps_per_s'] / 1e9:.1f} G steps/s, exact {r2['matches_decode_kernel']}")
     gather_gbs, chase_ns, gather_modes = (None, None, None)
@@ -1435,7 +1435,7 @@ def main():
                                   "M_lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6) / 1e6,
                                   "matches_decode_kernel": rs_ok,
                                   "note": "2^19 independent (state, token) pairs of a 65536-row trace in one k_lf launch "
-                                          "(the in-wave sweep k_lf_sweep<true>, which the library picks from 2^19 rows: one lane per row, narrow rows packed, cached rows probed eight per round trip, tail rows in-wave), cold after a clean eviction, timed queued"},
+                                          "(the in-wave sweep k_lf_sweep<true>, which the library picks from 2^18 rows: one lane per row, narrow rows packed, cached rows probed eight per round trip, tail rows in-wave), cold after a clean eviction, timed queued"},
                      "bytes_model": "64-B lines the LF plan reads per live row (bench.lf_plan_bytes)"},
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},

@@ -717,7 +717,7 @@ struct Tuning {
   int32_t lf_quad = 1;
   int32_t lf_split = 0;
   int32_t search_p8 = 1;
-  uint64_t lf_sweep_min = 1ull << 19;
+  uint64_t lf_sweep_min = 1ull << 18;
   uint64_t sa_chunk = 1ull << 29;
 };
 const Tuning& tuning();

@@ -1558,12 +1558,15 @@ __global__ void __launch_bounds__(256) k_csr_pairs(const uint64_t* __restrict__ 
 //  * lf_work: 0 = the grouped kernel only, 1 / 2 = the worklist sweeps
 //    above (k_lf_sweep + k_lf_tail, or tail rows in-wave); -1 = chosen by
 //    the launch's row count: the in-wave sweep from lf_sweep_min rows
-//    (default 2^19), the grouped kernel below.  Measured on the C3 index, cold
+//    (default 2^18), the grouped kernel below.  Measured on the C3 index, cold
 //    / warm us (profiles/r03_rank/worklist/): 2^19 pairs 71.8 / 60.9 grouped vs
 //    76.6 / 47.7 in-wave; 2^20 126.6 / 109.5 vs 123.0 / 77.6; 2^21 216.4 / 202.4
 //    vs 177.6 / 140.2; round 5, after an eviction that leaves no dirty lines
 //    (profiles/r05_rank_temp/): 2^19 72.9 / 63.7 vs 63.1 / 51.5, 2^21 207.3 /
-//    205.3 vs 142.8 / 140.5 -- the in-wave sweep from 2^19 rows.
+//    205.3 vs 142.8 / 140.5; with its tail rows rewritten (packed E scans,
+//    settled misses, quarter-wave descents; profiles/r05_tails/rank_by_launch_size.json)
+//    2^17 36.0 / 31.0 vs 44.7 / 30.3, 2^18 57.9 / 44.0 vs 50.2 / 36.9, 2^19 73.0 /
+//    63.1 vs 57.6 / 48.4, 2^20 116.8 / 112.1 vs 79.8 / 72.0 -- the sweep from 2^18 rows.
 struct LfTuning {
   uint32_t G;
   uint32_t Gs;   // get_range

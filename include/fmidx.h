@@ -106,7 +106,7 @@ typedef struct fm_tuning {
   int32_t lf_split;         /* two-pass LF launch, cheap rows then wide rows (0: measured slower) */
   int32_t search_p8;        /* get_range probes cached wide rows eight per round trip (1) */
   int32_t reserved2;
-  uint64_t lf_sweep_min;    /* see lf_work (2^19) */
+  uint64_t lf_sweep_min;    /* see lf_work (2^18) */
   uint64_t sa_chunk;        /* suffix sorter: rows per sort chunk (2^29) */
 } fm_tuning;
 int fm_tuning_init(fm_tuning* t);
