@@ -320,7 +320,8 @@ def test_lf_sweep_descents_vs_oracle(dev):
     wider than the sweep's E scans and narrower than the range cache (the
     descents, four per wave round), ranges ending at n with n mod 1024 in the
     block's second half (the half-block rank from the level's total), cached
-    ranges with probe misses (cache_min 64) -- against the oracle."""
+    ranges with probe misses (cache_min 64), and an index without the E array
+    (every row a probe or a descent) -- against the oracle."""
     import torch
 
     from fmidx.options import tuning
@@ -339,8 +340,8 @@ def test_lf_sweep_descents_vs_oracle(dev):
         if 600 <= n_est % 1024 <= 1000:
             break
         docs.append(doc())
-    for cache_min in (None, 64):
-        ours = ours_index(docs, cache_min=cache_min)
+    for cache_min, opts in ((None, {}), (64, {}), (None, {"lf_e": 0})):   # lf_e 0: no E array, every tail a descent
+        ours = ours_index(docs, cache_min=cache_min, **opts)
         ora = OracleIndex()
         ora.initialize(docs, in_memory=True)
         n = ours.size()
