@@ -64,10 +64,6 @@ constexpr uint64_t kEarlyZeroWidth = FMIDX_EARLY_ZERO_WIDTH;   // rows this narr
 #define FMIDX_EZ_SLEEP 0   // measurement variant: s_sleep (x 64 clocks) between a thread's early zero stores
 #endif
 constexpr int kEzSleep = FMIDX_EZ_SLEEP;
-#ifndef FMIDX_SPEC_ZERO
-#define FMIDX_SPEC_ZERO 1   // measurement variant 0: a cached range's probe miss is not zero-filled early
-#endif
-constexpr bool kSpecZero = FMIDX_SPEC_ZERO != 0;
 constexpr int kUnroll = 4;                    // uint4 loads in flight per thread while streaming
 constexpr uint32_t kPayMagic = 0x58534D46u;    // the shard payload's magic (csrc/shard.hip)
 constexpr uint32_t kPayMaxWords = 8192;        // W of a payload row: vocab <= 262144
@@ -403,7 +399,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   __shared__ Plan plan;
   __shared__ uint64_t s_lohi[3];              // new range + its only symbol when the transition table knew it (else ~0)
   __shared__ unsigned long long s_scan[2];    // workgroup E scan: first / last occurrence
-  __shared__ uint32_t s_spec;                 // a cached range's transition probe: 1 hit, 2 miss
   FM_STAMP_DECL;
   // sized at launch to the slice (16 KB at a 128k vocabulary instead of the
   // 32 KB maximum): LDS is what bounds the workgroups resident per CU at
@@ -472,8 +467,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // Zero-fill by waves 1.. only: loads and stores share vmcnt in issue order,
   // so a wave with stores in flight cannot wait on a load without also
   // waiting for them -- wave 0 (LF + plan) must stay store-free.
-  // the slice's zeros by threads kEzFirst.. (chunk k by thread kEzFirst + k mod (kDecThreads - kEzFirst))
-  auto zero_fill = [&]() {
+  if (early_zero && threadIdx.x >= kEzFirst) {
     for (uint64_t k = threadIdx.x - kEzFirst; k < nch; k += kDecThreads - kEzFirst) {
       if (kEzSleep && k >= kDecThreads - kEzFirst) __builtin_amdgcn_s_sleep(kEzSleep);
       const uint64_t t = t0 + k * CH;
@@ -485,8 +479,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         for (uint64_t j = t; j < min(t1, t + CH); ++j) out_row[j] = 0;
       }
     }
-  };
-  if (early_zero && threadIdx.x >= kEzFirst) zero_fill();
+  }
   if (wg_scan) {
     const uint64_t c = (uint64_t)(st_tok + shift);
     constexpr int kU = (kScanMax + kDecThreads - 1) / kDecThreads;
@@ -522,31 +515,6 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     }
     lds_barrier();
   }
-  // A cached incoming range (workgroup-uniform): wave 0 probes the transition
-  // table alone first, and on a miss -- nearly always a symbol the range lacks,
-  // i.e. an empty row (0.15 % of the keys are left out of the table) -- the
-  // other waves zero-fill the row right away, while wave 0 confirms it (the
-  // range's bitmap word for c, or the descent for a left-out key).  Those rows
-  // used to write their 128 KB of zeros only after that second round trip, and
-  // were often the step's last to finish (profiles/r05_final/stamps/).
-  const int64_t sym_in = st_tok + shift;
-  const bool spec = kSpecZero && DO_LF && !PAY && !reset && !early_zero && !wg_scan && v.trans_cap &&
-                    v.probe_first && in_lo < in_hi && in_hi - in_lo >= v.cache_min &&
-                    !(in_lo == 0 && in_hi == v.n) && sym_in >= 0 && (uint64_t)sym_in <= v.max_sym;
-  bool spec_zero = false;
-  bool sp_hit = false;
-  uint64_t sp_lo = 0, sp_hi = 0, sp_pid = 0;
-  const uint32_t* sp_tbm = nullptr;
-  int64_t sp_one = -1;
-  if (spec) {   // workgroup-uniform
-    if (threadIdx.x < 64) {
-      lf_probe_cached(v, (uint64_t)sym_in, in_lo, in_hi, sp_hit, sp_lo, sp_hi, sp_tbm, sp_one, sp_pid);
-      if (threadIdx.x == 0) s_spec = sp_hit ? 1u : 2u;
-    }
-    lds_barrier();
-    spec_zero = s_spec == 2u;
-    if (spec_zero && threadIdx.x >= kEzFirst) zero_fill();
-  }
   // Wave 0: the LF step (all 64 lanes), then the bitmap plan of the new range
   // (all 64 lanes), published with the range by a single barrier.  A range
   // whose LF step was an E scan gets its content with the scan (E2): wave 0
@@ -568,18 +536,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         // from the full range the LF step lands on symbol c's C-block, whose
         // allowed set is c's precomputed follow-set bitmap
         if (l == 0 && h >= v.n) follow = t + shift;
-        if (spec && sp_hit) {
-          l = sp_lo;
-          h = sp_hi;
-          tbm = sp_tbm;
-          one = sp_one;
-        } else if (spec) {   // the probe missed: the range's word for c, then (left-out key) the descent
-          const uint32_t pword =
-              sp_pid ? v.cache_bm[(sp_pid - 1) * v.bm_words + ((uint32_t)sym_in >> 5)] : ~0u;
-          l = in_lo;
-          h = in_hi;
-          lf_step_tail(v, (uint64_t)sym_in, pword, l, h);
-        } else if (wg_scan) {
+        if (wg_scan) {
           const uint64_t a = s_scan[0], b = s_scan[1];
           l = b ? (a & kELfMask) : 0;
           h = b ? (b & kELfMask) + 1 : 0;
@@ -675,9 +632,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   //               waves 4.. zero-fill now, overlapping the stream round trip
   //   otherwise   every wave gathers (bitmaps + partial ends), every wave emits
   // The zero-filling waves own their chunks in the final emit (program order).
-  const bool late_zero = kDecThreads >= 512 && !early_zero && !spec_zero && lo < hi && plan.nb == 0;
-  const uint32_t e_first =
-      (early_zero || spec_zero) ? (uint32_t)kEzFirst : (late_zero ? 256u : 0u);   // emit/zero owners: tid >= e_first
+  const bool late_zero = kDecThreads >= 512 && !early_zero && lo < hi && plan.nb == 0;
+  const uint32_t e_first = early_zero ? (uint32_t)kEzFirst : (late_zero ? 256u : 0u);   // emit/zero owners: tid >= e_first
   if (late_zero && threadIdx.x >= e_first) {
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
       const uint64_t t = t0 + k * CH;
@@ -722,7 +678,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     const uint32_t nb = plan.nb;
     if (nb == 0) {
       // streamed only
-      const uint32_t nthr = (early_zero || spec_zero) ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
+      const uint32_t nthr = early_zero ? 64u : (late_zero ? 256u : (uint32_t)kDecThreads);
       if (threadIdx.x < nthr) {
         if (v.bwt)
           stream_symbols(v.bwt, plan.a0, plan.b0, plan.a1, plan.b1, base_bit, lim, win, nthr);
@@ -802,7 +758,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   // A zeroed chunk's final store follows its zero store from the same thread
   // to the same address, in program order: per-location coherence orders the
   // two, no wait for the zero stores' acknowledgements is needed.
-  const bool zeroed = early_zero || late_zero || spec_zero;
+  const bool zeroed = early_zero || late_zero;
   const int64_t rel0 = (int64_t)t0 + shift - w_lo * 32;   // >= 0
   if (direct) {
     // bits of chunk k = bitmap bits [t0 + CH k + shift, + CH).  All of a

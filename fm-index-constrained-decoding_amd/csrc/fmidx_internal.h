@@ -669,93 +669,6 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
-// The 2-level descent / wide E scan, by a whole wave (uniform inputs;
-// lo < hi <= n, not the full range, sym valid).  pword = the range's cached
-// bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
-// step after the descent's first level.
-__device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint32_t pword, uint64_t& lo,
-                                             uint64_t& hi) {
-  if (v.E && hi - lo <= kENarrow) {
-    uint32_t cm = 0;
-    lf_step_fast<false>(v, (int64_t)c, lo, hi, nullptr, cm);
-    return;
-  }
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t q = lane & 31u;
-  const bool side = lane >= 32;
-  const uint32_t c32 = (uint32_t)c;
-  const int64_t dd = v.D2[c32];
-  uint64_t z[kW2MaxLevels];
-#pragma unroll
-  for (int l = 0; l < kW2MaxLevels; ++l)
-    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
-  uint64_t pos = side ? hi : lo;
-#pragma unroll 1
-  for (int l = 0; l < (int)v.NL2; ++l) {
-    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
-    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
-    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {
-      lo = 0;
-      hi = 0;
-      return;
-    }
-    pos = z[l] + r;
-  }
-  const uint64_t other = __shfl_xor(pos, 32, 64);
-  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
-  if (l2 >= h2) {
-    lo = 0;
-    hi = 0;
-    return;
-  }
-  lo = (uint64_t)((int64_t)l2 + dd);
-  hi = (uint64_t)((int64_t)h2 + dd);
-}
-
-// The transition probe of a cached range ALONE (lf_step_decode's probe-first
-// round trip, by all 64 lanes of a wave; uniform inputs: lo < hi <= n, not the
-// full range, hi - lo >= cache_min, sym valid): a hit gives the child range and
-// its bitmap (cbm) or only symbol (one); a miss gives the range's own cache id +
-// 1 (pid1, from lanes 48-63's read of its range-cache run; 0: not found), whose
-// bitmap word for c then tells an absent symbol from a key the table left out.
-__device__ __forceinline__ void lf_probe_cached(const DevView& v, uint64_t c, uint64_t lo, uint64_t hi, bool& hit,
-                                                uint64_t& clo, uint64_t& chi, const uint32_t*& cbm, int64_t& one,
-                                                uint64_t& pid1) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t key0 = lo | (c << kTransSymShift);
-  uint64_t tw = kTransEmpty;
-  if (lane < 3 * kTransProbe) {
-    const uint64_t slot = trans_slot(trans_home(lo, hi, c, v.trans_cap), lane / 3);
-    tw = v.trans_tab[3 * slot + lane % 3];
-  } else if (v.cache_mask) {
-    const uint32_t k = lane - 3 * kTransProbe;
-    tw = v.cache_tab[2 * ((cache_hash(lo, hi) + k / 2) & v.cache_mask) + (k & 1)];
-  }
-  const uint64_t w1n = __shfl_down(tw, 1, 64);
-  const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
-  cbm = nullptr;
-  one = -1;
-  pid1 = 0;
-  hit = bh != 0;
-  clo = 0;
-  chi = 0;
-  if (bh) {   // wave-uniform
-    const int src = __ffsll((long long)bh) - 1;
-    const uint64_t w1 = __shfl(tw, src + 1, 64), w2 = __shfl(tw, src + 2, 64);
-    clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
-    chi = clo + ((w2 >> 4) & kMask34);
-    const uint64_t aux = w2 >> 38;
-    if (aux & kTransOne)
-      one = (int64_t)(aux & (kTransOne - 1));
-    else if (aux)
-      cbm = v.cache_bm + (aux - 1) * v.bm_words;
-    return;
-  }
-  const uint64_t bc = __ballot(lane >= 3 * kTransProbe && ((lane - 3 * kTransProbe) & 1u) == 0 && tw == lo &&
-                               (w1n & kMask34) == hi);
-  if (bc) pid1 = (__shfl(w1n, __ffsll((long long)bc) - 1, 64) >> kCacheIdShift) + 1;
-}
-
 // ---------------------------------------------------------------------------
 // suffix-array / inverse-suffix-array samples (locate.hip): text-order
 // sampling at sdsl csa_wt's default rates

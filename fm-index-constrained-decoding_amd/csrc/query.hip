@@ -644,6 +644,49 @@ constexpr uint64_t kSweepScan = 64;   // widest range k_lf_sweep scans in E
 #define FMIDX_SWEEP_PASS 2
 #endif
 constexpr int kSweepPass = FMIDX_SWEEP_PASS;   // 64-entry passes per round trip of the packed scan (2: 92 VGPRs; 4: 100)
+// The 2-level descent / wide E scan, by a whole wave (uniform inputs;
+// lo < hi <= n, not the full range, sym valid).  pword = the range's cached
+// bitmap word holding bit c (~0 when unknown): a symbol the range lacks ends the
+// step after the descent's first level.
+__device__ __forceinline__ void lf_step_tail(const DevView& v, uint64_t c, uint32_t pword, uint64_t& lo,
+                                             uint64_t& hi) {
+  if (v.E && hi - lo <= kENarrow) {
+    uint32_t cm = 0;
+    lf_step_fast<false>(v, (int64_t)c, lo, hi, nullptr, cm);
+    return;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t q = lane & 31u;
+  const bool side = lane >= 32;
+  const uint32_t c32 = (uint32_t)c;
+  const int64_t dd = v.D2[c32];
+  uint64_t z[kW2MaxLevels];
+#pragma unroll
+  for (int l = 0; l < kW2MaxLevels; ++l)
+    z[l] = (l < (int)v.NL2) ? v.w2[l].Z[(c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u)] : 0;
+  uint64_t pos = side ? hi : lo;
+#pragma unroll 1
+  for (int l = 0; l < (int)v.NL2; ++l) {
+    const uint32_t d = (c32 >> v.w2[l].shift) & ((1u << v.w2[l].bits) - 1u);
+    const uint64_t r = rank_w2(v.w2[l], pos, d, q);
+    if (l == 0 && !((pword >> (c32 & 31u)) & 1u)) {
+      lo = 0;
+      hi = 0;
+      return;
+    }
+    pos = z[l] + r;
+  }
+  const uint64_t other = __shfl_xor(pos, 32, 64);
+  const uint64_t l2 = side ? other : pos, h2 = side ? pos : other;
+  if (l2 >= h2) {
+    lo = 0;
+    hi = 0;
+    return;
+  }
+  lo = (uint64_t)((int64_t)l2 + dd);
+  hi = (uint64_t)((int64_t)h2 + dd);
+}
+
 // The 2-level descent of FOUR ranges at once, one per quarter-wave (lanes
 // 16 r .. 16 r + 15: row r; within a quarter, 8 lanes rank the lower end and 8
 // the upper, rank_w2_q8 -- at most half a block of digits per rank): the LF
