@@ -727,8 +727,8 @@ __device__ __forceinline__ void lf_descend_quad(const DevView& v, bool act, uint
   hi = (uint64_t)((int64_t)h2 + dd);
 }
 
-#ifndef FMIDX_SWEEP_PAIR_TAIL
-#define FMIDX_SWEEP_PAIR_TAIL 1   // measurement variant 0: the tail rows one at a time (round 3-5's form)
+#ifndef FMIDX_SWEEP_TAIL_BATCH
+#define FMIDX_SWEEP_TAIL_BATCH 1   // measurement variant 0: the tail rows one at a time (round 3-5's form)
 #endif
 constexpr int kTailPass = 8;      // 64-entry passes per round trip of the tail rows' packed E scan
 
@@ -871,7 +871,7 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   }
   tail = tail || (probe && !probed);
   if (INLINE) {
-#if FMIDX_SWEEP_PAIR_TAIL
+#if FMIDX_SWEEP_TAIL_BATCH
     // The wave's tail rows (1.8 per wave on a decode trace: 0.8 E scans of 65..512 rows, 1.0
     // descents; round 5: 37 % of the sweep's time at 2^19 pairs went to them, stepped one at a
     // time), then every row is written:
