@@ -1179,15 +1179,19 @@ def main():
             torch.sum(flush, 0, dtype=torch.int64, out=flush_acc)
 
     def timed(graph, reps=1, reset=False, cold=False, queued=False):
-        # queued (one-launch graphs, the rank legs): the replay is enqueued behind the
-        # eviction while the GPU is still busy with it, so the events bracket the
-        # kernel itself and not the host's graph-launch latency (~10 us, which a
-        # 20-step replay spreads over its steps but a one-launch replay would carry
-        # whole); its eviction is the clean one (evict(clean=True)), since without the
-        # host's gap the kernel would otherwise start while the eviction's dirty lines drain
+        # queued (the one-launch rank legs; `graph` is then a callable that launches the
+        # kernel directly): the launch is enqueued behind the eviction while the GPU is
+        # still busy with it, so the events bracket the kernel itself and not the host's
+        # launch latency; a DIRECT launch, not a one-node graph replay, whose own GPU-side
+        # cost (~13 us per replay, rocprof kernel trace against the events,
+        # profiles/r05_graph_launch/) a 20-step replay spreads over its steps but a
+        # one-launch replay would carry whole -- the 1M-request gather ceiling is timed
+        # the same way; its eviction is the clean one (evict(clean=True)), since without
+        # the host's gap the kernel would otherwise start while the eviction's dirty lines drain
+        run = graph.replay if hasattr(graph, "replay") else graph
         ts = []
-        if queued:   # one untimed replay: the kernel's first launch in the process loads its code
-            graph.replay()
+        if queued:   # one untimed launch: the kernel's first launch in the process loads its code
+            run()
             torch.cuda.synchronize()
         for _ in range(reps):
             if reset:
@@ -1197,12 +1201,14 @@ def main():
                 torch.cuda.synchronize()
             if cold:
                 evict(clean=queued)
+            elif queued:
+                run()   # warm and queued: the previous launch keeps the GPU busy while this one is enqueued
             if not queued:
                 torch.cuda.synchronize()
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             a.record()
-            graph.replay()
+            run()
             b.record()
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
@@ -1219,29 +1225,25 @@ def main():
     all_lo = lo_hist[W - 1:S - 1].reshape(-1).contiguous()
     all_hi = hi_hist[W - 1:S - 1].reshape(-1).contiguous()
     big_lo, big_hi = torch.empty_like(all_lo), torch.empty_like(all_hi)
-    g_lfbig = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g_lfbig):
-        fm.lf_step_batch(all_tok, all_lo, all_hi, SHIFT, lo_out=big_lo, hi_out=big_hi, reset_below=0)
-    lfbig_cold = timed(g_lfbig, 5, cold=True, queued=True)
+    lfbig_cold = timed(lambda: fm.lf_step_batch(all_tok, all_lo, all_hi, SHIFT, lo_out=big_lo, hi_out=big_hi,
+                                                reset_below=0), 5, cold=True, queued=True)
     rs_olo, rs_ohi = torch.empty_like(rs_lo), torch.empty_like(rs_hi)
-    g_rs = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g_rs):
-        fm.lf_step_batch(rs_tok, rs_lo, rs_hi, SHIFT, lo_out=rs_olo, hi_out=rs_ohi, reset_below=0)
-    rs_cold = timed(g_rs, 5, cold=True, queued=True)
+    rs_cold = timed(lambda: fm.lf_step_batch(rs_tok, rs_lo, rs_hi, SHIFT, lo_out=rs_olo, hi_out=rs_ohi,
+                                             reset_below=0), 5, cold=True, queued=True)
     log(f"rank 2^19 cold launches (us, median reported): {', '.join(f'{t * 1e3:.1f}' for t in rs_cold)}")
     rs_ok = bool(torch.equal(rs_olo, rs_ref[0]) and torch.equal(rs_ohi, rs_ref[1]))
     r2 = None
     if r2_tok is not None:
         r2_olo, r2_ohi = torch.empty_like(r2_lo), torch.empty_like(r2_hi)
-        g_r2 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_r2):
+
+        def r2_launch():
             fm.lf_step_batch(r2_tok, r2_lo, r2_hi, SHIFT, lo_out=r2_olo, hi_out=r2_ohi, reset_below=0)
-        r2_cold = timed(g_r2, 5, cold=True, queued=True)
-        r2_warm = timed(g_r2, 3)
+        r2_cold = timed(r2_launch, 5, cold=True, queued=True)
+        r2_warm = timed(r2_launch, 3, queued=True)
         r2 = {"rows": int(r2_tok.numel()), "avg_launch_us_cold": float(np.median(r2_cold)) * 1e3,
               "avg_launch_us_warm": float(np.median(r2_warm)) * 1e3,
               "matches_decode_kernel": bool(torch.equal(r2_olo, r2_ref[0]) and torch.equal(r2_ohi, r2_ref[1]))}
-        del g_r2, r2_olo, r2_ohi
+        del r2_olo, r2_ohi
     mask_ms = [t / K for t in timed(g_mask, 5)]
     packed_cold = None
     if g_packed is not None:
@@ -1435,7 +1437,7 @@ def main():
                                   "M_lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6) / 1e6,
                                   "matches_decode_kernel": rs_ok,
                                   "note": "2^19 independent (state, token) pairs of a 65536-row trace in one k_lf launch "
-                                          "(the in-wave sweep k_lf_sweep<true>, which the library picks from 2^18 rows: one lane per row, narrow rows packed, cached rows probed eight per round trip, tail rows in-wave), cold after a clean eviction, timed queued"},
+                                          "(the in-wave sweep k_lf_sweep<true>, which the library picks from 2^18 rows: one lane per row, narrow rows packed, cached rows probed eight per round trip, tail rows in-wave), cold after a clean eviction, one direct launch timed queued behind it (no graph node)"},
                      "bytes_model": "64-B lines the LF plan reads per live row (bench.lf_plan_bytes)"},
             "k_decode_mask_only": {"avg_launch_us": mask_us, "alg_bytes_per_launch": mask_bytes_per_launch,
                                    "GBps": mask_bytes_per_launch / (mask_us * 1e-6) / 1e9},
@@ -1457,7 +1459,10 @@ def main():
                  "frac_of_gather_ceiling": (rank_gbs_scale / gather_gbs) if gather_gbs else None,
                  "lf_steps_per_s": rs_tok.numel() / (rs_us * 1e-6),
                  "b256_GBps": rank_gbs, "b256_avg_launch_us_cold": lf_us_cold,
-                 "pairs_2_21": r2},
+                 "pairs_2_21": r2,
+                 "timing": "each launch direct (not a one-node graph replay: ~13 us of GPU-side cost per replay, "
+                           "profiles/r05_graph_launch/), enqueued behind a clean 1 GiB eviction, median of 5, as "
+                           "the 1M-request gather ceiling"},
     }
     # PMC traffic (tools/pmc_traffic.sh) is collected in a separate rocprofv3 run and committed;
     # it is used only when it was counted on this very library build, config and mask layout

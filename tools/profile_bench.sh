@@ -38,4 +38,6 @@ PY
 python3 tools/trace_durations.py "$TRACE" "k_decode<true, true," --out "$OUT/c4_shard_decode_dispatches.json" > /dev/null || true
 python3 tools/trace_durations.py "$TRACE" "k_or_unpack" --out "$OUT/c4_or_dispatches.json" || true
 python3 tools/trace_durations.py "$TRACE" "k_lf_group" --out "$OUT/lf_group_dispatches.json" > /dev/null || true
+# the rank legs (2^19 / 2^21 pairs: the in-wave sweep, by grid size) against the bench's events
+python3 tools/trace_durations.py "$TRACE" "k_lf_sweep" --out "$OUT/lf_sweep_dispatches.json" > /dev/null || true
 rm -rf "$OUT/raw"

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--works", default="0,2", help="LF variants (tuning lf_work) to time")
     ap.add_argument("--rank-only", action="store_true", help="only the rank launches")
     ap.add_argument("--sizes", default="19,21", help="log2 of the pairs per launch (2^19 / 2^21: the bench's pairs)")
+    ap.add_argument("--eager", action="store_true",
+                    help="also time each rank launch as a direct (eager) launch, queued the same way "
+                         "(no graph node: the graph replay's own GPU-side cost is the difference)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     V = 128256
@@ -115,6 +118,13 @@ def main():
                     ts = timed(g.replay, temp, args.reps)
                     e[temp + "_us"] = sorted(ts)
                     e[temp + "_median_us"] = float(np.median(ts))
+                if args.eager:
+                    def direct():
+                        fm.lf_step_batch(tok, lo, hi, SHIFT, lo_out=olo, hi_out=ohi, reset_below=0)
+                    for temp in ("cold", "warm"):
+                        ts = timed(direct, temp, args.reps)
+                        e["eager_" + temp + "_us"] = sorted(ts)
+                        e["eager_" + temp + "_median_us"] = float(np.median(ts))
                 e["exact"] = bool(torch.equal(olo, ref[0]) and torch.equal(ohi, ref[1]))
                 del g
             except Exception as ex:
