@@ -32,6 +32,7 @@ import gc
 import json
 import os
 import sys
+import threading
 import time
 import traceback
 
@@ -1024,6 +1025,8 @@ def main():
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the doc-range sharded leg")
     ap.add_argument("--sharded-at-1", action="store_true",
                     help="run the sharded leg at N = 1 too (one shard; exercises the path on a one-GPU box)")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0,
+                    help="seconds the doc-range sharded leg may take before the line is printed without it")
     ap.add_argument("--sharded-batches", default="2048",
                     help="global batch sizes the sharded leg runs besides --batch (comma list; '' = none)")
     ap.add_argument("--no-c4", action="store_true",
@@ -1576,12 +1579,39 @@ def main():
         holder = [bwt, fm]
         del bwt, fm
         torch.cuda.empty_cache()
+        # Watchdog: the replica line is already measured; a sharded leg stuck in a collective or a
+        # peer wait (first run over more than one rank on a new node) must not take it down.  Every
+        # rank arms its own timer; on expiry rank 0 prints the line with the leg marked as timed out
+        # and every rank leaves with status 0 (os._exit: no teardown of the stuck communicator).
+        emit_lock = threading.Lock()
+        emitted = [False]
+
+        def on_stuck():
+            with emit_lock:
+                if emitted[0]:
+                    return
+                emitted[0] = True
+                result["sharded"] = {"value": None,
+                                     "error": f"watchdog: the sharded leg did not finish within {args.sharded_timeout:g} s"}
+                log(result["sharded"]["error"])
+                if rank == 0:
+                    line_out.write(json.dumps(result) + "\n")
+                    line_out.flush()
+                sys.stderr.flush()
+                os._exit(0)
+
+        dog = threading.Timer(args.sharded_timeout, on_stuck)
+        dog.daemon = True
+        dog.start()
         try:
             result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, K, W, world, rank, dev, shs)
             log(f"sharded: {result['sharded']['value'] / 1e6:.2f} M masks/s, "
                 f"{result['sharded']['ms_per_step'] * 1e3:.1f} us/step, exact {result['sharded']['masks_equal_unsharded']}")
         except Exception as e:  # the replica line must still print
             result["sharded"] = {"value": None, "error": repr(e)}
+        dog.cancel()
+        with emit_lock:   # the timer may be firing right now: it prints, this thread waits for its exit
+            emitted[0] = True
     elif want_c4:
         holder = [bwt, fm]
         del bwt, fm
