@@ -77,8 +77,16 @@ def payload_capacity(B: int, vocab: int) -> int:
 
 
 def _stream_of(t) -> int:
+    """The raw handle of the current stream on t's device: torch's C-level
+    getter (~0.1 us) where it exists -- torch.cuda.current_stream() builds a
+    Stream object on every call (~2 us, a quarter of a decode-step launch's
+    host cost, tools/probe_launch_host.py)."""
     import torch
 
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if raw is not None:
+        return int(raw(idx))
     return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
