@@ -729,7 +729,8 @@ class PeerExchange:
         from ._lib import check, lib
 
         if stream is None:
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            stream = torch._C._cuda_getCurrentRawStream(idx)   # (no Stream object per step)
         world = self.world
         if self._skip_signal:
             self._skip_signal -= 1
@@ -843,7 +844,7 @@ def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, u
                else torch.empty((B, W), dtype=torch.int32, device=ptrs.device))
     assert out.stride(1) == 1 and out.device == ptrs.device
     ld = out.stride(0) * out.element_size()
-    stream = torch.cuda.current_stream(ptrs.device).cuda_stream
+    stream = torch._C._cuda_getCurrentRawStream(ptrs.device.index)
     if flags is not None:
         fw, ctr, err_ptr, spins = flags
         if fw.numel() < nparts:
@@ -878,7 +879,7 @@ def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = 
                else torch.empty((B, W), dtype=torch.int32, device=parts.device))
     assert parts.dtype == torch.int32 and parts.is_contiguous() and out.stride(1) == 1
     ld = out.stride(0) * out.element_size()
-    stream = torch.cuda.current_stream(parts.device).cuda_stream
+    stream = torch._C._cuda_getCurrentRawStream(parts.device.index)
     check(lib().fm_shard_or_rows(c_void_p(parts.data_ptr()), P, stride, B, vocab, int(shift), c_void_p(out.data_ptr()),
                                  ld, 1 if unpack else 0, c_void_p(stream)), "shard_or_rows")
     return out
@@ -960,7 +961,7 @@ def or_bits(parts, vocab: int, out=None, unpack: bool = True):
         raise ValueError(f"or_bits: out must be a row-major {'uint8' if unpack else 'int32'} {want}, "
                          f"got {out.dtype} {tuple(out.shape)} strides {out.stride()}")
     ld = out.stride(0) * out.element_size()
-    stream = torch.cuda.current_stream(parts.device).cuda_stream
+    stream = torch._C._cuda_getCurrentRawStream(parts.device.index)
     check(lib().fm_or_bits(c_void_p(parts.data_ptr()), P, B * W, B, W, vocab, c_void_p(out.data_ptr()), ld,
                            1 if unpack else 0, c_void_p(stream)), "or_bits")
     return out
