@@ -1561,6 +1561,15 @@ def main():
                 result["rank"]["request_rate_G_per_s"] = rate
                 result["rank"]["frac_of_request_ceiling"] = rate / req_ceiling if req_ceiling else None
                 result["rank"]["frac_of_request_ceiling_1M_cold"] = rate / req_ceiling_1m if req_ceiling_1m else None
+                # the 2^21-pair launches of the same file (33.5 MB of new states written each)
+                r21 = [r for r in t["dispatches"] if "k_lf_sweep" in r["kernel"] and 3e7 <= r.get("write_bytes", 0) < 4e7]
+                p21 = result["rank"].get("pairs_2_21")
+                if r21 and p21 and p21.get("avg_launch_us_cold"):
+                    req21 = float(np.median([r["rdreq"] for r in r21]))
+                    rate21 = req21 / (p21["avg_launch_us_cold"] * 1e-6) / 1e9
+                    p21.update({"pmc_requests_per_launch": req21, "request_rate_G_per_s": rate21,
+                                "frac_of_request_ceiling": rate21 / req_ceiling if req_ceiling else None,
+                                "frac_of_request_ceiling_1M_cold": rate21 / req_ceiling_1m if req_ceiling_1m else None})
         except Exception as e:
             result[where]["pmc_requests_source"] = f"unreadable: {e!r}"
     if cpu_leg:
