@@ -1004,6 +1004,40 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
 
 
 # ---------------------------------------------------------------------------
+class LegWatchdog:
+    """A timer that, unless finish() comes first, runs ``on_expiry`` (which prints what
+    must still be printed) and ends the process with status 0 -- os._exit, so that a
+    thread stuck in a collective or a device wait cannot hold the exit.  finish() and the
+    expiry exclude each other: whichever comes second does nothing (a finish() racing the
+    expiry waits for the exit)."""
+
+    def __init__(self, seconds: float, on_expiry, exit_code: int = 0):
+        self._lock = threading.Lock()
+        self._done = False
+        self._on_expiry = on_expiry
+        self._code = exit_code
+        self._timer = threading.Timer(seconds, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def _fire(self):
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+            try:
+                self._on_expiry()
+            finally:
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(self._code)
+
+    def finish(self):
+        self._timer.cancel()
+        with self._lock:
+            self._done = True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1592,35 +1626,22 @@ def main():
         # peer wait (first run over more than one rank on a new node) must not take it down.  Every
         # rank arms its own timer; on expiry rank 0 prints the line with the leg marked as timed out
         # and every rank leaves with status 0 (os._exit: no teardown of the stuck communicator).
-        emit_lock = threading.Lock()
-        emitted = [False]
-
         def on_stuck():
-            with emit_lock:
-                if emitted[0]:
-                    return
-                emitted[0] = True
-                result["sharded"] = {"value": None,
-                                     "error": f"watchdog: the sharded leg did not finish within {args.sharded_timeout:g} s"}
-                log(result["sharded"]["error"])
-                if rank == 0:
-                    line_out.write(json.dumps(result) + "\n")
-                    line_out.flush()
-                sys.stderr.flush()
-                os._exit(0)
+            result["sharded"] = {"value": None,
+                                 "error": f"watchdog: the sharded leg did not finish within {args.sharded_timeout:g} s"}
+            log(result["sharded"]["error"])
+            if rank == 0:
+                line_out.write(json.dumps(result) + "\n")
+                line_out.flush()
 
-        dog = threading.Timer(args.sharded_timeout, on_stuck)
-        dog.daemon = True
-        dog.start()
+        dog = LegWatchdog(args.sharded_timeout, on_stuck)
         try:
             result["sharded"] = sharded_leg(holder, args.seed, n_tokens, V, K, W, world, rank, dev, shs)
             log(f"sharded: {result['sharded']['value'] / 1e6:.2f} M masks/s, "
                 f"{result['sharded']['ms_per_step'] * 1e3:.1f} us/step, exact {result['sharded']['masks_equal_unsharded']}")
         except Exception as e:  # the replica line must still print
             result["sharded"] = {"value": None, "error": repr(e)}
-        dog.cancel()
-        with emit_lock:   # the timer may be firing right now: it prints, this thread waits for its exit
-            emitted[0] = True
+        dog.finish()
     elif want_c4:
         holder = [bwt, fm]
         del bwt, fm

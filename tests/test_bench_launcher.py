@@ -128,3 +128,49 @@ def test_launcher_parent_never_calls_torch_cuda(monkeypatch):
     assert ex.value.code == 0
     assert not calls
     assert spawned and spawned[0][0] == 4 and spawned[0][1][-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def _run_stub(tmp_path, body, timeout=60):
+    import subprocess
+
+    head = textwrap.dedent(f"""
+        import sys, time
+        sys.path.insert(0, {REPO!r})
+        from bench import LegWatchdog
+    """)
+    cmd = _stub(tmp_path, head + textwrap.dedent(body))
+    t0 = time.time()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    return p, time.time() - t0
+
+
+def test_leg_watchdog_prints_and_exits_zero_when_the_leg_hangs(tmp_path):
+    """The N > 1 sharded leg's watchdog (bench.LegWatchdog): a leg that never returns
+    (a thread stuck in a collective) ends the process with status 0 right after the
+    expiry callback printed the line."""
+    p, dt = _run_stub(tmp_path, """
+        def expire():
+            print('{"value": 1, "sharded": {"error": "watchdog"}}', flush=True)
+        dog = LegWatchdog(0.5, expire)
+        time.sleep(30)          # the stuck leg
+        print("not reached")
+    """)
+    assert p.returncode == 0, p.stderr
+    assert '"watchdog"' in p.stdout and "not reached" not in p.stdout
+    assert dt < 20
+
+
+def test_leg_watchdog_finish_cancels(tmp_path):
+    """A leg that returns in time: finish() cancels the timer, the process goes on and
+    the expiry callback never runs."""
+    p, _ = _run_stub(tmp_path, """
+        def expire():
+            print("expired", flush=True)
+        dog = LegWatchdog(1.0, expire)
+        time.sleep(0.1)
+        dog.finish()
+        time.sleep(1.5)         # past the timer's deadline
+        print("line", flush=True)
+    """)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.split() == ["line"]
