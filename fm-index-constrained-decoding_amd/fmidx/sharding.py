@@ -117,10 +117,12 @@ class ShardedDecoder:
     is valid until the next step.
     """
 
-    def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "max_u8",
+    def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "auto",
                  halo: Optional[int] = None, peer_barrier: str = "flags", graph: bool = False,
                  spins: Optional[int] = None):
-        """reduce: "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
+        """reduce: "auto" (the default: "peer" with the flag barrier -- the fastest exact exchange,
+        bench.py's sharded leg -- over an RCCL group of more than one rank, i.e. the GPUs of one
+        node; "max_u8" otherwise), "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
         (all_gather of the packed rows + fm_or_bits), "sparse" (BWT slices /
         bitmaps per row, fm_shard_pack + all_gather + fm_shard_or_rows) or
         "peer" (the same payloads read in place over xGMI: PeerExchange, whose
@@ -133,6 +135,13 @@ class ShardedDecoder:
         self.vocab = vocab
         self.shift = shift
         self.group = group
+        if reduce == "auto":
+            reduce = "max_u8"
+            if group is not None:
+                import torch.distributed as dist
+
+                if dist.get_backend(group) == "nccl" and dist.get_world_size(group) > 1:
+                    reduce = "peer"
         if reduce not in ("max_u8", "gather_bits", "sparse", "peer"):
             raise ValueError(reduce)
         if graph and not (reduce == "peer" and peer_barrier == "flags"):

@@ -285,3 +285,16 @@ def test_fixed_slot_payload_reads_like_compact():
     want = or_payloads_host(compact.unsqueeze(0), B, V, SH)
     assert torch.equal(got, want)
     assert torch.equal(want, torch.from_numpy(bits[:, :V]))
+
+
+def test_decoder_default_exchange_without_rccl():
+    """reduce="auto" (the default) is the peer exchange only over an RCCL group of more than one
+    rank; a single process (group None) resolves to the plain max_u8 path."""
+    from fmidx.sharding import ShardedDecoder
+
+    class _Shard:   # only the attributes the constructor reads
+        pass
+
+    assert ShardedDecoder(_Shard(), 16, 0).reduce == "max_u8"
+    with pytest.raises(ValueError):
+        ShardedDecoder(_Shard(), 16, 0, reduce="ring")
