@@ -582,14 +582,20 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
             nonlocal payload
             lo, hi = lo0.clone(), hi0.clone()
             bufs = [(lo, hi), (torch.empty_like(lo), torch.empty_like(hi))]
-            flags = mode in ("peer_flags", "peer_flags_graph")
+            flags = mode in ("peer_flags", "peer_flags_graph", "peer_flags_checked")
+            checked = mode == "peer_flags_checked"
             tok_static = torch.empty_like(tokens[0])
+            ev_chk = torch.cuda.Event()
 
             def step(i, tok=None):
                 nonlocal payload
                 src, dst = bufs[i % 2], bufs[(i + 1) % 2]
                 if flags:            # state in place, the buffer and the step number on the device
                     peer.flags_step(ix, tokens[i] if tok is None else tok, lo, hi, V, SHIFT, out)
+                    if checked:      # exact or absent (ShardedDecoder's default): wait, read the error word
+                        ev_chk.record()
+                        ev_chk.synchronize()
+                        peer.check()
                     return
                 if mode == "peer":   # the decode kernel writes the payload itself
                     pay = peer.payload()
@@ -673,7 +679,16 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
                                    "masks_equal_unsharded": exact_pf, "flag_timeouts": to_pf,
                                    "step": "as peer, with the flag barrier: fm_peer_signal (the device step counter "
                                            "advanced, a system-scope release, stores into every rank's flag array) "
-                                           "+ fm_shard_or_rows_peers_wait; state updated in place; eager launches"}
+                                           "+ fm_shard_or_rows_peers_wait; state updated in place; eager launches; "
+                                           "the error word read only after the timed region (ShardedDecoder's "
+                                           "check='deferred')"}
+            ms_pc, exact_pc, to_pc = run("peer_flags_checked")
+            modes["peer_flags_checked"] = {"ms_per_step": ms_pc, "value": B / (ms_pc / 1e3),
+                                           "masks_equal_unsharded": exact_pc, "flag_timeouts": to_pc,
+                                           "wait_cost_us_per_step": (ms_pc - ms_pf) * 1e3,
+                                           "step": "as peer_flags, plus the exact-or-absent check every step "
+                                                   "(ShardedDecoder's default check='sync'): an event after the "
+                                                   "OR pass, waited on, then the error word read"}
             try:
                 ms_pg, exact_pg, to_pg = run("peer_flags_graph")
                 modes["peer_flags_graph"] = {"ms_per_step": ms_pg, "value": B / (ms_pg / 1e3),
@@ -1004,14 +1019,19 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
 
 
 # ---------------------------------------------------------------------------
+WATCHDOG_EXIT = 3   # a leg that hung: the line is printed, the run still fails
+
+
 class LegWatchdog:
     """A timer that, unless finish() comes first, runs ``on_expiry`` (which prints what
-    must still be printed) and ends the process with status 0 -- os._exit, so that a
+    must still be printed) and ends the process with status ``exit_code`` (default
+    WATCHDOG_EXIT = 3: a hang is evidence of a fault, so the launcher and CI see a failed
+    run even though the already-measured line is on stdout) -- os._exit, so that a
     thread stuck in a collective or a device wait cannot hold the exit.  finish() and the
     expiry exclude each other: whichever comes second does nothing (a finish() racing the
     expiry waits for the exit)."""
 
-    def __init__(self, seconds: float, on_expiry, exit_code: int = 0):
+    def __init__(self, seconds: float, on_expiry, exit_code: int = WATCHDOG_EXIT):
         self._lock = threading.Lock()
         self._done = False
         self._on_expiry = on_expiry
@@ -1625,7 +1645,8 @@ def main():
         # Watchdog: the replica line is already measured; a sharded leg stuck in a collective or a
         # peer wait (first run over more than one rank on a new node) must not take it down.  Every
         # rank arms its own timer; on expiry rank 0 prints the line with the leg marked as timed out
-        # and every rank leaves with status 0 (os._exit: no teardown of the stuck communicator).
+        # and every rank leaves with status WATCHDOG_EXIT (3: the run fails, the measured line is still
+        # on stdout; os._exit: no teardown of the stuck communicator).
         def on_stuck():
             result["sharded"] = {"value": None,
                                  "error": f"watchdog: the sharded leg did not finish within {args.sharded_timeout:g} s"}

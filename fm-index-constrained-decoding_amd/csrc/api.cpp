@@ -1014,6 +1014,12 @@ int fm_set_build_options(fm_index* h, const fm_build_options* o) {
   fmidx::BuildOpts x = to_internal(*o);
   if (fmidx::apply_build_overrides(x) || !valid(x)) return -1;
   std::lock_guard<std::mutex> lk(h->mu);
+  if (h->idx.built) {
+    // the options shape the structures a build makes; a built index keeps the ones it was built
+    // with, and fm_get_build_options must keep describing them (stats()['follow_bytes'] ...)
+    set_error("set_build_options: the index is already built (set them before initialize / load)");
+    return -1;
+  }
   h->idx.opts = x;
   return 0;
   FM_API_END

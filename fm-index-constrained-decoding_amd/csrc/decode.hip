@@ -342,8 +342,20 @@ __device__ __forceinline__ void store16_emit(__amdgpu_buffer_rsrc_t r, uint32_t 
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kLateAux);
 }
 
+// AUX: kStoreAux (sc1, agent-scope write-through) for masks; kPayAux for the peer exchange's payload
+template <int AUX = kStoreAux>
 __device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t x) {
-  __builtin_amdgcn_raw_buffer_store_b32(x, r, off, 0, kStoreAux);
+  __builtin_amdgcn_raw_buffer_store_b32(x, r, off, 0, AUX);
+}
+
+// The peer exchange's payload (PAY) is read by OTHER GPUs over xGMI, straight from this GPU's
+// memory (csrc/shard.hip k_or_rows<true>: system-scope loads).  Its stores are system-scope
+// write-through (sc0 sc1): every payload byte has left this XCD's L2 when the store is
+// acknowledged, so its visibility to a remote reader does not depend on the end-of-kernel
+// release (its scope, or which XCDs' L2s it writes back) -- DESIGN.md §5 "Visibility".
+constexpr int kPayAux = 1 | 16;
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // global_store_dword sc0 sc1
 }
 
 // 16 mask bits -> 16 bytes of 0/1
@@ -375,17 +387,32 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // (the symbols) and nothing else -- no zero-fill, no bitmap; every other row
 // writes its packed bitmap into its slot exactly as PACKED does; the row's
 // workgroup writes its desc / off words, row 0's the header.
+// The row-state pointers: __restrict__ (never aliased: the uint8 / packed launches refuse in-place
+// state) except in the payload variant, whose flag-barrier step updates the state IN PLACE.  There
+// every wave consumes its state load (the early-zero / wg_scan decisions) before the plan barrier,
+// and thread 0 stores the new state after it (see the store below).
+template <bool PAY> struct StatePtr {
+  typedef const uint64_t* __restrict__ in;
+  typedef uint64_t* __restrict__ out;
+};
+template <> struct StatePtr<true> {
+  typedef const uint64_t* in;
+  typedef uint64_t* out;
+};
+
 template <bool PACKED, bool DO_LF, int kDecThreads, bool PAY = false>
 // Argument order: the per-row state pointers and the slice geometry come first
 // so that, with kernel-argument preloading (Makefile: -amdgpu-kernarg-preload-
 // count), they arrive in SGPRs at dispatch and the row-state loads issue
 // before any kernel-argument memory load; the large DevView comes last.
+// (PAY updates the state in place -- lo_in == lo_out -- so its state pointers carry no
+// __restrict__: StateIn / StateOut below.)
 __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_SMALL_WG_WAVES) k_decode(const int64_t* __restrict__ tok,
-                                                       const uint64_t* __restrict__ lo_in,
-                                                       const uint64_t* __restrict__ hi_in, uint64_t m,
+                                                       typename StatePtr<PAY>::in lo_in,
+                                                       typename StatePtr<PAY>::in hi_in, uint64_t m,
                                                        uint32_t S, uint32_t SW, uint64_t vocab,
-                                                       uint64_t* __restrict__ lo_out,
-                                                       uint64_t* __restrict__ hi_out,
+                                                       typename StatePtr<PAY>::out lo_out,
+                                                       typename StatePtr<PAY>::out hi_out,
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
                                                        uint64_t early_width, DevView v,
@@ -393,6 +420,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        uint32_t* __restrict__ pay_alt,
                                                        const uint32_t* __restrict__ pay_sel) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
+  constexpr int kAux4 = PAY ? kPayAux : kStoreAux;   // the 4-B stores' cache policy
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
   // zero-filling waves -- from thread 256, 512 or 768 -- measured the same)
   constexpr int kEzFirst = 64;
@@ -472,7 +500,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       if (kEzSleep && k >= kDecThreads - kEzFirst) __builtin_amdgcn_s_sleep(kEzSleep);
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
-        store4(orsrc, (uint32_t)(k * 4), 0u);
+        store4<kAux4>(orsrc, (uint32_t)(k * 4), 0u);
       } else if (aligned16 && t + CH <= t1) {
         store16(orsrc, (uint32_t)(k * 16), make_uint4(0, 0, 0, 0));
       } else {
@@ -590,13 +618,13 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     const bool sparse = lo >= hi || (hi - lo < Wd && plan.nb == 0);   // workgroup-uniform
     if (threadIdx.x == 0) {
       const uint64_t H = 4 + ((2 * m + 3) & ~3ull);
-      pay[4 + row] = sparse ? (uint32_t)(lo < hi ? hi - lo : 0) : (Wd | 0x80000000u);
-      pay[4 + m + row] = (uint32_t)(H + row * W4);
+      sys_store(&pay[4 + row], sparse ? (uint32_t)(lo < hi ? hi - lo : 0) : (Wd | 0x80000000u));
+      sys_store(&pay[4 + m + row], (uint32_t)(H + row * W4));
       if (row == 0) {
-        pay[0] = (uint32_t)(H + m * W4);
-        pay[1] = (uint32_t)m;
-        pay[2] = Wd;
-        pay[3] = kPayMagic;
+        sys_store(&pay[0], (uint32_t)(H + m * W4));
+        sys_store(&pay[1], (uint32_t)m);
+        sys_store(&pay[2], Wd);
+        sys_store(&pay[3], kPayMagic);
       }
     }
     if (sparse) {
@@ -615,7 +643,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const uint32_t i = i0 + threadIdx.x + (uint32_t)u * kDecThreads;
-          if (i < w) store4(orsrc, i * 4, sy[u]);
+          if (i < w) store4<kAux4>(orsrc, i * 4, sy[u]);
         }
       }
       if (DO_LF && threadIdx.x == 0) {
@@ -638,7 +666,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     for (uint64_t k = threadIdx.x - e_first; k < nch; k += kDecThreads - e_first) {
       const uint64_t t = t0 + k * CH;
       if (PACKED) {
-        store4(orsrc, (uint32_t)(k * 4), 0u);
+        store4<kAux4>(orsrc, (uint32_t)(k * 4), 0u);
       } else if (aligned16 && t + CH <= t1) {
         store16(orsrc, (uint32_t)(k * 16), make_uint4(0, 0, 0, 0));
       } else {
@@ -799,7 +827,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         if (PACKED && !full) bits &= (1u << (uint32_t)(t1 - t)) - 1u;
         if (zeroed && bits == 0) continue;
         if (PACKED) {
-          store4(orsrc, k * 4, bits);
+          store4<kAux4>(orsrc, k * 4, bits);
         } else if (aligned16 && full) {
           store16_emit(orsrc, k * 16, bits16_to_bytes(bits), zeroed);
         } else {
@@ -831,7 +859,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
       if (cnt < CH) bits &= (1u << cnt) - 1u;
       if (zeroed && bits == 0) continue;
       if (PACKED) {
-        store4(orsrc, (uint32_t)(k * 4), bits);   // t0 and t are multiples of 32
+        store4<kAux4>(orsrc, (uint32_t)(k * 4), bits);   // t0 and t are multiples of 32
       } else if (aligned16 && cnt == 16) {
         store16_emit(orsrc, (uint32_t)(k * 16), bits16_to_bytes(bits), zeroed);
       } else {

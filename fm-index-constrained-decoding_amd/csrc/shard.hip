@@ -232,6 +232,13 @@ __device__ __forceinline__ uint64_t pack_row_words(uint64_t l, uint64_t h, uint6
   return (count + 3) & ~3ull;
 }
 
+// The payload's stores are system-scope write-through (sc0 sc1): a payload packed into a peer
+// exchange's buffer is read by other GPUs over xGMI from this GPU's memory, and no byte of it may
+// wait in this XCD's L2 for the end-of-kernel release (DESIGN.md §5 "Visibility").
+__device__ __forceinline__ void pay_store(uint32_t* p, uint32_t x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint64_t* __restrict__ lo,
                                                           const uint64_t* __restrict__ hi,
                                                           const uint32_t* __restrict__ bits, uint64_t ldw,
@@ -241,7 +248,7 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint64_t H = payload_header_words(B);
   if (B == 0) {   // the empty payload: its header alone
-    if (t < H) pay[t] = t == 0 ? (uint32_t)H : t == 2 ? W : t == 3 ? kPayloadMagic : 0u;
+    if (t < H) pay_store(&pay[t], t == 0 ? (uint32_t)H : t == 2 ? W : t == 3 ? kPayloadMagic : 0u);
     return;
   }
   // the padded sizes of rows [0, b): every load issued before any is used
@@ -272,17 +279,17 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
 #pragma unroll
   for (int k = 0; k < kPackRowThreads / 64; ++k) off += s_part[k];
   if (t == 0) {
-    pay[4 + b] = desc;
-    pay[4 + B + b] = (uint32_t)off;
+    pay_store(&pay[4 + b], desc);
+    pay_store(&pay[4 + B + b], (uint32_t)off);
     if (b == B - 1) {
-      pay[0] = (uint32_t)(off + words);
-      pay[1] = (uint32_t)B;
-      pay[2] = W;
-      pay[3] = kPayloadMagic;
+      pay_store(&pay[0], (uint32_t)(off + words));
+      pay_store(&pay[1], (uint32_t)B);
+      pay_store(&pay[2], W);
+      pay_store(&pay[3], kPayloadMagic);
     }
   }
   if (b == 0)
-    for (uint64_t i = 4 + 2 * B + t; i < H; i += kPackRowThreads) pay[i] = 0u;
+    for (uint64_t i = 4 + 2 * B + t; i < H; i += kPackRowThreads) pay_store(&pay[i], 0u);
   const uint32_t count = desc & 0x7FFFFFFFu;
   const bool dense = (desc >> 31) != 0;
   const uint64_t s0 = min(l0, v.n - 1);
@@ -305,7 +312,7 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t i = i0 + u * kPackRowThreads + t;
-      if (i < (uint32_t)words) dst[i] = i < count ? x[u] : 0u;
+      if (i < (uint32_t)words) pay_store(&dst[i], i < count ? x[u] : 0u);
     }
   }
 }

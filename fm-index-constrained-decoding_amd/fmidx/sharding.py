@@ -94,6 +94,35 @@ def shard_text_device(text, beginnings, world: int, rank: int, halo: int):
     return out, (a, b)
 
 
+def host_identity() -> str:
+    """This machine's identity: hostname + kernel boot id (two containers of one
+    node share the boot id; two nodes never do)."""
+    import socket
+
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}/{boot}"
+
+
+def peer_capable(group) -> bool:
+    """True when the peer exchange can serve ``group``: an RCCL ("nccl") group of
+    more than one rank whose ranks all run on ONE host -- the payload buffers are
+    mapped through hipIpc handles, which do not cross nodes.  Collective (every
+    rank of ``group`` calls it): the ranks' host identities are all_gathered."""
+    if group is None:
+        return False
+    import torch.distributed as dist
+
+    if dist.get_backend(group) != "nccl" or dist.get_world_size(group) <= 1:
+        return False
+    every = [None] * dist.get_world_size(group)
+    dist.all_gather_object(every, host_identity(), group=group)
+    return len(set(every)) == 1
+
+
 class HaloExceeded(ValueError):
     """A row's pattern outgrew the shards' halo: OR over shards would no longer
     equal the unsharded mask (occurrences crossing a shard boundary by more
@@ -119,10 +148,11 @@ class ShardedDecoder:
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "auto",
                  halo: Optional[int] = None, peer_barrier: str = "flags", graph: bool = False,
-                 spins: Optional[int] = None):
+                 spins: Optional[int] = None, check: str = "sync"):
         """reduce: "auto" (the default: "peer" with the flag barrier -- the fastest exact exchange,
-        bench.py's sharded leg -- over an RCCL group of more than one rank, i.e. the GPUs of one
-        node; "max_u8" otherwise), "max_u8" (all_reduce MAX of the uint8 mask), "gather_bits"
+        bench.py's sharded leg -- over an RCCL group of more than one rank whose ranks all run on
+        one host (the IPC mappings do not cross nodes; same_host()); "max_u8" otherwise), "max_u8"
+        (all_reduce MAX of the uint8 mask), "gather_bits"
         (all_gather of the packed rows + fm_or_bits), "sparse" (BWT slices /
         bitmaps per row, fm_shard_pack + all_gather + fm_shard_or_rows) or
         "peer" (the same payloads read in place over xGMI: PeerExchange, whose
@@ -130,20 +160,28 @@ class ShardedDecoder:
         ``graph`` (peer + flags): the step -- the payload decode, the signal,
         the OR pass -- is captured into ONE HIP graph at its first call and
         replayed for every later step (the tokens copied into its static
-        input); the step number and the buffer parity live on the device."""
+        input); the step number and the buffer parity live on the device.
+        ``check`` (flag barrier only): "sync" (the default) -- every step waits
+        for its own OR pass (an event after it) and reads the exchange's error
+        word before returning, so a step whose barrier timed out raises
+        PeerBarrierTimeout and returns NO mask: masks are exact or absent;
+        "deferred" -- no wait: the error word is read at the next call (and at
+        close()), so the step that timed out has already handed back a mask
+        that may be inexact (one stale mask at most) -- for callers that
+        overlap the next step's host work with this step's GPU work and accept
+        that contract."""
         self.index = index
         self.vocab = vocab
         self.shift = shift
         self.group = group
         if reduce == "auto":
-            reduce = "max_u8"
-            if group is not None:
-                import torch.distributed as dist
-
-                if dist.get_backend(group) == "nccl" and dist.get_world_size(group) > 1:
-                    reduce = "peer"
+            reduce = "peer" if peer_capable(group) else "max_u8"
         if reduce not in ("max_u8", "gather_bits", "sparse", "peer"):
             raise ValueError(reduce)
+        if check not in ("sync", "deferred"):
+            raise ValueError(check)
+        self.check = check
+        self._ev = None        # the event a checked flag-barrier step waits on
         if graph and not (reduce == "peer" and peer_barrier == "flags"):
             raise ValueError("graph: only the peer exchange with the flag barrier holds no collective")
         self.reduce = reduce
@@ -269,7 +307,7 @@ class ShardedDecoder:
                 self._g_tok.copy_(tokens)
                 self._g.replay()
             px.step += 1
-            return self._out
+            return self._checked(self._out)
         if self._buf is None:              # start() resets it: fresh second state buffers
             self._lo2 = torch.empty_like(self.lo)
             self._hi2 = torch.empty_like(self.hi)
@@ -279,7 +317,7 @@ class ShardedDecoder:
                                        reset_below=0)
         self.lo, self._lo2 = self._lo2, self.lo
         self.hi, self._hi2 = self._hi2, self.hi
-        return self._peer(pay, B, self.vocab, self.shift, out=self._out)
+        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out))
 
     def _combine_peer(self, bits):
         import torch
@@ -294,7 +332,23 @@ class ShardedDecoder:
         self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=pay)
         if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
             self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=pay.device)
-        return self._peer(pay, B, self.vocab, self.shift, out=self._out)
+        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out))
+
+    def _checked(self, out):
+        """Exact or absent: with the flag barrier and check="sync", wait for the
+        step's OR pass (an event recorded after it on the current stream) and
+        read the error word -- a step whose barrier timed out raises
+        PeerBarrierTimeout here and its mask is never returned."""
+        if self.peer_barrier != "flags" or self.check != "sync" or self._peer is None:
+            return out
+        import torch
+
+        if self._ev is None:
+            self._ev = torch.cuda.Event()
+        self._ev.record()
+        self._ev.synchronize()
+        self._peer.check()
+        return out
 
     def close(self):
         """Release the peer exchange's mappings (collective: every rank calls it);
@@ -386,15 +440,19 @@ class ShardedIndex:
     bits ORed over the ranks -- so such a call returns the unsharded host
     path's output, or raises where the reference raises.  Every rank makes the
     same calls in the same order (they depend on the inputs, not the shard).
-    The default exchange is the fastest exact one: "peer" with the flag barrier
-    (no collective per exchange; a timed-out barrier raises
-    PeerBarrierTimeout).  The ``index.py`` query surface (get_range, distinct,
+    The default exchange ("auto") is the fastest exact one where it can run:
+    "peer" with the flag barrier (no collective per exchange; a timed-out
+    barrier raises PeerBarrierTimeout) over an RCCL group whose ranks share one
+    host (peer_capable), "sparse" otherwise (another backend, or ranks on
+    several nodes, where hipIpc mappings cannot reach).  The ``index.py`` query surface (get_range, distinct,
     ...) is the unsharded index's business and is not offered here."""
 
     sharded = True
 
-    def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "peer",
+    def __init__(self, shard, occurring_distinct, group=None, halo: Optional[int] = None, exchange: str = "auto",
                  shift: int = 10, peer_barrier: str = "flags", spins: Optional[int] = None):
+        if exchange == "auto":
+            exchange = "peer" if peer_capable(group) else "sparse"
         if exchange not in ("sparse", "dense", "peer"):
             raise ValueError(exchange)
         self.peer_barrier = peer_barrier
@@ -999,7 +1057,7 @@ def unpack_bits(packed, vocab: int):
     return bits[:, :vocab].contiguous()
 
 
-__all__ = ["shard_docs", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
+__all__ = ["shard_docs", "peer_capable", "host_identity", "halo_tokens", "shard_corpus", "shard_text_device", "ShardedDecoder", "HaloExceeded",
            "ShardedIndex",
            "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "or_payloads", "SparseExchange",
            "PeerExchange", "PeerBarrierTimeout", "or_peer_payloads", "pack_payload_host", "or_payloads_host",

@@ -63,7 +63,9 @@ void fm_destroy(fm_index* h);
  * Then change fields as needed.  An int field of -1 or a size field of 0 means
  * "the profile's value".  The environment variable FMIDX_BUILD_OPTIONS
  * ("key=value,...", keys = the field names) overrides the fields at
- * fm_create / fm_set_build_options time (measurement runs). */
+ * fm_create / fm_set_build_options time (measurement runs).
+ * fm_set_build_options returns -1 once the handle's index is built (a built
+ * index keeps, and fm_get_build_options reports, the options it was built with). */
 #define FM_PROFILE_DEFAULT 0
 #define FM_PROFILE_COMPACT 1
 typedef struct fm_build_options {

@@ -144,10 +144,10 @@ def _run_stub(tmp_path, body, timeout=60):
     return p, time.time() - t0
 
 
-def test_leg_watchdog_prints_and_exits_zero_when_the_leg_hangs(tmp_path):
+def test_leg_watchdog_prints_and_fails_when_the_leg_hangs(tmp_path):
     """The N > 1 sharded leg's watchdog (bench.LegWatchdog): a leg that never returns
-    (a thread stuck in a collective) ends the process with status 0 right after the
-    expiry callback printed the line."""
+    (a thread stuck in a collective) ends the process with status 3 (WATCHDOG_EXIT: a
+    hang fails the run) right after the expiry callback printed the line."""
     p, dt = _run_stub(tmp_path, """
         def expire():
             print('{"value": 1, "sharded": {"error": "watchdog"}}', flush=True)
@@ -155,7 +155,7 @@ def test_leg_watchdog_prints_and_exits_zero_when_the_leg_hangs(tmp_path):
         time.sleep(30)          # the stuck leg
         print("not reached")
     """)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == 3, p.stderr
     assert '"watchdog"' in p.stdout and "not reached" not in p.stdout
     assert dt < 20
 

@@ -20,7 +20,8 @@ it builds too:
     and boosts BOOST * 2^k past the float range (bf16: inf written, as the
     reference writes it; fp32: the reference's RuntimeError raised);
 and, separately, the flag barrier's timeout: rank 1 skips its signal for one
-step, and both ranks raise PeerBarrierTimeout instead of returning masks."""
+step, and both ranks raise PeerBarrierTimeout at that step instead of
+returning its mask (check="deferred": at the next call)."""
 import os
 import socket
 import time
@@ -140,7 +141,10 @@ def _qwen_host_path_cases(full, ix, F, rng):
     from fmidx.sharding import ShardedIndex
 
     bad = []
-    sidx = ShardedIndex(ix, full.occurring_distinct, group=dist.group.WORLD, halo=HALO)
+    # the processors' default exchange over gloo is "sparse" (auto: peer needs an RCCL group on one
+    # host); the peer exchange with the flag barrier is asked for explicitly here
+    assert ShardedIndex(ix, full.occurring_distinct, group=dist.group.WORLD, halo=HALO).exchange == "sparse"
+    sidx = ShardedIndex(ix, full.occurring_distinct, group=dist.group.WORLD, halo=HALO, exchange="peer")
     assert sidx.exchange == "peer" and sidx.peer_barrier == "flags"
     kw = dict(num_beams=1, min_new_tokens=3, always_allow_eos=True, length_reward_factor=2.0)
     ref_p = P.QwenIndexBasedLogitsProcessor(index=full, **kw)
@@ -198,9 +202,11 @@ def test_peer_exchange_two_processes(tmp_path, barrier):
 
 def _timeout_child(rank, world, port, outdir, _):
     """Rank 1 skips its flag-barrier signal at step 3: the step's OR pass times
-    out on both ranks (spin bound 2^16 polls, tens of ms), and the next call of
-    each rank raises PeerBarrierTimeout instead of returning a mask; close()
-    raises it too."""
+    out on both ranks (spin bound 2^16 polls, tens of ms).  With the default
+    check="sync" both ranks raise PeerBarrierTimeout AT step 3 -- the step that
+    timed out returns no mask (exact or absent); with the opt-in
+    check="deferred" the raise comes at the next call (step 4), as documented.
+    close() raises it too, either way."""
     import torch
     import torch.distributed as dist
 
@@ -218,31 +224,37 @@ def _timeout_child(rank, world, port, outdir, _):
         rng = np.random.default_rng(5)
         B = 32
         starts = rng.integers(0, len(F) - 40, size=B)
-        dec = ShardedDecoder(ix, V, 10, group=dist.group.WORLD, reduce="peer", halo=HALO, peer_barrier="flags",
-                             spins=1 << 16)
-        dec.start([F[a:a + 2] for a in starts], "cuda")
-        raised_at, msgs = None, []
-        for step in range(6):
-            dist.barrier()                  # the ranks start each step together: only the skip times out
-            if step == 3 and rank == 1:
-                dec._peer._skip_signal = 1
-            t = torch.tensor([F[a + 2 + step] for a in starts], dtype=torch.int64, device="cuda")
+        res = []
+        for check, want_at in (("sync", 3), ("deferred", 4)):
+            dec = ShardedDecoder(ix, V, 10, group=dist.group.WORLD, reduce="peer", halo=HALO, peer_barrier="flags",
+                                 spins=1 << 16, check=check)
+            dec.start([F[a:a + 2] for a in starts], "cuda")
+            raised_at, msgs, returned = None, [], []
+            for step in range(6):
+                dist.barrier()                  # the ranks start each step together: only the skip times out
+                if step == 3 and rank == 1:
+                    dec._peer._skip_signal = 1
+                t = torch.tensor([F[a + 2 + step] for a in starts], dtype=torch.int64, device="cuda")
+                try:
+                    dec.step(t)
+                    returned.append(step)
+                except PeerBarrierTimeout as e:
+                    raised_at = step
+                    msgs.append(str(e))
+                    break
+                torch.cuda.synchronize()        # deferred: the pass (and its error word) done before the next call
+            closed_raises = False
             try:
-                dec.step(t)
-            except PeerBarrierTimeout as e:
-                raised_at = step
-                msgs.append(str(e))
-                break
-            torch.cuda.synchronize()        # the step's pass (and its error word) is done before the next call
-        closed_raises = False
-        try:
-            dec.close()
-        except PeerBarrierTimeout:
-            closed_raises = True
-        res = "ok" if (raised_at == 4 and closed_raises and "step 4" in msgs[0]) else \
-            f"raised at {raised_at}, close raised {closed_raises}, {msgs}"
+                dec.close()
+            except PeerBarrierTimeout:
+                closed_raises = True
+            # the device step counter is 1-based: host step s is exchange step s + 1
+            if not (raised_at == want_at and closed_raises and bool(msgs) and "step 4" in msgs[0] and
+                    (check == "deferred" or 3 not in returned)):
+                res.append(f"{check}: raised at {raised_at} (want {want_at}), close raised {closed_raises}, "
+                           f"returned {returned}, {msgs}")
         with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
-            f.write(res)
+            f.write("\n".join(res) if res else "ok")
     finally:
         dist.destroy_process_group()
 

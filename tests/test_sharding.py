@@ -298,3 +298,51 @@ def test_decoder_default_exchange_without_rccl():
     assert ShardedDecoder(_Shard(), 16, 0).reduce == "max_u8"
     with pytest.raises(ValueError):
         ShardedDecoder(_Shard(), 16, 0, reduce="ring")
+
+
+def test_auto_exchange_needs_one_host(monkeypatch):
+    """"auto" picks the peer exchange (hipIpc mappings) only when every
+    rank of an RCCL group runs on ONE host; ranks on two nodes, or another
+    backend, fall back to max_u8 (ShardedDecoder) / sparse (ShardedIndex)."""
+    import torch.distributed as dist
+
+    import fmidx.sharding as S
+
+    class _Shard:
+        device = 0
+
+    hosts = {"ids": ["a/boot", "a/boot"]}
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    monkeypatch.setattr(dist, "get_world_size", lambda g=None: 2)
+
+    def gather(out, obj, group=None):
+        out[:] = hosts["ids"]
+
+    monkeypatch.setattr(dist, "all_gather_object", gather)
+    g = object()
+    assert S.peer_capable(g)
+    assert S.ShardedDecoder(_Shard(), 16, 0, group=g).reduce == "peer"
+    assert S.ShardedIndex(_Shard(), [], group=g).exchange == "peer"
+    hosts["ids"] = ["a/boot", "b/boot"]                     # two nodes
+    assert not S.peer_capable(g)
+    assert S.ShardedDecoder(_Shard(), 16, 0, group=g).reduce == "max_u8"
+    assert S.ShardedIndex(_Shard(), [], group=g).exchange == "sparse"
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "gloo")
+    hosts["ids"] = ["a/boot", "a/boot"]
+    assert not S.peer_capable(g)
+    assert S.ShardedIndex(_Shard(), [], group=None).exchange == "sparse"
+    assert isinstance(S.host_identity(), str)
+
+
+def test_decoder_check_modes():
+    """check="sync" (the default: a flag-barrier step raises at the step that timed
+    out) or "deferred" (the opt-in of the previous behaviour); nothing else."""
+    from fmidx.sharding import ShardedDecoder
+
+    class _Shard:
+        pass
+
+    assert ShardedDecoder(_Shard(), 16, 0).check == "sync"
+    assert ShardedDecoder(_Shard(), 16, 0, check="deferred").check == "deferred"
+    with pytest.raises(ValueError):
+        ShardedDecoder(_Shard(), 16, 0, check="never")
