@@ -1474,7 +1474,18 @@ int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint6
   FM_API_BEGIN
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
-  return fmidx::launch_shard_pack(h->idx.view, d_lo, d_hi, B, d_bits, ldw, vocab, d_payload, cap_words,
+  return fmidx::launch_shard_pack(h->idx.view, d_lo, d_hi, B, d_bits, ldw, vocab, nullptr, d_payload, cap_words,
+                                  reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_shard_pack_facts(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
+                        uint64_t ldw, uint64_t vocab, const int32_t* d_facts, uint32_t* d_payload, uint64_t cap_words,
+                        void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  return fmidx::launch_shard_pack(h->idx.view, d_lo, d_hi, B, d_bits, ldw, vocab, d_facts, d_payload, cap_words,
                                   reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
@@ -1482,7 +1493,16 @@ int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint6
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
                      int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
   FM_API_BEGIN
-  return fmidx::launch_shard_or_rows(d_parts, nparts, part_stride, B, vocab, shift, d_out, ld_out, unpack,
+  return fmidx::launch_shard_or_rows(d_parts, nparts, part_stride, B, vocab, shift, d_out, ld_out, unpack, nullptr,
+                                     reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_shard_or_rows_facts(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
+                           int64_t shift, void* d_out, uint64_t ld_out, int unpack, int32_t* d_facts_out,
+                           void* stream) {
+  FM_API_BEGIN
+  return fmidx::launch_shard_or_rows(d_parts, nparts, part_stride, B, vocab, shift, d_out, ld_out, unpack, d_facts_out,
                                      reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
@@ -1491,7 +1511,7 @@ int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_
                            uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream) {
   FM_API_BEGIN
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
-                                           nullptr, nullptr, 0, nullptr, reinterpret_cast<hipStream_t>(stream));
+                                           nullptr, nullptr, 0, nullptr, nullptr, reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 
@@ -1505,7 +1525,18 @@ int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, ui
     return -1;
   }
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
-                                           d_flags, d_step, spins, err, reinterpret_cast<hipStream_t>(stream));
+                                           d_flags, d_step, spins, err, nullptr, reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_shard_or_rows_peers_facts(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
+                                 const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,
+                                 int32_t* d_facts_out, void* stream) {
+  FM_API_BEGIN
+  return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
+                                           d_flags, d_step, spins, err, d_facts_out,
+                                           reinterpret_cast<hipStream_t>(stream));
   FM_API_END
 }
 

@@ -617,7 +617,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     const uint64_t W4 = ((uint64_t)Wd + 3) & ~3ull;
     const bool sparse = lo >= hi || (hi - lo < Wd && plan.nb == 0);   // workgroup-uniform
     if (threadIdx.x == 0) {
-      const uint64_t H = 4 + ((2 * m + 3) & ~3ull);
+      const uint64_t H = payload_header_words(m);
       sys_store(&pay[4 + row], sparse ? (uint32_t)(lo < hi ? hi - lo : 0) : (Wd | 0x80000000u));
       sys_store(&pay[4 + m + row], (uint32_t)(H + row * W4));
       if (row == 0) {
@@ -986,7 +986,7 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
                           uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, uint32_t* pay_alt,
                           const uint32_t* pay_sel, hipStream_t s) {
   if (m == 0) return 0;
-  const uint64_t W = (vocab + 31) / 32, W4 = (W + 3) & ~3ull, H = 4 + ((2 * m + 3) & ~3ull);
+  const uint64_t W = (vocab + 31) / 32, W4 = (W + 3) & ~3ull, H = payload_header_words(m);
   if (!pay || !tok || !lo_in || !hi_in || !lo_out || !hi_out || vocab == 0 || W > kPayMaxWords ||
       m >= (1ull << 31) || (reinterpret_cast<uintptr_t>(pay) & 15) || (pay_sel && !pay_alt) ||
       (reinterpret_cast<uintptr_t>(pay_alt) & 15)) {

@@ -830,14 +830,22 @@ int launch_distinct_csr(const uint64_t* k, const uint64_t* cap_off, const uint64
                         uint64_t m, uint64_t* off, uint64_t* pairs, hipStream_t s);
 
 // shard.hip: OR of the shards' packed allowed rows (+ expansion to uint8)
+// The exchange payload's header (uint32 words): [0] total words [1] B [2] W [3] magic, desc[B] and
+// off[B] from word 4 (padded to 4 words), then the processors' facts area -- facts[k * B + b], k = 0..2
+// (count([last]) > 0, range non-empty, distinct non-empty: 0/1; zeros when the payload carries none)
+// -- padded to 4 words; row data after it.
+__host__ __device__ __forceinline__ uint64_t payload_facts_at(uint64_t B) { return 4 + ((2 * B + 3) & ~3ull); }
+__host__ __device__ __forceinline__ uint64_t payload_header_words(uint64_t B) {
+  return payload_facts_at(B) + ((3 * B + 3) & ~3ull);
+}
 uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab);
 int launch_shard_pack(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t B, const uint32_t* bits,
-                      uint64_t ldw, uint64_t vocab, uint32_t* pay, uint64_t cap, hipStream_t s);
+                      uint64_t ldw, uint64_t vocab, const int32_t* facts, uint32_t* pay, uint64_t cap, hipStream_t s);
 int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride, uint64_t B, uint64_t vocab,
-                         int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s);
+                         int64_t shift, void* out, uint64_t ld, int unpack, int32_t* facts_out, hipStream_t s);
 int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
                                int64_t shift, void* out, uint64_t ld, int unpack, const uint32_t* flags,
-                               const uint32_t* ctr, uint32_t spins, uint32_t* err, hipStream_t s);
+                               const uint32_t* ctr, uint32_t spins, uint32_t* err, int32_t* facts_out, hipStream_t s);
 int launch_peer_signal(const uint64_t* dst, uint64_t world, uint32_t* ctr, hipStream_t s);
 int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t wpr,
                    uint64_t vocab, void* out, uint64_t ld_out, int unpack, hipStream_t s);

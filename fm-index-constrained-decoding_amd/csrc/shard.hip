@@ -203,6 +203,10 @@ int launch_or_bits(const uint32_t* parts, uint64_t nparts, uint64_t part_stride,
 //   [0] total words (a multiple of 4)   [1] B   [2] words per bitmap row W   [3] kPayloadMagic
 //   [4, 4 + B)        desc[b] = count | (dense << 31)
 //   [4 + B, 4 + 2B)   off[b]  = word offset of row b's data in this payload
+//   [F, F + 3B)       facts[k * B + b], F = payload_facts_at(B): a processor call's per-row facts
+//                     (k_prep over the shard: count([last]) > 0, range non-empty, distinct non-empty),
+//                     ORed by the OR pass -- so a sharded processor call needs no collective for them
+//                     (zeros when the payload carries none)
 //   data: row b's `count` words at off[b] (zero-padded to a multiple of 4):
 //         dense  -- the W words of its allowed-token bitmap (the decode step's packed row)
 //         sparse -- BWT[lo, hi) of the shard (T' symbols; token = symbol - shift when in [0, V)),
@@ -213,7 +217,6 @@ namespace {
 
 constexpr uint32_t kPayloadMagic = 0x58534D46u;   // "FMSX"
 
-__host__ __device__ __forceinline__ uint64_t payload_header_words(uint64_t B) { return 4 + ((2 * B + 3) & ~3ull); }
 
 // One workgroup per row, one launch: the workgroup sums the padded sizes of
 // the rows before its own (every thread loads a few (lo, hi) pairs -- B * 16
@@ -242,7 +245,8 @@ __device__ __forceinline__ void pay_store(uint32_t* p, uint32_t x) {
 __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint64_t* __restrict__ lo,
                                                           const uint64_t* __restrict__ hi,
                                                           const uint32_t* __restrict__ bits, uint64_t ldw,
-                                                          uint64_t B, uint32_t W, uint32_t* __restrict__ pay) {
+                                                          uint64_t B, uint32_t W, const int32_t* __restrict__ facts,
+                                                          uint32_t* __restrict__ pay) {
   __shared__ uint64_t s_part[kPackRowThreads / 64];
   const uint64_t b = blockIdx.x;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -278,6 +282,10 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
   uint64_t off = H;
 #pragma unroll
   for (int k = 0; k < kPackRowThreads / 64; ++k) off += s_part[k];
+  if (t < 3) {   // the row's facts (ORed by the readers' OR pass), zeros without any
+    const uint64_t F = payload_facts_at(B);
+    pay_store(&pay[F + t * B + b], facts ? (uint32_t)(facts[t * B + b] != 0) : 0u);
+  }
   if (t == 0) {
     pay_store(&pay[4 + b], desc);
     pay_store(&pay[4 + B + b], (uint32_t)off);
@@ -288,8 +296,11 @@ __global__ void __launch_bounds__(kPackRowThreads) k_pack(DevView v, const uint6
       pay_store(&pay[3], kPayloadMagic);
     }
   }
-  if (b == 0)
-    for (uint64_t i = 4 + 2 * B + t; i < H; i += kPackRowThreads) pay_store(&pay[i], 0u);
+  if (b == 0) {   // the paddings of the desc / off words and of the facts area
+    const uint64_t F = payload_facts_at(B);
+    for (uint64_t i = 4 + 2 * B + t; i < F; i += kPackRowThreads) pay_store(&pay[i], 0u);
+    for (uint64_t i = F + 3 * B + t; i < H; i += kPackRowThreads) pay_store(&pay[i], 0u);
+  }
   const uint32_t count = desc & 0x7FFFFFFFu;
   const bool dense = (desc >> 31) != 0;
   const uint64_t s0 = min(l0, v.n - 1);
@@ -383,7 +394,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
                                                             int unpack, const uint32_t* __restrict__ flags,
                                                             const uint32_t* __restrict__ ctr, uint32_t spins,
-                                                            uint32_t* __restrict__ err) {
+                                                            uint32_t* __restrict__ err, int32_t* __restrict__ facts_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // [round4(W)]
   // per part: its sparse count (0 for dense parts), data offset, and first 16-B slot in the
   // flat space of every sparse list padded to a multiple of 4 words
@@ -426,14 +437,26 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     // whose data lies past the part's end (a gather shorter than the payload: the speculative
     // all_gather of SparseExchange, redone in full when it was too short) is read as empty --
     // never beyond the part
-    uint32_t d = 0, o = 0;
+    uint32_t d = 0, o = 0, f[3] = {0u, 0u, 0u};
     const uint32_t* pp = nullptr;
+    const uint64_t F = payload_facts_at(B);
     if (t < nparts) {
       pp = PEERS ? reinterpret_cast<const uint32_t*>(tab[t]) : parts + (uint64_t)t * stride;
       d = part_word<PEERS>(pp, 4 + b);
       o = part_word<PEERS>(pp, 4 + B + b);
+      if (facts_out) {   // the row's facts, in the same round trip (the header is within every part)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) f[k] = part_word<PEERS>(pp, F + (uint64_t)k * B + b);
+      }
       const uint64_t end = (uint64_t)o + (((d & 0x7FFFFFFFu) + 3u) & ~3u);
-      if (!(o >= 4 + 2 * B && end <= stride)) d = o = 0;
+      if (!(o >= payload_header_words(B) && end <= stride)) d = o = 0;
+    }
+    if (facts_out) {   // OR over the parts: some shard has it
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const bool any = __ballot(t < nparts && f[k] != 0) != 0;
+        if (t == 0) facts_out[(uint64_t)k * B + b] = any ? 1 : 0;
+      }
     }
     const bool dense = (d >> 31) != 0;
     const uint32_t q = dense ? 0u : (d + 3u) >> 2;
@@ -629,7 +652,7 @@ uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab) {
 }
 
 int launch_shard_pack(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t B, const uint32_t* bits,
-                      uint64_t ldw, uint64_t vocab, uint32_t* pay, uint64_t cap, hipStream_t s) {
+                      uint64_t ldw, uint64_t vocab, const int32_t* facts, uint32_t* pay, uint64_t cap, hipStream_t s) {
   const uint64_t W = (vocab + 31) / 32;
   if (!lo || !hi || !pay || (B && !bits) || ldw < W || B >= (1ull << 31) ||
       W > (uint64_t)kOrRowMaxWords) {
@@ -642,13 +665,13 @@ int launch_shard_pack(const DevView& v, const uint64_t* lo, const uint64_t* hi, 
               (unsigned long long)shard_payload_capacity(B, vocab));
     return -1;
   }
-  k_pack<<<(unsigned)(B ? B : 1), kPackRowThreads, 0, s>>>(v, lo, hi, bits, ldw, B, (uint32_t)W, pay);
+  k_pack<<<(unsigned)(B ? B : 1), kPackRowThreads, 0, s>>>(v, lo, hi, bits, ldw, B, (uint32_t)W, facts, pay);
   FM_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride, uint64_t B, uint64_t vocab,
-                         int64_t shift, void* out, uint64_t ld, int unpack, hipStream_t s) {
+                         int64_t shift, void* out, uint64_t ld, int unpack, int32_t* facts_out, hipStream_t s) {
   const uint64_t W = (vocab + 31) / 32;
   if (!parts || !out || !nparts || nparts > (uint64_t)kOrMaxParts || W > (uint64_t)kOrRowMaxWords ||
       stride < payload_header_words(B) ||
@@ -666,17 +689,20 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
   }
   if (or_per_part())
     k_or_rows<false, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr);
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr,
+        facts_out);
   else
     k_or_rows<false, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr);
+        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr,
+        facts_out);
   FM_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t cap, uint64_t B, uint64_t vocab,
                                int64_t shift, void* out, uint64_t ld, int unpack, const uint32_t* flags,
-                               const uint32_t* ctr, uint32_t spins, uint32_t* err, hipStream_t s) {
+                               const uint32_t* ctr, uint32_t spins, uint32_t* err, int32_t* facts_out,
+                               hipStream_t s) {
   const uint64_t W = (vocab + 31) / 32;
   if (!ptrs || !out || !nparts || nparts > (uint64_t)kOrMaxParts || W > (uint64_t)kOrRowMaxWords ||
       cap < shard_payload_capacity(B, vocab) || cap >= (1ull << 30) ||
@@ -694,10 +720,12 @@ int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t c
   if (!spins) spins = kFlagSpins;
   if (or_per_part())
     k_or_rows<true, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err);
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err,
+        facts_out);
   else
     k_or_rows<true, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err);
+        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err,
+        facts_out);
   FM_HIP(hipGetLastError());
   return 0;
 }

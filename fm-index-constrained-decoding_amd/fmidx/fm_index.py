@@ -403,17 +403,27 @@ class FMIndex:
                                            c_void_p(_stream_of(lo))), "decode_step_payload")
         return payload
 
-    def shard_pack(self, lo, hi, bits, vocab: int, payload=None):
+    def shard_pack(self, lo, hi, bits, vocab: int, payload=None, facts=None):
         """The sparse exchange payload of this shard's rows (fm_shard_pack):
         per row its BWT slice when narrower than a bitmap, else its packed
         allowed-bit row from ``bits`` (int32 [B, >= ceil(vocab/32)], the
-        decode step's packed output).  Returns the int32 payload tensor
-        (capacity for the worst case; word 0 = words used)."""
+        decode step's packed output).  ``facts`` (int32 [3, B], a processor
+        call's per-row facts): stored in the payload's facts area
+        (fm_shard_pack_facts), for the OR pass to OR.  Returns the int32
+        payload tensor (capacity for the worst case; word 0 = words used)."""
         import torch
 
         B = lo.numel()
         if payload is None or payload.numel() < payload_capacity(B, vocab):   # the batch may have grown
             payload = torch.empty(payload_capacity(B, vocab), dtype=torch.int32, device=lo.device)
+        if facts is not None:
+            if not (facts.dtype == torch.int32 and facts.is_contiguous() and facts.numel() == 3 * B):
+                raise ValueError(f"shard_pack: facts must be a contiguous int32 [3, {B}] tensor")
+            check(lib().fm_shard_pack_facts(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), B,
+                                            c_void_p(bits.data_ptr()), bits.stride(0), int(vocab),
+                                            c_void_p(facts.data_ptr()), c_void_p(payload.data_ptr()),
+                                            payload.numel(), c_void_p(_stream_of(lo))), "shard_pack_facts")
+            return payload
         check(lib().fm_shard_pack(self._h, c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), B,
                                   c_void_p(bits.data_ptr()), bits.stride(0), int(vocab), c_void_p(payload.data_ptr()),
                                   payload.numel(), c_void_p(_stream_of(lo))), "shard_pack")

@@ -411,7 +411,14 @@ class _ShardedDeviceStep(_DeviceStep):
         h = self.prep(input_ids, scores, cfg)
         if h is None:
             return None
-        # the peer exchange packs first: the facts all_reduce is then its barrier
+        if getattr(self.sidx, "facts_in_payload", False) and self.sidx.group is not None:
+            # sparse / peer exchanges: the facts ride in the payload and the OR pass ORs them (> 0 is
+            # all k_prep_finish asks of a sum) -- no collective for them; over the peer exchange with
+            # the flag barrier the call holds no collective at all
+            bits, facts = self.sidx.or_bits(h["mlo"], h["mhi"], h["bits"], h["V"], facts=h["facts"])
+            return self.finish(h, facts, bits)
+        # the dense exchange (or no group): the peer exchange would pack first so that the facts
+        # all_reduce is its barrier
         staged = self.sidx.stage(h["mlo"], h["mhi"], h["bits"], h["V"])
         facts = self.sidx.sum_facts(h["facts"])
         bits = self.sidx.or_bits(h["mlo"], h["mhi"], h["bits"], h["V"], staged=staged)

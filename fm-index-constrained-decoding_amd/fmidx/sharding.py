@@ -148,7 +148,7 @@ class ShardedDecoder:
 
     def __init__(self, index, vocab: int, shift: int = 10, group=None, reduce: str = "auto",
                  halo: Optional[int] = None, peer_barrier: str = "flags", graph: bool = False,
-                 spins: Optional[int] = None, check: str = "sync"):
+                 spins: Optional[int] = None, check: str = "sync", unpack: bool = True):
         """reduce: "auto" (the default: "peer" with the flag barrier -- the fastest exact exchange,
         bench.py's sharded leg -- over an RCCL group of more than one rank whose ranks all run on
         one host (the IPC mappings do not cross nodes; same_host()); "max_u8" otherwise), "max_u8"
@@ -169,7 +169,11 @@ class ShardedDecoder:
         close()), so the step that timed out has already handed back a mask
         that may be inexact (one stale mask at most) -- for callers that
         overlap the next step's host work with this step's GPU work and accept
-        that contract."""
+        that contract.
+        ``unpack`` (the "peer" and "sparse" exchanges): False makes ``step``
+        return the ORed rows as packed int32 words [B, ceil(V/32)] (bit t of a
+        row = token t) instead of the uint8 [B, V] mask -- what the processors'
+        epilogue consumes -- so the OR pass writes V/8 bytes per row, not V."""
         self.index = index
         self.vocab = vocab
         self.shift = shift
@@ -180,6 +184,9 @@ class ShardedDecoder:
             raise ValueError(reduce)
         if check not in ("sync", "deferred"):
             raise ValueError(check)
+        if not unpack and reduce not in ("peer", "sparse"):
+            raise ValueError("unpack=False: the peer and sparse exchanges only")
+        self.unpack = unpack
         self.check = check
         self._ev = None        # the event a checked flag-barrier step waits on
         if graph and not (reduce == "peer" and peer_barrier == "flags"):
@@ -284,15 +291,16 @@ class ShardedDecoder:
             self._peer = PeerExchange(self.group, B, self.vocab, self.lo.device, barrier=self.peer_barrier,
                                       spins=self.spins)
             self._g = None
-        self._peer.check()                 # a timed-out step before this one: raise, return no mask
-        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != self.lo.device:
-            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=self.lo.device)
+        self._peer.check()                 # a timed-out step before this one (check="deferred"): raise
+        if self._out_stale(B, self.lo.device):
+            self._out = self._new_out(B, self.lo.device)
             self._g = None
         if self.peer_barrier == "flags":
             px = self._peer
 
             def launch(tok):
-                px.flags_step(self.index, tok, self.lo, self.hi, self.vocab, self.shift, self._out)
+                px.flags_step(self.index, tok, self.lo, self.hi, self.vocab, self.shift, self._out,
+                              unpack=self.unpack)
 
             if not self.graph:
                 launch(tokens)
@@ -317,7 +325,18 @@ class ShardedDecoder:
                                        reset_below=0)
         self.lo, self._lo2 = self._lo2, self.lo
         self.hi, self._hi2 = self._hi2, self.hi
-        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out))
+        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out, unpack=self.unpack))
+
+    def _out_shape(self, B: int):
+        return (B, self.vocab) if self.unpack else (B, (self.vocab + 31) // 32)
+
+    def _out_stale(self, B: int, device) -> bool:
+        return self._out is None or tuple(self._out.shape) != self._out_shape(B) or self._out.device != device
+
+    def _new_out(self, B: int, device):
+        import torch
+
+        return torch.empty(self._out_shape(B), dtype=torch.uint8 if self.unpack else torch.int32, device=device)
 
     def _combine_peer(self, bits):
         import torch
@@ -330,9 +349,9 @@ class ShardedDecoder:
         self._peer.check()
         pay = self._peer.payload()
         self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=pay)
-        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != pay.device:
-            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=pay.device)
-        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out))
+        if self._out_stale(B, pay.device):
+            self._out = self._new_out(B, pay.device)
+        return self._checked(self._peer(pay, B, self.vocab, self.shift, out=self._out, unpack=self.unpack))
 
     def _checked(self, out):
         """Exact or absent: with the flag barrier and check="sync", wait for the
@@ -365,12 +384,13 @@ class ShardedDecoder:
 
         self._payload = self.index.shard_pack(self.lo, self.hi, bits, self.vocab, payload=self._payload)
         B = self.lo.numel()
-        if self._out is None or self._out.shape != (B, self.vocab) or self._out.device != self._payload.device:
-            self._out = torch.empty((B, self.vocab), dtype=torch.uint8, device=self._payload.device)
+        if self._payload.is_cuda and self._out_stale(B, self._payload.device):
+            self._out = self._new_out(B, self._payload.device)
         if self._xchg is None:
             self._xchg = SparseExchange(self.group)
             self.exchange_words = self._xchg.words
-        return self._xchg(self._payload, B, self.vocab, self.shift, out=self._out)
+        return self._xchg(self._payload, B, self.vocab, self.shift, out=self._out if self._payload.is_cuda else None,
+                          unpack=self.unpack)
 
     def local_mask(self):
         return self.index.allowed_mask(self.lo, self.hi, self.vocab, self.shift)
@@ -481,9 +501,18 @@ class ShardedIndex:
             dist.all_reduce(facts, op=dist.ReduceOp.SUM, group=self.group)
         return facts
 
-    def stage(self, lo, hi, bits, vocab: int) -> bool:
-        """The peer exchange's pack, issued before the facts all_reduce so that
-        it is the exchange's barrier.  True when staged that way."""
+    @property
+    def facts_in_payload(self) -> bool:
+        """True when a processor call's facts travel in the exchange's payload
+        (sparse and peer exchanges: ORed by the OR pass, no collective for
+        them); the dense exchange sums them with an all_reduce."""
+        return self.exchange in ("sparse", "peer")
+
+    def stage(self, lo, hi, bits, vocab: int, facts=None) -> bool:
+        """The peer exchange's pack (with the call's facts in the payload when
+        given).  Without ``facts`` it is issued before the facts all_reduce, so
+        that that collective is the exchange's barrier: True when staged that
+        way."""
         if self.group is None or self.exchange != "peer":
             return False
         B = lo.numel()
@@ -491,9 +520,9 @@ class ShardedIndex:
             self.close()
             self._peer = PeerExchange(self.group, B, vocab, lo.device, barrier=self.peer_barrier, spins=self.spins)
         self._peer.check()
-        self.shard.shard_pack(lo, hi, bits, vocab, payload=self._peer.payload())
+        self.shard.shard_pack(lo, hi, bits, vocab, payload=self._peer.payload(), facts=facts)
         self._staged = True
-        return self.peer_barrier == "collective"
+        return facts is None and self.peer_barrier == "collective"
 
     def check_exchange(self):
         """Raise PeerBarrierTimeout if a peer-exchange step has timed out (no
@@ -509,27 +538,37 @@ class ShardedIndex:
             px, self._peer = self._peer, None
             px.close()
 
-    def or_bits(self, lo, hi, bits, vocab: int, staged: bool = False):
+    def or_bits(self, lo, hi, bits, vocab: int, staged: bool = False, facts=None):
         """OR of every rank's packed allowed bits (int32 [B, W]) -> int32 [B, W].
         ``staged``: stage() packed this step's payload before a collective
-        every rank issued after it (the peer exchange's barrier)."""
+        every rank issued after it (the peer exchange's barrier).  ``facts``
+        (int32 [3, B], sparse / peer exchanges): the call's facts ride in the
+        payload (stage() packed them when it ran) and their OR over the ranks
+        is returned too -> (words, facts_or)."""
         if self.group is None:
-            return bits
+            return bits if facts is None else (bits, (facts != 0).to(facts.dtype))
         import torch
         import torch.distributed as dist
 
         B, W = lo.numel(), (vocab + 31) // 32
+        fo = None
+        if facts is not None:
+            if not self.facts_in_payload:
+                raise ValueError("or_bits: the dense exchange does not carry facts (sum_facts)")
+            fo = torch.empty((3, B), dtype=torch.int32, device=lo.device)
         if self.exchange == "peer":
             if not self._staged:
-                self.stage(lo, hi, bits, vocab)
+                self.stage(lo, hi, bits, vocab, facts=facts)
                 staged = False          # packed just now: no collective has run since
             self._staged = False
-            return self._peer(self._peer.payload(), B, vocab, self.shift, unpack=False, barrier_done=staged)
+            w = self._peer(self._peer.payload(), B, vocab, self.shift, unpack=False, barrier_done=staged, facts_out=fo)
+            return w if fo is None else (w, fo)
         if self.exchange == "sparse":
-            self._payload = self.shard.shard_pack(lo, hi, bits, vocab, payload=self._payload)
+            self._payload = self.shard.shard_pack(lo, hi, bits, vocab, payload=self._payload, facts=facts)
             if self._xchg is None:
                 self._xchg = SparseExchange(self.group)
-            return self._xchg(self._payload, B, vocab, self.shift, unpack=False)
+            w = self._xchg(self._payload, B, vocab, self.shift, unpack=False, facts_out=fo)
+            return w if fo is None else (w, fo)
         world = dist.get_world_size(self.group)
         mine = bits[:, :W].contiguous()
         if self._parts is None or self._parts.shape != (world, B, W):
@@ -588,9 +627,15 @@ class ShardedIndex:
         return self.shard.size()
 
 
-def payload_header_words(B: int) -> int:
-    """Words of a payload's header (csrc/shard.hip: 4 + 2B rounded to 4)."""
+def payload_facts_at(B: int) -> int:
+    """Word offset of a payload's facts area (after [4 words] desc[B] off[B], padded to 4)."""
     return 4 + ((2 * B + 3) & ~3)
+
+
+def payload_header_words(B: int) -> int:
+    """Words of a payload's header (csrc/fmidx_internal.h payload_header_words): the
+    descriptors, then the facts area (3B words, padded to 4)."""
+    return payload_facts_at(B) + ((3 * B + 3) & ~3)
 
 
 def payload_capacity(B: int, vocab: int) -> int:
@@ -633,7 +678,7 @@ class SparseExchange:
         dist.all_gather_into_tensor(parts, mine.contiguous(), group=self.group)
         return parts.view(world, m)
 
-    def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+    def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True, facts_out=None):
         import torch
         import torch.distributed as dist
 
@@ -649,7 +694,7 @@ class SparseExchange:
             # nor below its header
             guess = min(payload_capacity(B, vocab),
                         max(payload_header_words(B), (int(max(self._max) * self.slack) + 3) & ~3))
-            res = or_payloads(self._gather(payload, guess), B, vocab, shift, out=out, unpack=unpack)
+            res = or_payloads(self._gather(payload, guess), B, vocab, shift, out=out, unpack=unpack, facts_out=facts_out)
         words = [int(x) for x in sizes.tolist()]
         m = max(words)
         self.words.append(words)
@@ -658,7 +703,7 @@ class SparseExchange:
             return res
         if guess:
             self.respecified += 1
-        return or_payloads(self._gather(payload, m), B, vocab, shift, out=out, unpack=unpack)
+        return or_payloads(self._gather(payload, m), B, vocab, shift, out=out, unpack=unpack, facts_out=facts_out)
 
 
 class PeerBarrierTimeout(RuntimeError):
@@ -823,14 +868,15 @@ class PeerExchange:
         self.signal()
         return self.or_flags(B, vocab, shift, out=out, unpack=unpack)
 
-    def or_flags(self, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+    def or_flags(self, B: int, vocab: int, shift: int, out=None, unpack: bool = True, facts_out=None):
         """The flag barrier's OR pass of the step the counter names (its payload
         buffer by the counter's parity)."""
         return or_peer_payloads(self.ptab, self.cap, B, vocab, shift, out=out, unpack=unpack,
-                                flags=(self.flags, self.ctr, self._err_ptr, self.spins), buffers=2)
+                                flags=(self.flags, self.ctr, self._err_ptr, self.spins), buffers=2,
+                                facts_out=facts_out)
 
     def __call__(self, payload, B: int, vocab: int, shift: int, out=None, unpack: bool = True,
-                 barrier_done: bool = False):
+                 barrier_done: bool = False, facts_out=None):
         self.check()
         k = self.step % 2
         if payload.data_ptr() != self.bufs[k].data_ptr():
@@ -839,11 +885,12 @@ class PeerExchange:
             raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
         if self.barrier_mode == "flags":
             self.signal()
-            out = self.or_flags(B, vocab, shift, out=out, unpack=unpack)
+            out = self.or_flags(B, vocab, shift, out=out, unpack=unpack, facts_out=facts_out)
         else:
             if not barrier_done:
                 self.barrier()
-            out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack)
+            out = or_peer_payloads(self.ptab[k], self.cap, B, vocab, shift, out=out, unpack=unpack,
+                                   facts_out=facts_out)
         self.step += 1
         return out
 
@@ -887,14 +934,16 @@ class PeerExchange:
 
 
 def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, unpack: bool = True, flags=None,
-                     buffers: int = 1):
+                     buffers: int = 1, facts_out=None):
     """OR of the payloads at the device addresses ``ptrs`` (int64 [P], on the
     GPU that runs the pass; each payload ``cap`` words, in this process or a
     peer's buffer mapped by fm_ipc_open) -> uint8 [B, vocab] (unpack) or int32
     [B, ceil(vocab/32)] words (fm_shard_or_rows_peers).  ``flags`` = (flag
     words int32 [>= P], the step counter int32 [1], the error word's address,
     spins): the flag barrier first (fm_shard_or_rows_peers_wait); ``ptrs`` is
-    then [2, P], the double buffer's two address rows (``buffers`` = 2)."""
+    then [2, P], the double buffer's two address rows (``buffers`` = 2).
+    ``facts_out`` (int32 [3, B]): the OR of the payloads' facts areas
+    (fm_shard_or_rows_peers_facts)."""
     import torch
     from ctypes import c_void_p
 
@@ -912,6 +961,17 @@ def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, u
     assert out.stride(1) == 1 and out.device == ptrs.device
     ld = out.stride(0) * out.element_size()
     stream = torch._C._cuda_getCurrentRawStream(ptrs.device.index)
+    if facts_out is not None:
+        _check_facts(facts_out, B, ptrs.device)
+        fw, ctr, err_ptr, spins = flags if flags is not None else (None, None, None, 0)
+        if fw is not None and fw.numel() < nparts:
+            raise ValueError("flag words: one per part")
+        check(lib().fm_shard_or_rows_peers_facts(
+            c_void_p(ptrs.data_ptr()), nparts, int(cap), B, vocab, int(shift), c_void_p(out.data_ptr()), ld,
+            1 if unpack else 0, c_void_p(fw.data_ptr()) if fw is not None else None,
+            c_void_p(ctr.data_ptr()) if ctr is not None else None, int(spins), c_void_p(err_ptr) if err_ptr else None,
+            c_void_p(facts_out.data_ptr()), c_void_p(stream)), "shard_or_rows_peers_facts")
+        return out
     if flags is not None:
         fw, ctr, err_ptr, spins = flags
         if fw.numel() < nparts:
@@ -927,18 +987,19 @@ def or_peer_payloads(ptrs, cap: int, B: int, vocab: int, shift: int, out=None, u
     return out
 
 
-def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = True):
+def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = True, facts_out=None):
     """OR of the ranks' sparse-exchange payloads ``parts`` (int32 [P, stride])
     -> uint8 [B, vocab] (unpack) or int32 [B, ceil(vocab/32)] words.  GPU:
-    fm_shard_or_rows; CPU tensors (gloo tests): the same format read with
-    torch ops (or_payloads_host)."""
+    fm_shard_or_rows(_facts); CPU tensors (gloo tests): the same format read
+    with torch ops (or_payloads_host).  ``facts_out`` (int32 [3, B]): the OR of
+    the payloads' facts areas."""
     import torch
     from ctypes import c_void_p
 
     from ._lib import check, lib
 
     if not parts.is_cuda:
-        return or_payloads_host(parts, B, vocab, shift, unpack=unpack)
+        return or_payloads_host(parts, B, vocab, shift, unpack=unpack, facts_out=facts_out)
     P, stride = parts.shape
     W = (vocab + 31) // 32
     if out is None:
@@ -947,25 +1008,39 @@ def or_payloads(parts, B: int, vocab: int, shift: int, out=None, unpack: bool = 
     assert parts.dtype == torch.int32 and parts.is_contiguous() and out.stride(1) == 1
     ld = out.stride(0) * out.element_size()
     stream = torch._C._cuda_getCurrentRawStream(parts.device.index)
+    if facts_out is not None:
+        _check_facts(facts_out, B, parts.device)
+        check(lib().fm_shard_or_rows_facts(c_void_p(parts.data_ptr()), P, stride, B, vocab, int(shift),
+                                           c_void_p(out.data_ptr()), ld, 1 if unpack else 0,
+                                           c_void_p(facts_out.data_ptr()), c_void_p(stream)), "shard_or_rows_facts")
+        return out
     check(lib().fm_shard_or_rows(c_void_p(parts.data_ptr()), P, stride, B, vocab, int(shift), c_void_p(out.data_ptr()),
                                  ld, 1 if unpack else 0, c_void_p(stream)), "shard_or_rows")
     return out
 
 
+def _check_facts(f, B: int, device):
+    import torch
+
+    if not (f.dtype == torch.int32 and f.is_contiguous() and f.numel() == 3 * B and f.device == device):
+        raise ValueError(f"facts: a contiguous int32 [3, {B}] tensor on {device}")
+
+
 _PAYLOAD_MAGIC = 0x58534D46
 
 
-def pack_payload_host(lo, hi, bwt, bits_words, vocab: int):
+def pack_payload_host(lo, hi, bwt, bits_words, vocab: int, facts=None):
     """The sparse-exchange payload (csrc/shard.hip's layout) built on the host
     from a shard's BWT (int array) and its packed rows (int32 [B, >= W]) --
-    for CPU indexes (gloo tests); the GPU path is fm_shard_pack."""
+    for CPU indexes (gloo tests); the GPU path is fm_shard_pack(_facts).
+    ``facts``: int [3, B] for the facts area (zeros without)."""
     import torch
 
     lo = np.asarray(lo, dtype=np.int64)
     hi = np.minimum(np.asarray(hi, dtype=np.int64), len(bwt))
     B = lo.size
     W = (vocab + 31) // 32
-    H = 4 + ((2 * B + 3) & ~3)
+    H = payload_header_words(B)
     bw = np.asarray(bits_words, dtype=np.int64).astype(np.uint32)
     desc, off, data = np.zeros(B, dtype=np.uint32), np.zeros(B, dtype=np.uint32), []
     at = H
@@ -982,17 +1057,25 @@ def pack_payload_host(lo, hi, bwt, bits_words, vocab: int):
     head[:4] = [at, B, W, _PAYLOAD_MAGIC]
     head[4:4 + B] = desc
     head[4 + B:4 + 2 * B] = off
+    if facts is not None:
+        F = payload_facts_at(B)
+        head[F:F + 3 * B] = (np.asarray(facts).reshape(3, B) != 0).astype(np.uint32).reshape(-1)
     out = np.concatenate([head] + data)
     return torch.from_numpy(out.view(np.int32).copy())
 
 
-def or_payloads_host(parts, B: int, vocab: int, shift: int, unpack: bool = True):
+def or_payloads_host(parts, B: int, vocab: int, shift: int, unpack: bool = True, facts_out=None):
+    """The OR pass on the host (gloo tests).  ``facts_out`` (a torch int32 [3, B]
+    tensor): the OR over the parts of their facts areas is written into it."""
     import torch
 
     W = (vocab + 31) // 32
     bits = np.zeros((B, W * 32), dtype=np.uint8)
+    F = payload_facts_at(B)
+    fo = np.zeros((3, B), dtype=np.int32)
     for p in parts.cpu().numpy().view(np.uint32):
         assert int(p[3]) == _PAYLOAD_MAGIC and int(p[1]) == B and int(p[2]) == W
+        fo |= (p[F:F + 3 * B].reshape(3, B) != 0).astype(np.int32)
         for b in range(B):
             d, o = int(p[4 + b]), int(p[4 + B + b])
             cnt = d & 0x7FFFFFFF
@@ -1004,6 +1087,8 @@ def or_payloads_host(parts, B: int, vocab: int, shift: int, unpack: bool = True)
                 tok = p[o:o + cnt].astype(np.int64) - shift
                 tok = tok[(tok >= 0) & (tok < vocab)]
                 bits[b, tok] = 1
+    if facts_out is not None:
+        facts_out.copy_(torch.from_numpy(fo))
     if unpack:
         return torch.from_numpy(bits[:, :vocab].copy())
     return torch.from_numpy(np.packbits(bits, axis=1, bitorder="little").view(np.int32).copy())
@@ -1061,4 +1146,4 @@ __all__ = ["shard_docs", "peer_capable", "host_identity", "halo_tokens", "shard_
            "ShardedIndex",
            "or_bits", "pack_bits", "unpack_bits", "payload_capacity", "or_payloads", "SparseExchange",
            "PeerExchange", "PeerBarrierTimeout", "or_peer_payloads", "pack_payload_host", "or_payloads_host",
-           "payload_header_words"]
+           "payload_header_words", "payload_facts_at"]

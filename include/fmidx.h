@@ -364,6 +364,20 @@ int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint6
                   uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
                      int64_t shift, void* d_out, uint64_t ld_out, int unpack, void* stream);
+/* The same two carrying a doc-sharded processor call's per-row facts in the
+ * payload (no collective for them; SURVEY §8e: "emptiness flags and
+ * count([last]) > 0 are also exact via OR"): fm_shard_pack_facts stores d_facts
+ * (int32 [3, B]: count([last]) > 0, range non-empty, distinct non-empty, as
+ * fm_processor_shard_prep writes them) in the payload's facts area;
+ * fm_shard_or_rows_facts writes their OR over the parts to d_facts_out (int32
+ * [3, B], 0/1) -- what fm_processor_shard_finish takes for the facts summed over
+ * the ranks.  fm_shard_pack (no facts) leaves the area zero. */
+int fm_shard_pack_facts(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
+                        uint64_t ldw, uint64_t vocab, const int32_t* d_facts, uint32_t* d_payload, uint64_t cap_words,
+                        void* stream);
+int fm_shard_or_rows_facts(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
+                           int64_t shift, void* d_out, uint64_t ld_out, int unpack, int32_t* d_facts_out,
+                           void* stream);
 
 /* The peer exchange (no host read, no gather): every rank packs into one of
  * two payload buffers of fm_shard_payload_capacity words (double-buffered by
@@ -403,6 +417,14 @@ int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, ui
                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
                                 const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,
                                 void* stream);
+/* Either peer pass (d_flags NULL: fm_shard_or_rows_peers, else
+ * fm_shard_or_rows_peers_wait) with the facts' OR written to d_facts_out, as
+ * fm_shard_or_rows_facts: a sharded processor call over the flag barrier holds
+ * no collective at all. */
+int fm_shard_or_rows_peers_facts(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
+                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
+                                 const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,
+                                 int32_t* d_facts_out, void* stream);
 /* Coherent host memory mapped for the device (hipHostMalloc mapped | coherent),
  * zeroed: kernels store into it, the host reads it without a copy (the flag
  * barrier's error word). */

@@ -163,7 +163,9 @@ def test_sparse_or_reads_nothing_past_a_short_gather(dev):
     bits = ix.allowed_mask(lo_t, hi_t, V, 10, packed=True)
     pay = ix.shard_pack(lo_t, hi_t, bits, V)
     used = int(pay[0].item())
-    H = 4 + ((2 * B + 3) & ~3)
+    from fmidx.sharding import payload_header_words
+
+    H = payload_header_words(B)
     for m in (H, H + 8, (H + used) // 2 // 4 * 4, used):
         parts = pay[:m].unsqueeze(0).contiguous()
         got = or_payloads(parts, B, V, 10)

@@ -62,15 +62,21 @@ def _drive(procs, ids, scores):
     B, Vs = hs[0]["B"], hs[0]["V"]
     W = (Vs + 31) // 32
     dense = or_bits(torch.stack([h["bits"][:, :W] for h in hs]).contiguous(), Vs, unpack=False)
-    pays = [p._dev.index.shard_pack(h["mlo"], h["mhi"], h["bits"], Vs) for p, h in zip(procs, hs)]
+    # the payloads carry each shard's facts (fm_shard_pack_facts); the OR pass ORs them
+    pays = [p._dev.index.shard_pack(h["mlo"], h["mhi"], h["bits"], Vs, facts=h["facts"]) for p, h in zip(procs, hs)]
     pays = [q[:int(q[0].item())] for q in pays]
     m = max(q.numel() for q in pays)
     parts = torch.zeros((len(pays), m), dtype=torch.int32, device=ids.device)
     for r, q in enumerate(pays):
         parts[r, :q.numel()] = q
-    sparse = or_payloads(parts, B, Vs, 10, unpack=False)
+    f_or = torch.empty((3, B), dtype=torch.int32, device=ids.device)
+    sparse = or_payloads(parts, B, Vs, 10, unpack=False, facts_out=f_or)
     assert torch.equal(dense, sparse)
-    outs = [p._dev.finish(h, facts.clone(), sparse) for p, h in zip(procs, hs)]
+    assert torch.equal(f_or, (facts > 0).to(torch.int32))
+    # even shards finish from the summed facts (the dense exchange's all_reduce), odd ones from the
+    # payload's ORed facts (the sparse / peer exchanges): every output must be the same
+    outs = [p._dev.finish(h, facts.clone() if r % 2 == 0 else f_or.clone(), sparse)
+            for r, (p, h) in enumerate(zip(procs, hs))]
     for o in outs[1:]:
         assert torch.equal(o.view(torch.int16 if o.dtype != torch.float32 else torch.int32),
                            outs[0].view(torch.int16 if o.dtype != torch.float32 else torch.int32))
@@ -224,14 +230,38 @@ def test_sparse_exchange_over_rccl_world_one(indexes):
         occ = full.occurring_distinct
         mk = lambda index: P.SeqIndexBasedLogitsProcessor(index=index, num_beams=1)  # noqa: E731
         ref = mk(full)
-        for exchange in ("sparse", "peer", "dense"):
-            sidx = ShardedIndex(full, occ, group=dist.group.WORLD, exchange=exchange)
+        calls = {"n": 0}
+        real = {k: getattr(dist, k) for k in ("all_reduce", "all_gather", "all_gather_into_tensor", "barrier",
+                                                "all_gather_object", "broadcast")}
+
+        def counting(k):
+            def f(*a, **kw):
+                calls["n"] += 1
+                return real[k](*a, **kw)
+            return f
+
+        for exchange, pb in (("sparse", "flags"), ("peer", "collective"), ("peer", "flags"), ("dense", "flags")):
+            sidx = ShardedIndex(full, occ, group=dist.group.WORLD, exchange=exchange, peer_barrier=pb)
             sp = mk(sidx)
             for step in range(4):
                 ids = torch.tensor([[1] + F[a:a + 2 + step] for a in starts[:8]], dtype=torch.int64).cuda()
                 scores = torch.from_numpy(rng.standard_normal((8, V)).astype(np.float32)).cuda()
-                assert torch.equal(sp(ids, scores.clone()).view(torch.int32),
-                                   ref(ids, scores.clone()).view(torch.int32)), (exchange, step)
+                want_out = ref(ids, scores.clone())
+                # (the peer exchange maps its buffers at the first call: count from the second)
+                for k in real:
+                    setattr(dist, k, counting(k))
+                calls["n"] = 0
+                try:
+                    got_out = sp(ids, scores.clone())
+                finally:
+                    for k, f in real.items():
+                        setattr(dist, k, f)
+                assert torch.equal(got_out.view(torch.int32), want_out.view(torch.int32)), (exchange, pb, step)
+                if step and exchange == "peer" and pb == "flags":
+                    # the facts ride in the payload, the flag barrier replaces the collective: none at all
+                    assert calls["n"] == 0, (exchange, pb, calls["n"])
+                if step and exchange == "peer" and pb == "collective":
+                    assert calls["n"] == 1, (exchange, pb, calls["n"])   # the barrier alone: facts in the payload
             # the sparse exchange with a larger batch on the same index (its payload and speculative
             # gather size are rebuilt for it: ADVICE r4)
             ids = torch.tensor([[1] + F[a:a + 3] for a in rng.integers(0, len(F) - 40, size=40)],

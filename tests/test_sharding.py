@@ -121,7 +121,15 @@ def expected_masks(docs, patterns, steps):
     return out
 
 
-def _worker(rank, world, port, halo, reduce, outdir, fused=False, grow=False):
+def _as_mask(m):
+    """A step's output as uint8 [B, V]: packed int32 words (unpack=False) expanded."""
+    a = m.numpy()
+    if a.dtype == np.int32:
+        a = np.unpackbits(a.view(np.uint8), axis=1, bitorder="little")[:, :V]
+    return a.copy()
+
+
+def _worker(rank, world, port, halo, reduce, outdir, fused=False, grow=False, unpack=True):
     import torch.distributed as dist
 
     from fmidx.sharding import ShardedDecoder, shard_corpus
@@ -132,11 +140,11 @@ def _worker(rank, world, port, halo, reduce, outdir, fused=False, grow=False):
     docs, patterns, steps = make_case()
     shard_docs_, _ = shard_corpus(docs, world, rank, halo)
     shard = (OracleShardFused if fused else OracleShard)(shard_docs_)
-    dec = ShardedDecoder(shard, V, SHIFT, group=dist.group.WORLD, reduce=reduce)
+    dec = ShardedDecoder(shard, V, SHIFT, group=dist.group.WORLD, reduce=reduce, unpack=unpack)
     assert dec.fused == fused
     masks = [dec.start(patterns, "cpu").numpy().copy()]
     for tk in steps:
-        masks.append(dec.step(torch.tensor(tk, dtype=torch.int64)).numpy().copy())
+        masks.append(_as_mask(dec.step(torch.tensor(tk, dtype=torch.int64))))
     if grow:
         # the same decoder restarted with a batch three times larger: the payload and the
         # speculative gather size of the smaller batch must not be reused for it
@@ -156,9 +164,9 @@ def _free_port():
     return p
 
 
-def _run(world, halo, reduce, fused=False, grow=False):
+def _run(world, halo, reduce, fused=False, grow=False, unpack=True):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d, fused, grow), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), halo, reduce, d, fused, grow, unpack), nprocs=world, join=True)
         return [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
 
 
@@ -170,6 +178,15 @@ def test_sharded_or_equals_unsharded(reduce, fused):
     want = np.stack(expected_masks(docs, patterns, steps))
     got = _run(2, 8 + 8 + 1, reduce, fused)      # halo >= longest pattern (7 + 8 steps) + 1
     for g in got:                          # every rank holds the reduced mask
+        assert np.array_equal(g, want)
+
+
+def test_sparse_exchange_packed_output():
+    """unpack=False: the step returns the ORed rows as packed int32 words (what the
+    processors' epilogue reads) -- equal, bit for bit, to the unsharded mask."""
+    docs, patterns, steps = make_case()
+    want = np.stack(expected_masks(docs, patterns, steps))
+    for g in _run(2, 8 + 8 + 1, "sparse", fused=True, unpack=False):
         assert np.array_equal(g, want)
 
 
@@ -248,6 +265,33 @@ def test_halo_guard():
         ShardedDecoder(shard, V, SHIFT, halo=3).start(pats + [[1, 2, 3]], "cpu")
 
 
+def test_payload_facts_or():
+    """The processors' per-row facts ride in the payload's facts area
+    (pack_payload_host / fm_shard_pack_facts) and the OR pass ORs them over the
+    parts: what fm_processor_shard_finish needs of the facts' sum (> 0)."""
+    from fmidx.sharding import or_payloads_host, pack_payload_host, payload_facts_at, payload_header_words
+
+    rng = np.random.default_rng(8)
+    V, B, SH, P = 90, 13, 10, 3
+    W = (V + 31) // 32
+    bwt = rng.integers(0, V + SH, size=500)
+    facts = [rng.integers(0, 2, size=(3, B)) * (rng.random((3, B)) < 0.3) for _ in range(P)]
+    pays = []
+    for p in range(P):
+        lo = rng.integers(0, 450, size=B)
+        hi = lo + rng.integers(0, 6, size=B)
+        pays.append(pack_payload_host(lo, hi, bwt, np.zeros((B, W), dtype=np.int32), V, facts=facts[p]))
+    m = max(q.numel() for q in pays)
+    parts = torch.zeros((P, m), dtype=torch.int32)
+    for p, q in enumerate(pays):
+        parts[p, :q.numel()] = q
+        assert int(q[payload_facts_at(B) + B + 4].item()) == int(facts[p][1, 4] != 0)
+    assert payload_header_words(B) == payload_facts_at(B) + ((3 * B + 3) & ~3)
+    fo = torch.empty((3, B), dtype=torch.int32)
+    or_payloads_host(parts, B, V, SH, facts_out=fo)
+    assert np.array_equal(fo.numpy(), (sum(f != 0 for f in facts) > 0).astype(np.int32))
+
+
 def test_fixed_slot_payload_reads_like_compact():
     """fm_decode_step_payload's layout -- every row at a fixed slot H + b *
     round4(W), the unused words of a slot left as they were -- read by the
@@ -270,7 +314,9 @@ def test_fixed_slot_payload_reads_like_compact():
         bits[b, t[(t >= 0) & (t < V)]] = 1
     words = np.packbits(bits, axis=1, bitorder="little").view(np.int32)
     compact = pack_payload_host(lo, hi, bwt, words, V)
-    H = 4 + ((2 * B + 3) & ~3)
+    from fmidx.sharding import payload_header_words
+
+    H = payload_header_words(B)
     W4 = (W + 3) & ~3
     fixed = rng.integers(-2**31, 2**31, size=H + B * W4).astype(np.int64).astype(np.uint32)   # garbage
     c = compact.numpy().view(np.uint32)

@@ -39,7 +39,9 @@ def main():
     W = (V + 31) // 32
     rng = np.random.default_rng(1)
     dev = torch.device("cuda", 0)
-    H = 4 + ((2 * B + 3) & ~3)
+    from fmidx.sharding import payload_header_words
+
+    H = payload_header_words(B)
     dense_rows = np.zeros((P, B, W), dtype=np.uint32)
     pays = []
     wide = rng.random(B) < args.wide
