@@ -1243,6 +1243,24 @@ int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, 
   FM_API_END
 }
 
+int fm_decode_step_payload_signal(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                                  const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out,
+                                  uint64_t* d_hi_out, uint64_t m, uint32_t* d_payload, uint64_t cap_words,
+                                  uint64_t vocab, uint32_t* d_payload_alt, uint32_t* d_step,
+                                  const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_done, void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  if (!d_step || !d_done || !d_payload_alt) {
+    set_error("decode_step_payload_signal: the step counter, the done counter and both payload buffers");
+    return -1;
+  }
+  return fmidx::launch_decode_payload(h->idx.view, d_tokens, shift, reset_below, d_lo_in, d_hi_in, d_lo_out, d_hi_out,
+                                      m, d_payload, cap_words, vocab, d_payload_alt, d_step,
+                                      reinterpret_cast<hipStream_t>(stream), d_flag_ptrs, world, d_done);
+  FM_API_END
+}
+
 int fm_distinct_count_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m,
                             const uint64_t* d_cap_off, uint64_t total_cap, uint64_t* d_syms,
                             uint64_t* d_counts, uint64_t* d_k, void* stream) {

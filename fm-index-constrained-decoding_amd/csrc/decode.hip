@@ -387,6 +387,40 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 // (the symbols) and nothing else -- no zero-fill, no bitmap; every other row
 // writes its packed bitmap into its slot exactly as PACKED does; the row's
 // workgroup writes its desc / off words, row 0's the header.
+// The flag barrier's signal fused into the payload decode (PAY with sig.done != null): every
+// workgroup, once all its payload stores are acknowledged (system-scope write-through: performed at
+// this GPU's memory side), adds one to *sig.done; the workgroup whose add is the grid's last does
+// what k_peer_signal (csrc/shard.hip) does as a separate launch -- a system-scope release, the step
+// number (*sig.ctr + 1) stored into every rank's flag word for this rank (system-scope stores over
+// xGMI), *sig.ctr advanced, *sig.done reset for the next step -- so a flag-barrier step is two
+// launches (decode, OR pass), not three.  Every workgroup reads *sig.ctr (the buffer parity)
+// before its add, so the advance follows every read of it.
+struct PeerSignal {
+  const uint64_t* dst;   // [world] the peers' flag-word addresses for this rank
+  uint32_t* ctr;         // this rank's device step counter
+  uint32_t* done;        // workgroups done with their payload stores (0 between steps)
+  uint32_t world;
+};
+
+__device__ __forceinline__ void peer_signal_done(const PeerSignal& sig) {
+  // every wave's stores acknowledged, then one add per workgroup (all waves reach this point: the
+  // callers' exits are workgroup-uniform)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(sig.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      const uint32_t value = __hip_atomic_load(sig.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      for (uint32_t r = 0; r < sig.world; ++r)
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(sig.dst[r]), value, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(sig.ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sig.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // The row-state pointers: __restrict__ (never aliased: the uint8 / packed launches refuse in-place
 // state) except in the payload variant, whose flag-barrier step updates the state IN PLACE.  There
 // every wave consumes its state load (the early-zero / wg_scan decisions) before the plan barrier,
@@ -418,7 +452,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        uint64_t early_width, DevView v,
                                                        uint32_t* __restrict__ pay,
                                                        uint32_t* __restrict__ pay_alt,
-                                                       const uint32_t* __restrict__ pay_sel) {
+                                                       const uint32_t* __restrict__ pay_sel,
+                                                       PeerSignal sig) {
   constexpr uint32_t CH = PACKED ? 32 : 16;
   constexpr int kAux4 = PAY ? kPayAux : kStoreAux;   // the 4-B stores' cache policy
   // first thread of the early zero-fill: wave 0 stays store-free (fewer
@@ -453,7 +488,24 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   FM_STAMP(v, 0);
   const uint64_t st_lo = (uint64_t)ql.x | ((uint64_t)ql.y << 32), st_hi = (uint64_t)qh.x | ((uint64_t)qh.y << 32);
   const int64_t st_tok = (int64_t)((uint64_t)qt.x | ((uint64_t)qt.y << 32));
-  if (row >= m) return;
+  if (row >= m) {   // a padding workgroup: nothing stored, still counted by the fused signal
+    if constexpr (PAY) {
+      if (sig.done && threadIdx.x == 0) {
+        // (its read of the counter, in PAY's buffer pick, does not exist: nothing to order)
+        const uint32_t prev = __hip_atomic_fetch_add(sig.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+          const uint32_t value = __hip_atomic_load(sig.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          for (uint32_t r = 0; r < sig.world; ++r)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(sig.dst[r]), value, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(sig.ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sig.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    return;
+  }
   const uint64_t t0 = (uint64_t)slice * SW;
   if (t0 >= vocab) return;
   const uint64_t t1 = min(vocab, t0 + SW);
@@ -650,6 +702,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
         lo_out[row] = lo;
         hi_out[row] = hi;
       }
+      if (sig.done) peer_signal_done(sig);
       return;
     }
   }
@@ -874,6 +927,9 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     lo_out[row] = lo;
     hi_out[row] = hi;
   }
+  if constexpr (PAY) {
+    if (sig.done) peer_signal_done(sig);
+  }
   FM_STAMP(v, 7);
   FM_STAMP_FLUSH(v, row);
 }
@@ -958,7 +1014,7 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   const size_t lds = (size_t)win_words(SW) * 4;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v, nullptr, nullptr, nullptr)
+                                        mask, ld, ew, v, nullptr, nullptr, nullptr, PeerSignal{})
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
@@ -984,7 +1040,8 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
 int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                           const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                           uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, uint32_t* pay_alt,
-                          const uint32_t* pay_sel, hipStream_t s) {
+                          const uint32_t* pay_sel, hipStream_t s, const uint64_t* sig_dst, uint64_t sig_world,
+                          uint32_t* sig_done) {
   if (m == 0) return 0;
   const uint64_t W = (vocab + 31) / 32, W4 = (W + 3) & ~3ull, H = payload_header_words(m);
   if (!pay || !tok || !lo_in || !hi_in || !lo_out || !hi_out || vocab == 0 || W > kPayMaxWords ||
@@ -1007,6 +1064,11 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
     set_error("decode payload: state in/out buffers overlap without being the same buffer");
     return -1;
   }
+  if (sig_done && (!pay_sel || sig_world > 64 || (sig_world && !sig_dst))) {
+    set_error("decode payload: the fused signal needs the step counter and 0..64 flag addresses");
+    return -1;
+  }
+  const PeerSignal sig{sig_dst, const_cast<uint32_t*>(pay_sel), sig_done, (uint32_t)sig_world};
   const uint32_t T = decode_threads(m);
   const uint32_t S = 1, SW = (uint32_t)((vocab + 63) & ~63ull);   // one slice per row: whole-row decisions
   const unsigned g = (unsigned)((m + 7) / 8 * 8);
@@ -1015,13 +1077,13 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
   const uint64_t ld = W4 * 4;
   if (T == 1024)
     k_decode<true, true, 1024, true><<<g, 1024, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                          reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
+                                                          reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
   else if (T == 512)
     k_decode<true, true, 512, true><<<g, 512, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
+                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
   else
     k_decode<true, true, 256, true><<<g, 256, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel);
+                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -815,7 +815,8 @@ int launch_decode(const DevView& v, const int64_t* tok, int64_t shift, int64_t r
 int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below,
                           const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                           uint64_t m, uint32_t* pay, uint64_t cap, uint64_t vocab, uint32_t* pay_alt,
-                          const uint32_t* pay_sel, hipStream_t s);
+                          const uint32_t* pay_sel, hipStream_t s, const uint64_t* sig_dst = nullptr,
+                          uint64_t sig_world = 0, uint32_t* sig_done = nullptr);
 int launch_cache_probe(const DevView& v, const uint64_t* lo, const uint64_t* hi, uint64_t m, uint8_t* out,
                        hipStream_t s);
 int launch_follow_bitmaps(const DevView& v, const uint64_t* C, uint64_t nsym, uint32_t* out,

@@ -75,6 +75,9 @@ SIGNATURES = {
     "fm_decode_step_payload": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p,
                                        c_void_p]),
+    "fm_decode_step_payload_signal": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p,
+                                              c_void_p, c_uint64, c_void_p, c_void_p]),
     "fm_shard_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p,
                               c_uint64, c_void_p]),
     "fm_shard_or_rows": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p, c_uint64,

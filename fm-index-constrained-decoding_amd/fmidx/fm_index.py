@@ -403,6 +403,20 @@ class FMIndex:
                                            c_void_p(_stream_of(lo))), "decode_step_payload")
         return payload
 
+    def decode_step_payload_signal(self, tokens, lo, hi, payload, payload_alt, step, flag_ptrs, world: int, done,
+                                   vocab: int, shift: int, reset_below: int = -(1 << 63)):
+        """decode_step_payload in place with the flag barrier's signal fused in
+        (fm_decode_step_payload_signal): the last workgroup posts the step to the
+        ``world`` flag words at ``flag_ptrs`` (int64 device addresses) and
+        advances ``step``; ``done`` (int32 [1], zero) counts the workgroups."""
+        check(lib().fm_decode_step_payload_signal(
+            self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below), c_void_p(lo.data_ptr()),
+            c_void_p(hi.data_ptr()), c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), lo.numel(),
+            c_void_p(payload.data_ptr()), payload.numel(), int(vocab), c_void_p(payload_alt.data_ptr()),
+            c_void_p(step.data_ptr()), c_void_p(flag_ptrs.data_ptr()), int(world), c_void_p(done.data_ptr()),
+            c_void_p(_stream_of(lo))), "decode_step_payload_signal")
+        return payload
+
     def shard_pack(self, lo, hi, bits, vocab: int, payload=None, facts=None):
         """The sparse exchange payload of this shard's rows (fm_shard_pack):
         per row its BWT slice when narrower than a bitmap, else its packed

@@ -769,6 +769,7 @@ class PeerExchange:
         # the flag barrier's words (one per rank) and this rank's step counter, shared like the payloads
         self.flags = torch.zeros(max(64, self.world), dtype=torch.int32, device=self.device)
         self.ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.done = torch.zeros(1, dtype=torch.int32, device=self.device)   # the fused signal's workgroup count
         # its error word: coherent host memory the OR pass stores into on a timeout
         ep = c_void_p()
         check(lib().fm_host_mapped_alloc(4, byref(ep)), "host_mapped_alloc")
@@ -852,20 +853,31 @@ class PeerExchange:
 
     def flags_step(self, index, tokens, lo, hi, vocab: int, shift: int, out, unpack: bool = True,
                    reset_below: int = 0):
-        """One decode step with the flag barrier, as three stream-ordered
+        """One decode step with the flag barrier, as two stream-ordered
         launches and nothing else (capturable; a captured call replays for
         every step): the payload decode of ``index`` -- the state (lo, hi)
-        updated in place, the payload buffer picked by the counter's parity --
-        the signal, the OR pass into ``out``.  The caller counts executed steps
+        updated in place, the payload buffer picked by the counter's parity,
+        the signal fused into its last workgroup -- then the OR pass into
+        ``out`` (an index without the fused form: three launches, the signal
+        its own).  The caller counts executed steps
         in ``self.step`` (host parity = device parity, for payload())."""
         if self.barrier_mode != "flags":
             raise ValueError("flags_step: the exchange's barrier is not the flag barrier")
         B = lo.numel()
         if B > self.rows or vocab != self.vocab:
             raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
-        index.decode_step_payload(tokens, lo, hi, lo, hi, self.bufs[0], vocab, shift, reset_below=reset_below,
-                                  payload_alt=self.bufs[1], step=self.ctr)
-        self.signal()
+        if hasattr(index, "decode_step_payload_signal"):
+            # the signal fused into the decode kernel (its last workgroup posts the step): two launches
+            world = self.world
+            if self._skip_signal:
+                self._skip_signal -= 1
+                world = 0
+            index.decode_step_payload_signal(tokens, lo, hi, self.bufs[0], self.bufs[1], self.ctr, self.signal_to,
+                                             world, self.done, vocab, shift, reset_below=reset_below)
+        else:
+            index.decode_step_payload(tokens, lo, hi, lo, hi, self.bufs[0], vocab, shift, reset_below=reset_below,
+                                      payload_alt=self.bufs[1], step=self.ctr)
+            self.signal()
         return self.or_flags(B, vocab, shift, out=out, unpack=unpack)
 
     def or_flags(self, B: int, vocab: int, shift: int, out=None, unpack: bool = True, facts_out=None):

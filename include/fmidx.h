@@ -360,6 +360,16 @@ int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, 
                            const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out, uint64_t* d_hi_out,
                            uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab,
                            uint32_t* d_payload_alt, const uint32_t* d_step, void* stream);
+/* The same step with the flag barrier's signal fused in (fm_peer_signal without its own launch):
+ * every workgroup, once its payload stores are acknowledged, adds one to *d_done (a uint32 zeroed
+ * once, reset by the kernel itself); the last one does fm_peer_signal's work -- a system-scope
+ * release, step = *d_step + 1 stored into every rank's flag word for this rank (d_flag_ptrs[world]),
+ * *d_step = step.  A flag-barrier step is then two launches (this, fm_shard_or_rows_peers_wait). */
+int fm_decode_step_payload_signal(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
+                                  const uint64_t* d_lo_in, const uint64_t* d_hi_in, uint64_t* d_lo_out,
+                                  uint64_t* d_hi_out, uint64_t m, uint32_t* d_payload, uint64_t cap_words,
+                                  uint64_t vocab, uint32_t* d_payload_alt, uint32_t* d_step,
+                                  const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_done, void* stream);
 int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
                   uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,
