@@ -398,27 +398,39 @@ __device__ __forceinline__ uint4 bits16_to_bytes(uint32_t b) {
 struct PeerSignal {
   const uint64_t* dst;   // [world] the peers' flag-word addresses for this rank
   uint32_t* ctr;         // this rank's device step counter
-  uint32_t* done;        // workgroups done with their payload stores (0 between steps)
+  uint32_t* done;        // kSigCounters counters, kSigStride words apart (zero between steps)
   uint32_t world;
 };
+// The count is two-level so that no one word takes every workgroup's add (a word saturates near
+// 90 returning atomics per us -- 2048 workgroups on one word cost B = 2048 steps ~13 us): counter r
+// (r < 8) counts the workgroups b with b % 8 == r, and the last of each adds to counter 8, whose
+// last signals.  Each counter on its own 128-B line.
+constexpr uint32_t kSigStride = 32;   // 9 counters: done[0 .. 9 * kSigStride)
+
+// one workgroup's arrival (called by ONE thread, after the workgroup's stores are acknowledged)
+__device__ __forceinline__ void peer_signal_arrive(const PeerSignal& sig) {
+  const uint32_t b = blockIdx.x, g = gridDim.x, r = b & 7u;
+  const uint32_t in_r = (g - r + 7u) / 8u;                 // workgroups with residue r
+  uint32_t* cr = sig.done + r * kSigStride;
+  if (__hip_atomic_fetch_add(cr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != in_r - 1u) return;
+  __hip_atomic_store(cr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every one of them has added
+  uint32_t* top = sig.done + 8u * kSigStride;
+  const uint32_t groups = g < 8u ? g : 8u;
+  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != groups - 1u) return;
+  __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t value = __hip_atomic_load(sig.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  for (uint32_t k = 0; k < sig.world; ++k)
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(sig.dst[k]), value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(sig.ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void peer_signal_done(const PeerSignal& sig) {
-  // every wave's stores acknowledged, then one add per workgroup (all waves reach this point: the
-  // callers' exits are workgroup-uniform)
+  // every wave's stores acknowledged, then one arrival per workgroup (all waves reach this point:
+  // the callers' exits are workgroup-uniform)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(sig.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      const uint32_t value = __hip_atomic_load(sig.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      for (uint32_t r = 0; r < sig.world; ++r)
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(sig.dst[r]), value, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(sig.ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sig.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (threadIdx.x == 0) peer_signal_arrive(sig);
 }
 
 // The row-state pointers: __restrict__ (never aliased: the uint8 / packed launches refuse in-place
@@ -490,19 +502,8 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   const int64_t st_tok = (int64_t)((uint64_t)qt.x | ((uint64_t)qt.y << 32));
   if (row >= m) {   // a padding workgroup: nothing stored, still counted by the fused signal
     if constexpr (PAY) {
-      if (sig.done && threadIdx.x == 0) {
-        // (its read of the counter, in PAY's buffer pick, does not exist: nothing to order)
-        const uint32_t prev = __hip_atomic_fetch_add(sig.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == gridDim.x - 1) {
-          const uint32_t value = __hip_atomic_load(sig.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-          for (uint32_t r = 0; r < sig.world; ++r)
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(sig.dst[r]), value, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(sig.ctr, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(sig.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+      // (it stored nothing and read no counter: it only arrives)
+      if (sig.done && threadIdx.x == 0) peer_signal_arrive(sig);
     }
     return;
   }

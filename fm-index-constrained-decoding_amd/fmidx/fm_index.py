@@ -408,7 +408,10 @@ class FMIndex:
         """decode_step_payload in place with the flag barrier's signal fused in
         (fm_decode_step_payload_signal): the last workgroup posts the step to the
         ``world`` flag words at ``flag_ptrs`` (int64 device addresses) and
-        advances ``step``; ``done`` (int32 [1], zero) counts the workgroups."""
+        advances ``step``; ``done`` (int32 [288], zero: nine counters on their own
+        128-B lines) counts the workgroups."""
+        if done.numel() < 9 * 32:
+            raise ValueError("decode_step_payload_signal: done needs 9 * 32 int32 words")
         check(lib().fm_decode_step_payload_signal(
             self._h, c_void_p(tokens.data_ptr()), int(shift), int(reset_below), c_void_p(lo.data_ptr()),
             c_void_p(hi.data_ptr()), c_void_p(lo.data_ptr()), c_void_p(hi.data_ptr()), lo.numel(),

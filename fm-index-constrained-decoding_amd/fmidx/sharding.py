@@ -769,7 +769,8 @@ class PeerExchange:
         # the flag barrier's words (one per rank) and this rank's step counter, shared like the payloads
         self.flags = torch.zeros(max(64, self.world), dtype=torch.int32, device=self.device)
         self.ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.done = torch.zeros(1, dtype=torch.int32, device=self.device)   # the fused signal's workgroup count
+        # the fused signal's workgroup counts (csrc/decode.hip: 9 counters, 32 words apart)
+        self.done = torch.zeros(9 * 32, dtype=torch.int32, device=self.device)
         # its error word: coherent host memory the OR pass stores into on a timeout
         ep = c_void_p()
         check(lib().fm_host_mapped_alloc(4, byref(ep)), "host_mapped_alloc")

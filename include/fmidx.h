@@ -361,8 +361,9 @@ int fm_decode_step_payload(fm_index* h, const int64_t* d_tokens, int64_t shift, 
                            uint64_t m, uint32_t* d_payload, uint64_t cap_words, uint64_t vocab,
                            uint32_t* d_payload_alt, const uint32_t* d_step, void* stream);
 /* The same step with the flag barrier's signal fused in (fm_peer_signal without its own launch):
- * every workgroup, once its payload stores are acknowledged, adds one to *d_done (a uint32 zeroed
- * once, reset by the kernel itself); the last one does fm_peer_signal's work -- a system-scope
+ * every workgroup, once its payload stores are acknowledged, arrives on d_done (288 uint32 zeroed once:
+ * nine counters 32 words apart -- one per residue of the workgroup index mod 8, then their join --
+ * reset by the kernel itself); the last one does fm_peer_signal's work -- a system-scope
  * release, step = *d_step + 1 stored into every rank's flag word for this rank (d_flag_ptrs[world]),
  * *d_step = step.  A flag-barrier step is then two launches (this, fm_shard_or_rows_peers_wait). */
 int fm_decode_step_payload_signal(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_t reset_below,
