@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
                                                        typename StatePtr<PAY>::out hi_out,
                                                        int64_t shift, int64_t reset_below,
                                                        uint8_t* __restrict__ mask, uint64_t ld,
-                                                       uint64_t early_width, DevView v,
+                                                       uint64_t early_width, uint32_t split_at, DevView v,
                                                        uint32_t* __restrict__ pay,
                                                        uint32_t* __restrict__ pay_alt,
                                                        const uint32_t* __restrict__ pay_sel,
@@ -481,7 +481,25 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   uint64_t row;
   uint32_t slice;
-  map_block(blockIdx.x, S, row, slice);
+  // The static split of the wide rows' emit (split_at != 0: uint8 masks, one slice per row, B <= 256;
+  // the grid is 2 x the padded rows).  Workgroup b < grid / 2 is row b's as always; workgroup
+  // grid / 2 + b is row b's HELPER.  A row whose incoming range is wide (a restart, or >= cache_min
+  // rows: the full range or a cached range -- the rows whose step ends in a 128-KB bitmap emit or a
+  // late zero-fill, the step's last to finish) is emitted in two halves: tokens [0, split_at) by its
+  // own workgroup, [split_at, V) by its helper, which takes the same LF step (redundantly: the probe
+  // lines are then in its XCD's L2 -- grid / 2 is a multiple of 8, so a row and its helper share an
+  // XCD) and stores no state.  The helper of any other row exits after the state load.  Decided by
+  // the row's own state alone: no schedule, no atomics, no second read of a bitmap half.  (With
+  // 89 VGPRs one 1024-thread workgroup fits a CU, so helpers are dispatched as the narrow rows'
+  // workgroups retire.)
+  const uint32_t half = gridDim.x / 2;
+  const bool helper = split_at != 0 && blockIdx.x >= half;
+  if (helper) {
+    row = blockIdx.x - half;
+    slice = 1;
+  } else {
+    map_block(blockIdx.x, S, row, slice);
+  }
   // The row state first, as VECTOR loads (vmcnt) through the preloaded
   // pointers: FM_PRELOAD_VIEW's scalar loads then wait on lgkmcnt alone and do
   // not serialise behind (or in front of) the state's round trip.  (Serving
@@ -500,16 +518,23 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
   FM_STAMP(v, 0);
   const uint64_t st_lo = (uint64_t)ql.x | ((uint64_t)ql.y << 32), st_hi = (uint64_t)qh.x | ((uint64_t)qh.y << 32);
   const int64_t st_tok = (int64_t)((uint64_t)qt.x | ((uint64_t)qt.y << 32));
-  if (row >= m) {   // a padding workgroup: nothing stored, still counted by the fused signal
+  if (row >= m) {   // a padding workgroup: nothing stored, still counted by the fused signal (PAY)
     if constexpr (PAY) {
       // (it stored nothing and read no counter: it only arrives)
       if (sig.done && threadIdx.x == 0) peer_signal_arrive(sig);
     }
     return;
   }
-  const uint64_t t0 = (uint64_t)slice * SW;
+  uint64_t t0 = (uint64_t)slice * SW;
+  uint64_t t1 = min(vocab, t0 + SW);
+  if (split_at) {
+    const uint64_t w_in = min(st_hi, v.n) > st_lo ? min(st_hi, v.n) - st_lo : 0;
+    const bool wide = st_tok < reset_below || w_in >= v.cache_min;
+    if (helper && !wide) return;                 // this row is emitted whole by its own workgroup
+    t0 = helper ? split_at : 0;
+    t1 = (wide && !helper) ? split_at : vocab;
+  }
   if (t0 >= vocab) return;
-  const uint64_t t1 = min(vocab, t0 + SW);
   const uint64_t ntok = t1 - t0;
   const uint64_t nch = (ntok + CH - 1) / CH;
   uint8_t* out_row = mask + row * ld;
@@ -932,7 +957,7 @@ __global__ void __launch_bounds__(kDecThreads, kDecThreads >= 1024 ? 1 : FMIDX_S
     if (sig.done) peer_signal_done(sig);
   }
   FM_STAMP(v, 7);
-  FM_STAMP_FLUSH(v, row);
+  if (!helper) FM_STAMP_FLUSH(v, row);
 }
 
 // cache probe per row (one wave each): 1 if [lo, hi) has a cached bitmap
@@ -960,6 +985,11 @@ static uint32_t decode_threads(uint64_t m) {
   if (e == 256 || e == 512 || e == 1024) return e;
   return m <= 256 ? 1024 : 256;
 }
+
+#ifndef FMIDX_DEC_SPLIT
+#define FMIDX_DEC_SPLIT 1   // measurement variant 0: the wide rows emitted whole by their own workgroup
+#endif
+constexpr bool kDecSplit = FMIDX_DEC_SPLIT != 0;
 
 #ifndef FMIDX_WAVE_BUDGET
 #define FMIDX_WAVE_BUDGET 4096   // measurement variant: resident waves the slice geometry aims at
@@ -1005,7 +1035,11 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   const uint32_t T = decode_threads(m);
   uint32_t S, SW;
   mask_geometry(m, vocab, T, S, SW);
-  const uint64_t grid = (m + 7) / 8 * 8 * S;
+  // the wide rows' emit split with a helper workgroup each (see k_decode): the fused uint8 step at
+  // one 1024-thread workgroup per row
+  const uint32_t split_at = (kDecSplit && do_lf && !packed && T == 1024 && S == 1 && vocab >= 2048)
+                                ? (uint32_t)(((vocab / 2) + 63) & ~63ull) : 0u;
+  const uint64_t grid = (m + 7) / 8 * 8 * S * (split_at ? 2 : 1);
   if (grid > 0x7fffffffull / T) {
     set_error("too many rows for one launch");
     return -1;
@@ -1015,7 +1049,7 @@ static int launch_decode_kernel(const DevView& v, const int64_t* tok, int64_t sh
   const size_t lds = (size_t)win_words(SW) * 4;
 #define FM_LAUNCH(P, L, TT)                                                                                    \
   k_decode<P, L, TT><<<g, TT, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift, reset_below, \
-                                        mask, ld, ew, v, nullptr, nullptr, nullptr, PeerSignal{})
+                                        mask, ld, ew, split_at, v, nullptr, nullptr, nullptr, PeerSignal{})
 #define FM_LAUNCH_T(P, L)          \
   do {                             \
     if (T == 1024)                 \
@@ -1078,13 +1112,13 @@ int launch_decode_payload(const DevView& v, const int64_t* tok, int64_t shift, i
   const uint64_t ld = W4 * 4;
   if (T == 1024)
     k_decode<true, true, 1024, true><<<g, 1024, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                          reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
+                                                          reset_below, mask, ld, 0, 0u, v, pay, pay_alt, pay_sel, sig);
   else if (T == 512)
     k_decode<true, true, 512, true><<<g, 512, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
+                                                        reset_below, mask, ld, 0, 0u, v, pay, pay_alt, pay_sel, sig);
   else
     k_decode<true, true, 256, true><<<g, 256, lds, s>>>(tok, lo_in, hi_in, m, S, SW, vocab, lo_out, hi_out, shift,
-                                                        reset_below, mask, ld, 0, v, pay, pay_alt, pay_sel, sig);
+                                                        reset_below, mask, ld, 0, 0u, v, pay, pay_alt, pay_sel, sig);
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -110,3 +110,71 @@ def test_build_options_refused_once_built(dev):
     assert lib().fm_set_build_options(ix._h, ctypes.byref(o)) == -1
     assert b"already built" in lib().fm_last_error()
     assert ix.build_options() == before and before["cache_min"] == 8
+
+
+@pytest.mark.parametrize("B", [256, 160])
+def test_decode_split_emit_vs_oracle(dev, B):
+    """The static split of the wide rows' emit (k_decode, B <= 256 at one
+    1024-thread workgroup per row, V = 128256: a row entering with a restart,
+    the full range or a range of >= cache_min rows is emitted as two halves --
+    tokens [0, 64128) by its own workgroup, the rest by its helper workgroup,
+    both taking the LF step).  Every step's uint8 mask and state equal the
+    oracle's, over rows that restart, stay wide (cached, cache_min 8), go
+    narrow, go empty, with tokens in both halves of the vocabulary."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from oracle.fm_oracle import OracleIndex, allowed_mask
+
+    rng = np.random.default_rng(B)
+    V = 128256
+    low = rng.integers(0, 400, size=120)
+    high = rng.integers(64000, 128200, size=400)
+    docs = []
+    for _ in range(500):
+        ln = int(rng.integers(10, 200))
+        d = [int(low[rng.integers(0, low.size)]) if rng.random() < 0.6 else int(high[rng.integers(0, high.size)])
+             for _ in range(ln)]
+        docs.append(d)
+    for d in docs[::4]:
+        d[:3] = [7, 8, 9]                 # a shared phrase: wide ranges
+    F = [t for d in reversed(docs) for t in d]
+    ours = FMIndex(device=0, options={"cache_min": 8, "bm_log2": 5})
+    ours.initialize(docs, in_memory=True)
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    starts = rng.integers(0, len(F) - 20, B)
+    pats = [[]] + [[7]] + [[7, 8]] + [F[s:s + int(rng.integers(1, 3))] for s in starts[3:]]
+    lo, hi = ours.get_range_batch(pats, 10)
+    lo_t = torch.tensor(lo.astype(np.int64), device=dev)
+    hi_t = torch.tensor(hi.astype(np.int64), device=dev)
+    lo2, hi2 = torch.empty_like(lo_t), torch.empty_like(hi_t)
+    mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+    plen = [len(p) for p in pats]
+    wide_seen = 0
+    for step in range(6):
+        tok = []
+        for b in range(B):
+            p = int(starts[b]) + plen[b]
+            if (b + step) % 17 == 3:
+                t = -1
+            elif rng.random() < 0.8 and p < len(F):
+                t = F[p]
+            else:
+                t = int(rng.integers(0, 128200))
+            tok.append(t)
+            pats[b] = [] if t < 0 else pats[b] + [t]
+            plen[b] = 0 if t < 0 else plen[b] + 1
+        w_in = (torch.clamp(hi_t, max=ours.size()) - lo_t).clamp(min=0)
+        wide_seen += int((w_in >= 8).sum())
+        tk = torch.tensor(tok, dtype=torch.int64, device=dev)
+        ours.decode_step(tk, lo_t, hi_t, mask, V, 10, reset_below=0, lo_out=lo2, hi_out=hi2)
+        lo_t, lo2, hi_t, hi2 = lo2, lo_t, hi2, hi_t
+        want = [ora.get_range(p) if p else (0, ours.size()) for p in pats]
+        want = [(a, b) if b > a else (0, 0) for a, b in want]
+        got = list(zip(lo_t.cpu().tolist(), hi_t.cpu().tolist()))
+        # an empty pattern's range (a restart) is the full range [0, n)
+        assert [(a, b) if b > a else (0, 0) for a, b in got] == want, step
+        ref = allowed_mask(ora, [w[0] for w in want], [w[1] for w in want], V, 10)
+        assert np.array_equal(mask.cpu().numpy(), ref), step
+    assert wide_seen > 50     # the split path ran (rows entering wide)
