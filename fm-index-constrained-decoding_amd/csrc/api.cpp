@@ -114,6 +114,13 @@ struct fm_index {
   // caller's stream, the host API on idx.stream)
   hipEvent_t ws_ev = nullptr;
   bool ws_ev_pending = false;
+  // the persistent LF sweep's own workspace (never shared: its tags and counters stay valid
+  // between launches), its last use, and the launch epoch (tags of earlier launches never match)
+  void* lfp_ws = nullptr;
+  size_t lfp_bytes = 0;
+  hipEvent_t lfp_ev = nullptr;
+  bool lfp_ev_pending = false;
+  uint32_t lfp_epoch = 0;
 };
 
 namespace {
@@ -507,6 +514,8 @@ void fm_destroy(fm_index* h) {
     if (h->hstage) (void)hipHostFree(h->hstage);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->ws_ev) (void)hipEventDestroy(h->ws_ev);
+    if (h->lfp_ws) (void)hipFree(h->lfp_ws);
+    if (h->lfp_ev) (void)hipEventDestroy(h->lfp_ev);
     if (h->idx.stream) (void)hipStreamDestroy(h->idx.stream);
   }
   delete h;
@@ -1183,6 +1192,28 @@ int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_
   FM_CHECK_BUILT(h);
   FM_GUARD(h);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (fmidx::lf_persist(m) && !capturing(s)) {
+    std::lock_guard<std::mutex> lk(h->mu);
+    const size_t need = fmidx::lf_persist_ws_bytes(m);
+    if (!h->lfp_ev) FM_HIP(hipEventCreateWithFlags(&h->lfp_ev, hipEventDisableTiming));
+    if (h->lfp_bytes < need) {
+      if (h->lfp_ev_pending) FM_HIP(hipEventSynchronize(h->lfp_ev));
+      if (h->lfp_ws) FM_HIP(hipFree(h->lfp_ws));
+      h->lfp_ws = nullptr;
+      h->lfp_bytes = 0;
+      FM_HIP(hipMalloc(&h->lfp_ws, need));
+      FM_HIP(hipMemsetAsync(h->lfp_ws, 0, need, s));   // counters, error word, tags: zero
+      h->lfp_bytes = need;
+    } else if (h->lfp_ev_pending) {
+      FM_HIP(hipStreamWaitEvent(s, h->lfp_ev, 0));
+    }
+    if (++h->lfp_epoch == 0) h->lfp_epoch = 1;
+    const int rc = fmidx::launch_lf_persist(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out,
+                                            m, s, h->lfp_ws, h->lfp_bytes, h->lfp_epoch, h->idx.device);
+    FM_HIP(hipEventRecord(h->lfp_ev, s));
+    h->lfp_ev_pending = true;
+    return rc;
+  }
   const size_t wsb = fmidx::lf_ws_bytes(m);
   // the worklist variant needs the workspace: under capture the launch takes the workspace-free kernels
   if (!wsb || capturing(s)) return fmidx::launch_lf_step(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out, m, s);
@@ -1555,6 +1586,19 @@ int fm_shard_or_rows_peers_facts(const uint64_t* d_part_ptrs, uint64_t nparts, u
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
                                            d_flags, d_step, spins, err, d_facts_out,
                                            reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+int fm_lf_persist_status(fm_index* h, uint32_t* err) {
+  FM_API_BEGIN
+  FM_CHECK_HANDLE(h);
+  FM_GUARD(h);
+  std::lock_guard<std::mutex> lk(h->mu);
+  *err = 0;
+  if (!h->lfp_ws) return 0;
+  if (h->lfp_ev_pending) FM_HIP(hipEventSynchronize(h->lfp_ev));
+  FM_HIP(hipMemcpy(err, static_cast<char*>(h->lfp_ws) + fmidx::lf_persist_err_offset(), 4, hipMemcpyDeviceToHost));
+  return 0;
   FM_API_END
 }
 

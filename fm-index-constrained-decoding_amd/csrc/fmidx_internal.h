@@ -712,7 +712,8 @@ struct Tuning {
   uint32_t dec_threads = 0;      // decode workgroup size; 0 = by batch
   uint32_t mask_slices = 0;      // decode slices per row; 0 = by the wave budget
   uint64_t lf_group_min = 8192;
-  int32_t lf_work = -1;          // -1 by row count, 0 grouped kernel, 1 worklist + tail, 2 in-wave sweep
+  int32_t lf_work = -1;          // -1 by row count, 0 grouped kernel, 1 worklist + tail, 2 in-wave sweep,
+                                 // 4 persistent sweep (heads, then a shared tail-queue drain)
   int32_t lf_gprobe = 1;
   int32_t lf_quad = 1;
   int32_t lf_split = 0;
@@ -798,6 +799,14 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
                    const uint64_t* lo, const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out,
                    uint64_t m, hipStream_t s, void* ws = nullptr);
 size_t lf_ws_bytes(uint64_t m);   // 0: this launch takes no workspace
+// the persistent LF sweep (tuning lf_work 4): whether it serves m rows, its own workspace (zeroed
+// when allocated, never shared), the launch (epoch: nonzero, new per launch), the error word's offset
+bool lf_persist(uint64_t m);
+size_t lf_persist_ws_bytes(uint64_t m);
+size_t lf_persist_err_offset();
+int launch_lf_persist(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below, const uint64_t* lo,
+                      const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out, uint64_t m, hipStream_t s, void* ws,
+                      size_t ws_bytes, uint32_t epoch, int dev);
 int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint64_t m,
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,
                   uint64_t* hi_out, hipStream_t s);

@@ -84,8 +84,8 @@ bool check_tuning(const Tuning& t) {
     set_error("tuning: dec_threads must be 0, 256, 512 or 1024");
     return false;
   }
-  if (t.lf_work < -1 || t.lf_work > 2) {
-    set_error("tuning: lf_work must be -1 (by row count), 0, 1 or 2");
+  if (t.lf_work < -1 || t.lf_work > 4 || t.lf_work == 3) {
+    set_error("tuning: lf_work must be -1 (by row count), 0, 1, 2 or 4");
     return false;
   }
   if (t.sa_chunk < 1024) {

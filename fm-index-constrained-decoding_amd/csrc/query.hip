@@ -741,20 +741,25 @@ constexpr int kTailPass = 8;      // 64-entry passes per round trip of the tail 
 #else
 #define FMIDX_SWEEP_ATTR
 #endif
-template <bool INLINE>
-__global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
-                                                        int64_t reset_below, const uint64_t* lo_in,
-                                                        const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
-                                                        uint64_t m, LfWork* lt, uint32_t* cnt, uint64_t cap) {
-  __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
-  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
-  __shared__ uint32_t s_n[kLfThreads / 64 + 1];
+// One wave's 64 rows of the LF sweep up to its tail rows (the head): the row
+// state (token, lo, hi: one round trip), the C lookup of full-range rows, the
+// narrow rows' E entries packed end to end over the wave, the cached rows'
+// transition probes eight at a time -- every row settled except the tail rows
+// (E scans of 65..512 rows, uncached wide ranges, probe misses), which come back
+// flagged with their (l, h, c, pid1).  i = this lane's row; valid = i < m.
+struct SweepRow {
+  uint64_t l, h, c;       // the row's range (h clamped to n) and symbol
+  uint64_t nl, nh;        // its new range (settled rows)
+  uint64_t pid1;          // a probe miss: the range's cache id + 1 (0: unknown)
+  bool tail;              // still to step (sweep_tails)
+};
+
+__device__ __forceinline__ void sweep_head(const DevView& v, const int64_t* __restrict__ tok, int64_t shift,
+                                           int64_t reset_below, const uint64_t* lo_in, const uint64_t* hi_in,
+                                           uint64_t m, uint64_t i, bool valid, unsigned long long (*mm)[64],
+                                           uint4* run, SweepRow& r) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = threadIdx.x >> 6;
   const uint32_t seg = lane / kProbeLanes;
-  const uint64_t i = (uint64_t)blockIdx.x * kLfThreads + threadIdx.x;
-  // (no early return: every wave of the workgroup reaches the append's barriers)
-  const bool valid = i < m;
   const uint64_t ii = valid ? i : m - 1;
   const int64_t t = (int64_t)row_load_u64(tok, m, ii);
   const uint64_t l = row_load_u64(lo_in, m, ii);
@@ -782,8 +787,8 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   }
   const uint32_t excl = inc - cnt_e;
   const uint32_t total = __shfl(inc, 63, 64);
-  s_mm[wv][0][lane] = ~0ull;
-  s_mm[wv][1][lane] = 0;
+  mm[0][lane] = ~0ull;
+  mm[1][lane] = 0;
   __builtin_amdgcn_wave_barrier();
   uint64_t pmask = __ballot(probe);   // probe rows left, batches of kProbeRows
   uint64_t res_lo = 0, res_hi = 0, pid1 = 0;   // a probe row's result (on its own lane)
@@ -794,18 +799,18 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
 #pragma unroll
     for (int k = 0; k < kSweepPass; ++k) {
       const uint32_t e = t0 + 64u * k + lane;
-      uint32_t r = 0;   // the last row whose offset is <= e (rows of no entries are never it)
+      uint32_t rr = 0;   // the last row whose offset is <= e (rows of no entries are never it)
 #pragma unroll
       for (int st = 32; st > 0; st >>= 1) {
-        const uint32_t x = __shfl(excl, (int)(r + st), 64);
-        if (x <= e) r += st;
+        const uint32_t x = __shfl(excl, (int)(rr + st), 64);
+        if (x <= e) rr += st;
       }
-      const uint64_t base = __shfl(l, (int)r, 64);
-      const uint32_t off = e - __shfl(excl, (int)r, 64);
-      cs[k] = __shfl(c, (int)r, 64);
+      const uint64_t base = __shfl(l, (int)rr, 64);
+      const uint32_t off = e - __shfl(excl, (int)rr, 64);
+      cs[k] = __shfl(c, (int)rr, 64);
       // unconditional (a surplus lane reads E[0]: one shared line)
       xs[k] = v.E[e < total ? base + off : 0];
-      rs[k] = e < total ? r : ~0u;
+      rs[k] = e < total ? rr : ~0u;
     }
     // the next batch of probe rows, in the same round trip
     int src = -1;
@@ -828,14 +833,14 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
 #pragma unroll
     for (int k = 0; k < kSweepPass; ++k) {
       if (rs[k] != ~0u && (xs[k] >> kESymShift) == cs[k]) {
-        atomicMin(&s_mm[wv][0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
-        atomicMax(&s_mm[wv][1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+        atomicMin(&mm[0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+        atomicMax(&mm[1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
       }
     }
     if (v.trans_cap && __ballot(pact)) {
       bool hit;
       uint64_t clo, chi, p1;
-      probe_finish(v, pl, ph, pc, pact, pld, s_run[wv], hit, clo, chi, p1);
+      probe_finish(v, pl, ph, pc, pact, pld, run, hit, clo, chi, p1);
       // hand each probed row its result (the batch's k-th row sits in segment k)
 #pragma unroll
       for (uint32_t k = 0; k < kProbeRows; ++k) {
@@ -854,7 +859,7 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   }
   __builtin_amdgcn_wave_barrier();
   // LF is increasing over a symbol's rows: the new range is [min LF, max LF + 1) of the matches
-  const uint64_t fmin = s_mm[wv][0][lane], fmax = s_mm[wv][1][lane];
+  const uint64_t fmin = mm[0][lane], fmax = mm[1][lane];
   uint64_t nl = 0, nh = 0;
   if (reset) {
     nl = 0;
@@ -869,146 +874,337 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
     nl = res_lo;
     nh = res_hi;
   }
-  tail = tail || (probe && !probed);
+  r.l = l;
+  r.h = h;
+  r.c = c;
+  r.nl = nl;
+  r.nh = nh;
+  r.pid1 = pid1;
+  r.tail = tail || (probe && !probed);
+}
+
+// The wave's tail rows (lanes with r.tail; their (l, h, c, pid1) per lane), stepped together, the
+// results into r.nl / r.nh of those lanes (1.8 tail rows per 64 on a decode trace: 0.8 E scans of
+// 65..512 rows, 1.0 descents; stepped one at a time they were 37 % of the sweep's time at 2^19
+// pairs in round 5):
+//  (1) every E-scan tail of the wave in ONE packed scan (their entries end to end over the
+//      wave, kTailPass passes per round trip), not one lf_step_fast round trip per row;
+//  (2) the descents four at a time, one per quarter-wave (lf_descend_quad).
+// A probe miss of a range whose bitmap is cached (pid1): the range's word for c, every such row of
+// the wave at once and in the round trip of (1) -- a symbol the range lacks (nearly every miss:
+// 0.15 % of the keys are left out of the table) settles the row as empty with no descent.
+// mm: the wave's LDS slots, untouched since the head for these rows (or reset by the caller).
+__device__ __forceinline__ void sweep_tails(const DevView& v, unsigned long long (*mm)[64], SweepRow& r) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool tail = r.tail;
+  const uint64_t l = r.l, h = r.h, c = r.c, pid1 = r.pid1;
+  uint64_t nl = r.nl, nh = r.nh;
+  const bool pm = tail && pid1 != 0;
+  const uint32_t* pwp = pm ? v.cache_bm + (pid1 - 1) * v.bm_words + ((uint32_t)c >> 5)
+                           : reinterpret_cast<const uint32_t*>(v.C);
+  const uint32_t pword_own = pm ? *pwp : ~0u;
+  const bool t1 = tail && v.E && h - l <= kENarrow;
+  {
+    const uint32_t cnt1 = t1 ? (uint32_t)(h - l) : 0u;
+    uint32_t inc1 = cnt1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc1, d, 64);
+      if (lane >= (uint32_t)d) inc1 += y;
+    }
+    const uint32_t excl1 = inc1 - cnt1;
+    const uint32_t total1 = __shfl(inc1, 63, 64);
+    for (uint32_t t0 = 0; t0 < total1; t0 += 64 * kTailPass) {   // wave-uniform
+      uint64_t xs[kTailPass], cs[kTailPass];
+      uint32_t rs[kTailPass];
+#pragma unroll
+      for (int k = 0; k < kTailPass; ++k) {
+        const uint32_t e = t0 + 64u * k + lane;
+        uint32_t rr = 0;   // the last row whose offset is <= e (rows of no entries are never it)
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const uint32_t x = __shfl(excl1, (int)(rr + st), 64);
+          if (x <= e) rr += st;
+        }
+        const uint64_t base = __shfl(l, (int)rr, 64);
+        const uint32_t off = e - __shfl(excl1, (int)rr, 64);
+        cs[k] = __shfl(c, (int)rr, 64);
+        xs[k] = v.E[e < total1 ? base + off : 0];   // unconditional (a surplus lane reads E[0])
+        rs[k] = e < total1 ? rr : ~0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kTailPass; ++k) {
+        if (rs[k] != ~0u && (xs[k] >> kESymShift) == cs[k]) {
+          atomicMin(&mm[0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+          atomicMax(&mm[1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
+        }
+      }
+    }
+    if (total1) {   // wave-uniform; the slots of these rows were untouched by the narrow scan
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t f0 = mm[0][lane], f1 = mm[1][lane];
+      if (t1) {
+        nl = f0 != ~0ull ? f0 : 0;
+        nh = f0 != ~0ull ? f1 + 1 : 0;
+      }
+    }
+  }
+#ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
+  uint64_t tb = 0;
+#else
+  const bool absent = pm && !((pword_own >> ((uint32_t)c & 31u)) & 1u);   // nl = nh = 0 already
+  if (absent) {
+    nl = 0;
+    nh = 0;
+  }
+  uint64_t tb = __ballot(tail && !t1 && !absent);
+#endif
+  while (tb) {   // wave-uniform: up to four rows per round, quarter-wave q takes the q-th
+    int sv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sv[k] = tb ? __ffsll((long long)tb) - 1 : -1;
+      if (tb) tb &= tb - 1;
+    }
+    const uint32_t qw = lane >> 4;
+    const int src = qw == 0 ? sv[0] : (qw == 1 ? sv[1] : (qw == 2 ? sv[2] : sv[3]));
+    const bool act = src >= 0;
+    const int s_ = act ? src : sv[0];   // an idle quarter repeats the first row (valid inputs), its result unused
+    uint64_t tl = __shfl(l, s_, 64), th = __shfl(h, s_, 64);
+    const uint64_t tc = __shfl(c, s_, 64);
+    lf_descend_quad(v, act, tc, __shfl(pword_own, s_, 64), tl, th);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t rl = __shfl(tl, 16 * k, 64), rh = __shfl(th, 16 * k, 64);
+      if (sv[k] >= 0 && (int)lane == sv[k]) {
+        nl = rl;
+        nh = rh;
+      }
+    }
+  }
+  r.nl = nl;
+  r.nh = nh;
+}
+
+template <bool INLINE>
+__global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevView v, const int64_t* __restrict__ tok, int64_t shift,
+                                                        int64_t reset_below, const uint64_t* lo_in,
+                                                        const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                                                        uint64_t m, LfWork* lt, uint32_t* cnt, uint64_t cap) {
+  __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
+  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
+  __shared__ uint32_t s_n[kLfThreads / 64 + 1];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * kLfThreads + threadIdx.x;
+  // (no early return: every wave of the workgroup reaches the append's barriers)
+  const bool valid = i < m;
+  SweepRow r;
+  sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], s_run[wv], r);
   if (INLINE) {
 #if FMIDX_SWEEP_TAIL_BATCH
-    // The wave's tail rows (1.8 per wave on a decode trace: 0.8 E scans of 65..512 rows, 1.0
-    // descents; round 5: 37 % of the sweep's time at 2^19 pairs went to them, stepped one at a
-    // time), then every row is written:
-    //  (1) every E-scan tail of the wave in ONE packed scan (their entries end to end over the
-    //      wave, kTailPass passes per round trip), not one lf_step_fast round trip per row;
-    //  (2) the descents four at a time, one per quarter-wave (lf_descend_quad).
-    // a probe miss of a range whose bitmap is cached (pid1): the range's word for c, every such row
-    // of the wave at once and in the round trip of (1) -- a symbol the range lacks (nearly every
-    // miss: 0.15 % of the keys are left out of the table) settles the row as empty with no descent
-    const bool pm = tail && pid1 != 0;
-    const uint32_t* pwp = pm ? v.cache_bm + (pid1 - 1) * v.bm_words + ((uint32_t)c >> 5)
-                             : reinterpret_cast<const uint32_t*>(v.C);
-    const uint32_t pword_own = pm ? *pwp : ~0u;
-    const bool t1 = tail && v.E && h - l <= kENarrow;
-    {
-      const uint32_t cnt1 = t1 ? (uint32_t)(h - l) : 0u;
-      uint32_t inc1 = cnt1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc1, d, 64);
-        if (lane >= (uint32_t)d) inc1 += y;
-      }
-      const uint32_t excl1 = inc1 - cnt1;
-      const uint32_t total1 = __shfl(inc1, 63, 64);
-      for (uint32_t t0 = 0; t0 < total1; t0 += 64 * kTailPass) {   // wave-uniform
-        uint64_t xs[kTailPass], cs[kTailPass];
-        uint32_t rs[kTailPass];
-#pragma unroll
-        for (int k = 0; k < kTailPass; ++k) {
-          const uint32_t e = t0 + 64u * k + lane;
-          uint32_t r = 0;   // the last row whose offset is <= e (rows of no entries are never it)
-#pragma unroll
-          for (int st = 32; st > 0; st >>= 1) {
-            const uint32_t x = __shfl(excl1, (int)(r + st), 64);
-            if (x <= e) r += st;
-          }
-          const uint64_t base = __shfl(l, (int)r, 64);
-          const uint32_t off = e - __shfl(excl1, (int)r, 64);
-          cs[k] = __shfl(c, (int)r, 64);
-          xs[k] = v.E[e < total1 ? base + off : 0];   // unconditional (a surplus lane reads E[0])
-          rs[k] = e < total1 ? r : ~0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kTailPass; ++k) {
-          if (rs[k] != ~0u && (xs[k] >> kESymShift) == cs[k]) {
-            atomicMin(&s_mm[wv][0][rs[k]], (unsigned long long)(xs[k] & kELfMask));
-            atomicMax(&s_mm[wv][1][rs[k]], (unsigned long long)(xs[k] & kELfMask));
-          }
-        }
-      }
-      if (total1) {   // wave-uniform; the slots of these rows were untouched by the narrow scan
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t f0 = s_mm[wv][0][lane], f1 = s_mm[wv][1][lane];
-        if (t1) {
-          nl = f0 != ~0ull ? f0 : 0;
-          nh = f0 != ~0ull ? f1 + 1 : 0;
-        }
-      }
-    }
-#ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
-    uint64_t tb = 0;
-#else
-    const bool absent = pm && !((pword_own >> ((uint32_t)c & 31u)) & 1u);   // nl = nh = 0 already
-    uint64_t tb = __ballot(tail && !t1 && !absent);
-#endif
-    while (tb) {   // wave-uniform: up to four rows per round, quarter-wave r takes the r-th
-      int sv[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        sv[k] = tb ? __ffsll((long long)tb) - 1 : -1;
-        if (tb) tb &= tb - 1;
-      }
-      const uint32_t qw = lane >> 4;
-      const int src = qw == 0 ? sv[0] : (qw == 1 ? sv[1] : (qw == 2 ? sv[2] : sv[3]));
-      const bool act = src >= 0;
-      const int s_ = act ? src : sv[0];   // an idle quarter repeats the first row (valid inputs), its result unused
-      uint64_t tl = __shfl(l, s_, 64), th = __shfl(h, s_, 64);
-      const uint64_t tc = __shfl(c, s_, 64);
-      lf_descend_quad(v, act, tc, __shfl(pword_own, s_, 64), tl, th);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t rl = __shfl(tl, 16 * k, 64), rh = __shfl(th, 16 * k, 64);
-        if (sv[k] >= 0 && (int)lane == sv[k]) {
-          nl = rl;
-          nh = rh;
-        }
-      }
-    }
+    sweep_tails(v, s_mm[wv], r);
 #else
     // the wave's tail rows one at a time by the whole wave (lf_step_tail), then every row is written
 #ifdef FMIDX_SWEEP_SKIP_TAIL   // measurement variant (wrong results): the launch without its tail rows' steps
     uint64_t tb = 0;
 #else
-    uint64_t tb = __ballot(tail);
+    uint64_t tb = __ballot(r.tail);
 #endif
     while (tb) {
       const int src = __ffsll((long long)tb) - 1;
       tb &= tb - 1;
-      uint64_t tl = __shfl(l, src, 64), th = __shfl(h, src, 64);
-      const uint64_t tc = __shfl(c, src, 64), tp = __shfl(pid1, src, 64);
+      uint64_t tl = __shfl(r.l, src, 64), th = __shfl(r.h, src, 64);
+      const uint64_t tc = __shfl(r.c, src, 64), tp = __shfl(r.pid1, src, 64);
       const uint32_t* pw = tp ? v.cache_bm + (tp - 1) * v.bm_words + ((uint32_t)tc >> 5)
                                 : reinterpret_cast<const uint32_t*>(v.C);
       const uint32_t pword = tp ? *pw : ~0u;
       lf_step_tail(v, tc, pword, tl, th);
       if ((int)lane == src) {
-        nl = tl;
-        nh = th;
+        r.nl = tl;
+        r.nh = th;
       }
     }
 #endif
     if (valid) {
-      lo_out[i] = nl;
-      hi_out[i] = nh;
+      lo_out[i] = r.nl;
+      hi_out[i] = r.nh;
     }
     return;
   }
+  const bool tail = r.tail;
   if (valid && !tail) {
-    lo_out[i] = nl;
-    hi_out[i] = nh;
+    lo_out[i] = r.nl;
+    hi_out[i] = r.nh;
   }
   // ---- tail rows: one atomic per workgroup (LDS-only barriers: nothing
   // crossing them is global data, so the stores above need not drain)
   const uint64_t tb = __ballot(tail);
   if (lane == 0) s_n[wv] = (uint32_t)__popcll(tb);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  const uint32_t r = (uint32_t)(blockIdx.x % kWorkRegions);
+  const uint32_t rg = (uint32_t)(blockIdx.x % kWorkRegions);
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
     for (uint32_t w = 0; w < kLfThreads / 64; ++w) tot += s_n[w];
-    s_n[kLfThreads / 64] = tot ? atomicAdd(&cnt[r], tot) : 0u;
+    s_n[kLfThreads / 64] = tot ? atomicAdd(&cnt[rg], tot) : 0u;
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (tail) {
     uint32_t pos = s_n[kLfThreads / 64];
     for (uint32_t w = 0; w < wv; ++w) pos += s_n[w];
     pos += (uint32_t)__popcll(tb & ((1ull << lane) - 1));
-    lt[(uint64_t)r * cap + pos] = LfWork{l, h, c | (pid1 << 32), i};
+    lt[(uint64_t)rg * cap + pos] = LfWork{r.l, r.h, r.c | (r.pid1 << 32), i};
+  }
+}
+
+// ------------------------------------------------- persistent LF sweep (lf_work 4)
+// The in-wave sweep above lives its rows' longest chain: a wave whose 64 rows hold a descent or a
+// wide E scan lives 16-27 us where one without lives 10 (round 5's stamps), and a 2^19-pair launch
+// is 1.6 residency rounds of such waves, so its last waves start late and end later.  Here the grid
+// is the resident wave count, and every wave
+//   heads  runs the head (sweep_head) of chunks w, w + W, w + 2W, ... (64 rows each; W = the
+//          grid's waves), stores the settled rows and APPENDS the tail rows to the tail queue of
+//          partition w mod 16 (one atomic per chunk reserves the slots; each entry is then written
+//          write-through and, after it is performed, its 4-B tag = the launch's epoch);
+//   drain  then claims queued tail rows up to four at a time (a compare-and-swap that claims only
+//          reserved slots) from every queue in turn, starting with its own, waits for their tags,
+//          and steps them together (sweep_tails: the E scans packed, the descents one per
+//          quarter-wave) -- tails are stepped four at a time by whichever wave is free, not one or
+//          two per wave by the wave that met them.
+// A wave leaves a queue when it holds no unclaimed reserved slot; a row appended later is drained
+// by the wave that appended it, which drains every queue after its heads.  So no wave waits for
+// another to finish anything but the few stores after a reservation (nothing waits on a wave that
+// is not resident), and the poll for a tag is bounded all the same (kPersistSpins; on expiry the
+// error word is set and the wave leaves).  Counters: two sets (the epoch's parity), each counter
+// on its own 128-B line; a launch zeroes the other set for the next launch on the stream.  Not
+// captured into graphs (the API launches it only on a stream that is not capturing).
+constexpr uint32_t kPParts = 16;                  // tail queues
+constexpr uint32_t kPStride = 32;                 // words between counters
+constexpr uint32_t kPCounters = 2 * kPParts;      // qtail[16] (reserved), qhead[16] (claimed)
+constexpr uint32_t kPSetWords = kPCounters * kPStride;
+constexpr uint32_t kPersistSpins = 1u << 22;
+constexpr int kPSysAux = 16;                      // sc1: entries written through, read past the L1
+
+struct PersistWs {
+  uint32_t* ctr;     // 2 x kPSetWords
+  LfWork* tq;        // kPParts x qcap
+  uint32_t* tag;     // kPParts x qcap
+  uint32_t* err;     // a tag poll ran out: the launch's rows are not all stepped
+};
+
+__device__ __forceinline__ uint32_t* pctr(uint32_t* set, uint32_t which, uint32_t q) {
+  return set + (which * kPParts + q) * kPStride;
+}
+
+__global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int64_t* __restrict__ tok, int64_t shift,
+                                                          int64_t reset_below, const uint64_t* lo_in,
+                                                          const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
+                                                          uint64_t m, PersistWs ws, uint32_t qcap, uint32_t epoch) {
+  __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
+  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
+  typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = threadIdx.x >> 6;
+  uint32_t* set = ws.ctr + (epoch & 1u) * kPSetWords;
+  if (blockIdx.x == 0 && threadIdx.x < kPCounters)   // the next launch's counters
+    ws.ctr[((epoch + 1u) & 1u) * kPSetWords + threadIdx.x * kPStride] = 0u;
+  const uint64_t nchunks = (m + 63) / 64;
+  const uint64_t gw = (uint64_t)blockIdx.x * (kLfThreads / 64) + wv;
+  const uint64_t nw = (uint64_t)gridDim.x * (kLfThreads / 64);
+  const uint32_t p0 = (uint32_t)(gw % kPParts);
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(ws.tq + (uint64_t)p0 * qcap, qcap * (uint32_t)sizeof(LfWork));
+  // ---- heads: chunks gw, gw + nw, ...
+  for (uint64_t chunk = gw; chunk < nchunks; chunk += nw) {   // wave-uniform
+    const uint64_t i = chunk * 64 + lane;
+    const bool valid = i < m;
+    SweepRow r;
+    sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], s_run[wv], r);
+    const bool tail = valid && r.tail;
+    if (valid && !tail) {
+      lo_out[i] = r.nl;
+      hi_out[i] = r.nh;
+    }
+    const uint64_t tb = __ballot(tail);
+    if (tb) {   // wave-uniform
+      uint32_t base = 0;
+      if (lane == 0)
+        base = __hip_atomic_fetch_add(pctr(set, 0, p0), (uint32_t)__popcll(tb), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      base = __shfl(base, 0, 64);
+      const uint32_t pos = base + (uint32_t)__popcll(tb & ((1ull << lane) - 1));
+      if (tail) {   // pos < qcap: a queue holds every row of its waves' chunks
+        const uint64_t sp = r.c | (r.pid1 << 32);
+        const v4u_ a = {(uint32_t)r.l, (uint32_t)(r.l >> 32), (uint32_t)r.h, (uint32_t)(r.h >> 32)};
+        const v4u_ b = {(uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)i, (uint32_t)(i >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(a, rq, pos * (uint32_t)sizeof(LfWork), 0, kPSysAux);
+        __builtin_amdgcn_raw_buffer_store_b128(b, rq, pos * (uint32_t)sizeof(LfWork) + 16u, 0, kPSysAux);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every entry performed before its tag
+      if (tail)
+        __hip_atomic_store(ws.tag + (uint64_t)p0 * qcap + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // ---- drain: every queue, from this wave's own
+  for (uint32_t k = 0; k < kPParts; ++k) {   // wave-uniform
+    const uint32_t q = (p0 + k) % kPParts;
+    uint32_t* qt = pctr(set, 0, q);
+    uint32_t* qh = pctr(set, 1, q);
+    for (;;) {
+      // claim up to four reserved slots: [j0, j0 + n)
+      uint32_t j0 = 0, n = 0;
+      if (lane == 0) {
+        uint32_t h = __hip_atomic_load(qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t = __hip_atomic_load(qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (h < t) {
+          const uint32_t want = min(4u, t - h);
+          const uint32_t old = atomicCAS(qh, h, h + want);   // device scope
+          if (old == h) {
+            j0 = h;
+            n = want;
+            break;
+          }
+          h = old;   // another wave claimed first
+        }
+      }
+      j0 = __shfl(j0, 0, 64);
+      n = __shfl(n, 0, 64);
+      if (!n) break;   // nothing reserved and unclaimed here now: the next queue
+      const bool mine = lane < n;
+      const uint32_t j = j0 + lane;
+      const uint64_t slot = (uint64_t)q * qcap + (mine ? j : j0);
+      // the slots are reserved: their tags follow within a few stores (bounded poll regardless)
+      bool ok = !mine;
+      for (uint32_t spin = 0; spin < kPersistSpins; ++spin) {
+        if (!ok) ok = __hip_atomic_load(ws.tag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!__all(ok)) {
+        if (lane == 0) __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      SweepRow r;
+      r.tail = mine;
+      r.nl = r.nh = 0;
+      const __amdgpu_buffer_rsrc_t re = make_rsrc(ws.tq + (uint64_t)q * qcap, qcap * (uint32_t)sizeof(LfWork));
+      const uint32_t jj = mine ? j : j0;
+      const v4u_ a = __builtin_amdgcn_raw_buffer_load_b128(re, jj * (uint32_t)sizeof(LfWork), 0, kPSysAux);
+      const v4u_ b = __builtin_amdgcn_raw_buffer_load_b128(re, jj * (uint32_t)sizeof(LfWork) + 16u, 0, kPSysAux);
+      r.l = (uint64_t)a.x | ((uint64_t)a.y << 32);
+      r.h = (uint64_t)a.z | ((uint64_t)a.w << 32);
+      const uint64_t sp = (uint64_t)b.x | ((uint64_t)b.y << 32);
+      r.c = sp & 0xFFFFFFFFull;
+      r.pid1 = sp >> 32;
+      const uint64_t row = (uint64_t)b.z | ((uint64_t)b.w << 32);
+      s_mm[wv][0][lane] = ~0ull;
+      s_mm[wv][1][lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      sweep_tails(v, s_mm[wv], r);
+      if (mine) {
+        lo_out[row] = r.nl;
+        hi_out[row] = r.nh;
+      }
+    }
   }
 }
 
@@ -1576,6 +1772,7 @@ struct LfTuning {
   bool split;
   bool work;          // worklist sweeps (k_lf_sweep + k_lf_tail) when a workspace is given
   bool work_inline;   // k_lf_sweep alone, tail rows stepped in-wave
+  bool persist;       // k_lf_persist (lf_work 4) from sweep_min rows, when the API gives its workspace
   uint64_t sweep_min; // work_inline from this many rows (lf_work -1: lf_sweep_min; 2: min_rows)
   bool search_p8;     // get_range at one lane per row probes cached rows eight at a time
 };
@@ -1593,8 +1790,9 @@ LfTuning load_lf_tuning() {
   t.split = p.lf_split != 0;
   const bool autow = p.lf_work < 0;
   t.work = p.lf_work == 1;
-  t.work_inline = autow || p.lf_work == 2;
-  t.sweep_min = autow ? p.lf_sweep_min : 0;
+  t.persist = p.lf_work == 4;
+  t.work_inline = autow || p.lf_work == 2 || t.persist;
+  t.sweep_min = (autow || t.persist) ? p.lf_sweep_min : 0;
   t.search_p8 = p.search_p8 != 0;
   return t;
 }
@@ -1680,6 +1878,58 @@ int launch_lf_step(const DevView& v, const int64_t* tok, int64_t shift, int64_t 
   FM_HIP(hipGetLastError());
   return 0;
 }
+
+bool lf_persist(uint64_t m) {
+  return lf_tuning().persist && m > lf_tuning().min_rows && m >= lf_tuning().sweep_min && m < (1ull << 28);
+}
+
+// the persistent sweep's workspace: [counters: 2 sets][err word, its own line][tail queues][tags]
+static uint64_t lf_persist_qcap(uint64_t m) { return 64 * ((((m + 63) / 64) + kPParts - 1) / kPParts); }
+
+size_t lf_persist_ws_bytes(uint64_t m) {
+  const uint64_t qcap = lf_persist_qcap(m);
+  return (size_t)2 * kPSetWords * 4 + 128 + (size_t)kPParts * qcap * (sizeof(LfWork) + 4);
+}
+
+// the grid: the resident workgroups (every wave a head worker, then a drainer)
+static unsigned lf_persist_grid(int dev) {
+  static unsigned cached[64] = {};
+  if (dev >= 0 && dev < 64 && cached[dev]) return cached[dev];
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lf_persist, kLfThreads, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  unsigned g = (unsigned)per_cu * (unsigned)cus;
+  g = std::max(4u, g / 4 * 4);   // waves a multiple of 16: wave w's chunks all in queue w mod 16
+  if (dev >= 0 && dev < 64) cached[dev] = g;
+  return g;
+}
+
+int launch_lf_persist(const DevView& v, const int64_t* tok, int64_t shift, int64_t reset_below, const uint64_t* lo,
+                      const uint64_t* hi, uint64_t* lo_out, uint64_t* hi_out, uint64_t m, hipStream_t s, void* ws,
+                      size_t ws_bytes, uint32_t epoch, int dev) {
+  if (m == 0) return 0;
+  const uint64_t qcap = lf_persist_qcap(m);
+  if (!ws || ws_bytes < lf_persist_ws_bytes(m) || qcap * sizeof(LfWork) >= (1ull << 32) || epoch == 0) {
+    set_error("lf persist: workspace of %llu bytes, %llu needed", (unsigned long long)ws_bytes,
+              (unsigned long long)lf_persist_ws_bytes(m));
+    return -1;
+  }
+  char* b = static_cast<char*>(ws);
+  PersistWs w;
+  w.ctr = reinterpret_cast<uint32_t*>(b);
+  w.err = reinterpret_cast<uint32_t*>(b + 2 * kPSetWords * 4);
+  w.tq = reinterpret_cast<LfWork*>(b + 2 * kPSetWords * 4 + 128);
+  w.tag = reinterpret_cast<uint32_t*>(w.tq + kPParts * qcap);
+  const uint64_t nchunks = (m + 63) / 64;
+  const unsigned g = (unsigned)std::min<uint64_t>(lf_persist_grid(dev), (nchunks + 3) / 4 * 4);
+  k_lf_persist<<<std::max(4u, g / 4 * 4), kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, w,
+                                                               (uint32_t)qcap, epoch);
+  FM_HIP(hipGetLastError());
+  return 0;
+}
+
+size_t lf_persist_err_offset() { return 2 * kPSetWords * 4; }
 
 int launch_search(const DevView& v, const int64_t* tok, const int64_t* off, uint64_t m,
                   int64_t shift, const uint64_t* lo_in, const uint64_t* hi_in, uint64_t* lo_out,

@@ -85,6 +85,7 @@ SIGNATURES = {
     "fm_shard_or_rows_peers": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
                                        c_uint64, c_int, c_void_p]),
     "fm_peer_signal": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p]),
+    "fm_lf_persist_status": (c_int, [c_void_p, POINTER(c_uint32)]),
     "fm_shard_or_rows_peers_wait": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
                                             c_uint64, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
     "fm_shard_pack_facts": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_void_p,

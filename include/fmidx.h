@@ -101,6 +101,7 @@ typedef struct fm_tuning {
   uint32_t reserved;
   uint64_t lf_group_min;    /* grouped LF / get_range kernels above this many rows (8192) */
   int32_t lf_work;          /* -1: the in-wave sweep from lf_sweep_min rows, else the grouped kernel; 0 grouped only;
+                               4: the persistent sweep from lf_sweep_min rows (heads, then a shared tail-queue drain);
                                1 sweep + worklist tail (not inside a captured graph: the grouped kernel
                                there); 2 in-wave sweep whenever grouped */
   int32_t lf_gprobe;        /* groups of >= 4 lanes probe the transition table themselves (1) */
@@ -424,6 +425,10 @@ int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_
  * The step number lives on the device, so decode + signal + OR captured once
  * into a graph replay for every step. */
 int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_step, void* stream);
+/* The persistent LF sweep (fm_tuning lf_work = 4, fm_lf_step_batch from lf_sweep_min rows on a stream
+ * that is not capturing): after a synchronisation with its last launch, *err != 0 if a launch gave up
+ * a wait (never on a sound run; its rows are then not all stepped). */
+int fm_lf_persist_status(fm_index* h, uint32_t* err);
 int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
                                 const uint32_t* d_flags, const uint32_t* d_step, uint32_t spins, uint32_t* err,

@@ -178,3 +178,71 @@ def test_decode_split_emit_vs_oracle(dev, B):
         ref = allowed_mask(ora, [w[0] for w in want], [w[1] for w in want], V, 10)
         assert np.array_equal(mask.cpu().numpy(), ref), step
     assert wide_seen > 50     # the split path ran (rows entering wide)
+
+
+def test_lf_persist_vs_oracle(dev):
+    """The persistent LF sweep (tuning lf_work 4: heads of static 64-row
+    chunks, tail rows appended to 16 shared queues and drained four at a time
+    by whichever wave is free) against the oracle, on a corpus made for tail
+    rows (17-bit symbols, ranges wider than the sweep's E scans and narrower
+    than the range cache, ranges ending at n, cached ranges with probe misses,
+    an index without E): three launches in a row (the counter sets and tags
+    alternate by epoch), one of them in place; no launch gave up a wait."""
+    import torch
+
+    from fmidx._lib import lib
+    from fmidx.index import FMIndex
+    from fmidx.options import tuning
+    from oracle.fm_oracle import OracleIndex
+
+    rng = np.random.default_rng(43)
+
+    def doc():
+        ln = int(rng.integers(40, 160))
+        common = rng.integers(0, 24, ln)
+        rare = rng.integers(60000, 120000, ln)
+        return [int(x) for x in np.where(rng.random(ln) < 0.9, common, rare)]
+
+    docs = [doc() for _ in range(300)]
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    F = [t for d in reversed(docs) for t in d]
+    for opts in ({}, {"cache_min": 64}, {"lf_e": 0}):
+        ours = FMIndex(device=0, options=opts or None)
+        ours.initialize(docs, in_memory=True)
+        n = ours.size()
+        for rep in range(3):
+            m = 30011 + 977 * rep
+            pats, nxt = [], []
+            for i in range(m):
+                ln = int(rng.integers(0, 3))
+                s = int(rng.integers(0, len(F) - ln))
+                pats.append(list(F[s:s + ln]))
+                nxt.append(F[int(rng.integers(0, len(F)))] if rng.random() < 0.85 else int(rng.integers(-1, 120000)))
+            want = [ora.get_range(p) if p else (0, n) for p in pats]
+            li = [w[0] for w in want]
+            hv = [w[1] for w in want]
+            hv[::7] = [n] * len(hv[::7])
+            li[::7] = [max(0, n - int(rng.integers(513, 4000))) for _ in range(len(li[::7]))]
+            want_lf = []
+            for i in range(m):
+                a_, b_ = li[i], min(hv[i], n)
+                if nxt[i] < 0:
+                    want_lf.append((0, n))                     # reset_below = 0: a restart
+                else:
+                    want_lf.append((0, 0) if a_ >= b_ else ora.backward_search_step(int(nxt[i]) + 10, a_, b_ - 1))
+            lo_in = torch.tensor(li, dtype=torch.int64, device=dev)
+            hi_in = torch.tensor(hv, dtype=torch.int64, device=dev)
+            tok = torch.tensor(nxt, dtype=torch.int64, device=dev)
+            with tuning(lf_work=4, lf_sweep_min=1):
+                if rep == 1:      # in place
+                    ours.lf_step_batch(tok, lo_in, hi_in, 10, reset_below=0)
+                    lo_out, hi_out = lo_in, hi_in
+                else:
+                    lo_out, hi_out = torch.empty_like(lo_in), torch.empty_like(hi_in)
+                    ours.lf_step_batch(tok, lo_in, hi_in, 10, lo_out=lo_out, hi_out=hi_out, reset_below=0)
+            got = list(zip(lo_out.cpu().tolist(), hi_out.cpu().tolist()))
+            bad = [i for i in range(m) if got[i] != tuple(want_lf[i])]
+            assert not bad, (opts, rep, [(i, nxt[i], li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]])
+        err = ctypes.c_uint32(7)
+        assert lib().fm_lf_persist_status(ours._h, ctypes.byref(err)) == 0 and err.value == 0, opts
