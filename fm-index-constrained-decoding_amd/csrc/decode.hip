@@ -987,7 +987,9 @@ static uint32_t decode_threads(uint64_t m) {
 }
 
 #ifndef FMIDX_DEC_SPLIT
-#define FMIDX_DEC_SPLIT 1   // measurement variant 0: the wide rows emitted whole by their own workgroup
+// measurement variant 1: the static split of the wide rows' emit (k_decode) -- exact, but slower at
+// C3: 15.9-16.0 us cold per step against 13.7-13.9 (profiles/r06_split/)
+#define FMIDX_DEC_SPLIT 0
 #endif
 constexpr bool kDecSplit = FMIDX_DEC_SPLIT != 0;
 

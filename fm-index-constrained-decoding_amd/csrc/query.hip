@@ -1078,6 +1078,12 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
 // error word is set and the wave leaves).  Counters: two sets (the epoch's parity), each counter
 // on its own 128-B line; a launch zeroes the other set for the next launch on the stream.  Not
 // captured into graphs (the API launches it only on a stream that is not capturing).
+#ifndef FMIDX_PERSIST_ONE
+#define FMIDX_PERSIST_ONE 0
+#endif
+#ifndef FMIDX_PERSIST_ALLQ
+#define FMIDX_PERSIST_ALLQ 0
+#endif
 constexpr uint32_t kPParts = 16;                  // tail queues
 constexpr uint32_t kPStride = 32;                 // words between counters
 constexpr uint32_t kPCounters = 2 * kPParts;      // qtail[16] (reserved), qhead[16] (claimed)
@@ -1144,8 +1150,8 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
         __hip_atomic_store(ws.tag + (uint64_t)p0 * qcap + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  // ---- drain: every queue, from this wave's own
-  for (uint32_t k = 0; k < kPParts; ++k) {   // wave-uniform
+  // ---- drain: this wave's own queue (FMIDX_PERSIST_ALLQ: every queue, from its own)
+  for (uint32_t k = 0; k < (FMIDX_PERSIST_ALLQ ? kPParts : 1u); ++k) {   // wave-uniform
     const uint32_t q = (p0 + k) % kPParts;
     uint32_t* qt = pctr(set, 0, q);
     uint32_t* qh = pctr(set, 1, q);
@@ -1922,7 +1928,10 @@ int launch_lf_persist(const DevView& v, const int64_t* tok, int64_t shift, int64
   w.tq = reinterpret_cast<LfWork*>(b + 2 * kPSetWords * 4 + 128);
   w.tag = reinterpret_cast<uint32_t*>(w.tq + kPParts * qcap);
   const uint64_t nchunks = (m + 63) / 64;
-  const unsigned g = (unsigned)std::min<uint64_t>(lf_persist_grid(dev), (nchunks + 3) / 4 * 4);
+  // FMIDX_PERSIST_ONE (measurement variant): one chunk per wave -- the heads dispatched as the in-wave
+  // sweep's are, only the tail rows shared
+  const unsigned g = FMIDX_PERSIST_ONE ? (unsigned)((nchunks + 3) / 4 * 4)
+                                       : (unsigned)std::min<uint64_t>(lf_persist_grid(dev), (nchunks + 3) / 4 * 4);
   k_lf_persist<<<std::max(4u, g / 4 * 4), kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, w,
                                                                (uint32_t)qcap, epoch);
   FM_HIP(hipGetLastError());
