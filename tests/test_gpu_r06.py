@@ -114,13 +114,15 @@ def test_build_options_refused_once_built(dev):
 
 @pytest.mark.parametrize("B", [256, 160])
 def test_decode_split_emit_vs_oracle(dev, B):
-    """The static split of the wide rows' emit (k_decode, B <= 256 at one
-    1024-thread workgroup per row, V = 128256: a row entering with a restart,
-    the full range or a range of >= cache_min rows is emitted as two halves --
-    tokens [0, 64128) by its own workgroup, the rest by its helper workgroup,
-    both taking the LF step).  Every step's uint8 mask and state equal the
-    oracle's, over rows that restart, stay wide (cached, cache_min 8), go
-    narrow, go empty, with tokens in both halves of the vocabulary."""
+    """The fused uint8 decode step at the headline's geometry (B <= 256: one
+    1024-thread workgroup per row, one vocabulary slice, V = 128256) -- and,
+    in a library built with FMIDX_DEC_SPLIT=1, the static split of the wide
+    rows' emit (a row entering with a restart, the full range or >= cache_min
+    rows emitted as two halves, the upper one by a helper workgroup; measured
+    slower and off by default, profiles/r06_split/).  Every step's mask and
+    state equal the oracle's, over rows that restart, stay wide (cached,
+    cache_min 8), go narrow, go empty, with tokens in both halves of the
+    vocabulary."""
     import torch
 
     from fmidx.index import FMIndex
