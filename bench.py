@@ -209,7 +209,8 @@ def lf_plan_bytes(prev_lo, prev_hi, tok, n, parent_cached, st, kernel: str):
     (decode.hip): full range -> C[c], C[c+1] + the C-block's cache id (2 lines);
     <= 512 rows -> E[lo, hi) (8 B per row); 513..kScanMax uncached rows
     (k_decode only) -> E[lo, hi); a range the transition table serves (a cached
-    parent) -> its 16-slot probe (384 B); otherwise the 2-level wavelet-matrix
+    parent) -> its 16-slot probe (2 x 128 B) + the line of the parent's own cache
+    entry, whose id the slots' keys hold (320 B); otherwise the 2-level wavelet-matrix
     descent: D2[c] + Z per level, and per level and endpoint the superblock
     count, the block header entry and the block prefix up to the position
     (level 0 exact from the position; level 1's position is data-dependent: its
@@ -237,9 +238,9 @@ def lf_plan_bytes(prev_lo, prev_hi, tok, n, parent_cached, st, kernel: str):
         rest &= ~narrow
     probe = rest & trans & (w >= cmin)
     hit = probe & pc
-    out[hit] = 384
+    out[hit] = 320
     desc = rest & ~hit
-    b = 384 * probe.astype(np.int64) + 3 * 64                # D2[c], Z[0][d0], Z[1][d1]
+    b = 320 * probe.astype(np.int64) + 3 * 64                # D2[c], Z[0][d0], Z[1][d1]
     for pos in (lo, hi):
         b = b + 2 * 64 + 64 * ((2 * (pos % 1024) + 63) // 64)  # level 0: sb + header + uint16 prefix
         b = b + 2 * 64 + 64 * ((512 + 63) // 64)             # level 1: sb + header + uint8 prefix (expected)

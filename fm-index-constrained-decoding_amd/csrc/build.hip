@@ -370,8 +370,8 @@ int device_build_from_bwt(Index* h, const uint32_t* d_bwt, uint64_t n, hipStream
   }
   // the range-cache table packs hi below a 34-bit id shift and the transition
   // slots pack child start / width in 34 bits: positions must fit 34 bits
-  static_assert(kCacheIdShift == 34 && kTransSymShift == 34, "position packing");
-  static_assert(kMaxSymBits <= 30, "transition key packs the symbol above bit 34");
+  static_assert(kCacheIdShift == 34 && kMask34 == (1ull << 34) - 1, "position packing");
+  static_assert(kTSymShift + 18 == 38, "transition key: 20-bit parent id, 18-bit symbol (wider ones left out)");
   if (n >= (1ull << 34)) {
     set_error("n = %llu rows: the index packs row positions in 34 bits (n < 2^34)", (unsigned long long)n);
     return -1;

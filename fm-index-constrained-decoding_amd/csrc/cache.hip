@@ -89,37 +89,50 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
                                                       uint64_t* __restrict__ tab, uint64_t cap,
                                                       uint32_t* __restrict__ fill,
                                                       unsigned long long* __restrict__ stats) {
+  __shared__ uint64_t s_pid;
   const uint64_t r = blockIdx.x;
   if (r >= m) return;
   const uint64_t kr = k[r];
   if (kr == ~0ull) return;
   const uint64_t lo = plo[r], hi = phi[r], base = off[r];
+  if (threadIdx.x == 0) s_pid = cache_id_thread(v, lo, hi);   // the parent's cache id + 1 (0: not cached)
+  __syncthreads();
+  const uint64_t pid1 = s_pid;
   unsigned long long ins = 0, drop = 0;
   for (uint64_t j = threadIdx.x; j < kr; j += 256) {
     const uint64_t c = syms[base + j], cw = cnt[base + j], clo = child[base + j];
-    uint64_t aux = 0;
+    // kind / aux: a cached child's cache id, a one-row child's only symbol, else the range alone
+    uint64_t kind = 0, aux = 0;
     if (cw >= v.cache_min) {
-      aux = cache_id_thread(v, clo, clo + cw);
+      const uint64_t id1 = cache_id_thread(v, clo, clo + cw);
+      if (id1 && id1 - 1 < kTAuxLimit) {
+        kind = kTKindCached;
+        aux = id1 - 1;
+      }
     } else if (cw == 1) {
       const uint64_t sym = bwt_sym(v, clo);
-      if (sym < kTransOne) aux = kTransOne | sym;
+      if (sym < kTAuxLimit) {
+        kind = kTKindOne;
+        aux = sym;
+      }
     }
-    const uint64_t w0 = lo | (c << kTransSymShift);
-    const uint64_t w1 = hi | ((clo & ((1ull << 30) - 1)) << kTransSymShift);
-    const uint64_t w2 = (clo >> 30) | (cw << 4) | (aux << 38);
+    // a key the slot cannot hold (a parent outside the cache or past 2^20 - 2 ids, a symbol of 18+
+    // bits) is left out: the descent serves it
+    const bool fits = pid1 && pid1 - 1 < kTPidNone && c < kTSymLimit;
+    const uint64_t w0 = trans_key(fits ? pid1 - 1 : 0, c) | (kind << 38) | ((clo & ((1ull << 24) - 1)) << 40);
+    const uint64_t w1 = (clo >> 24) | (cw << 10) | (aux << 44);
     const TransHome th = trans_home(lo, hi, c, cap);
     const uint64_t ba = th.a / kTransBucket, bb = th.b / kTransBucket;
     const bool a_first = __hip_atomic_load(fill + ba, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
                          __hip_atomic_load(fill + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool done = false;
-    for (uint32_t t = 0; t < 2 && !done; ++t) {
+    for (uint32_t t = 0; t < 2 && !done && fits; ++t) {
       const uint64_t bk = (t == 0) == a_first ? ba : bb;
       const uint32_t k = atomicAdd(fill + bk, 1u);
       if (k < kTransBucket) {
-        uint64_t* p = tab + 3 * (bk * kTransBucket + k);
+        uint64_t* p = tab + 2 * (bk * kTransBucket + k);
         p[0] = w0;
         p[1] = w1;
-        p[2] = w2;
         done = true;
       }
     }
@@ -210,18 +223,18 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
     return nb * kTransBucket;
   };
   uint64_t cap = slots_for(entries);
-  if (cap * 24 > budget && min_count < v.cache_min) {   // over budget: the cached children only
+  if (cap * kTransSlotBytes > budget && min_count < v.cache_min) {   // over budget: the cached children only
     min_count = v.cache_min;
     if (pass(min_count, nullptr, 0, nullptr, entries, nullptr)) return -1;
     cap = slots_for(entries);
   }
-  if (entries == 0 || cap * 24 > budget) return 0;
+  if (entries == 0 || cap * kTransSlotBytes > budget) return 0;
   uint64_t* tab = nullptr;
-  if (hipMalloc(reinterpret_cast<void**>(&tab), cap * 24) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&tab), cap * kTransSlotBytes) != hipSuccess) {
     (void)hipGetLastError();
     return 0;   // no room: the descent serves every step
   }
-  FM_HIP(hipMemsetAsync(tab, 0xFF, cap * 24, s));
+  FM_HIP(hipMemsetAsync(tab, 0xFF, cap * kTransSlotBytes, s));
   DBuf<unsigned long long> d_stats;
   DBuf<uint32_t> d_fill;   // per-bucket fill counts, for the insert only
   if (d_stats.alloc(2) || d_fill.alloc(cap / kTransBucket)) {
@@ -243,8 +256,8 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   h->trans_tab = tab;
   h->trans_entries = st[0];
   h->trans_dropped = st[1];
-  h->trans_bytes = cap * 24;
-  h->cache_bytes += cap * 24;
+  h->trans_bytes = cap * kTransSlotBytes;
+  h->cache_bytes += cap * kTransSlotBytes;
   v.trans_tab = tab;
   v.trans_cap = cap;
   return 0;

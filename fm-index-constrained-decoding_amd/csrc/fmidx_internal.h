@@ -73,7 +73,7 @@ struct DevView {
   // transition table of the cached ranges: (cached parent P, symbol c) ->
   // LF_c(P) for every symbol c occurring in P (or, under a memory budget, only
   // the cached children), with the child's bitmap id or, for a one-row child,
-  // its only symbol; 3 words per slot (layout at kTransSymShift below)
+  // its only symbol; 2 words per slot, keyed by the parent's cache id (layout at trans_key below)
   const uint64_t* trans_tab;
   uint64_t trans_cap;         // slots; 0 = none
   const uint32_t* cblock;     // per symbol c: cache id + 1 of its C-block [C[c], C[c+1]) (0 = not cached), or null
@@ -492,24 +492,37 @@ __host__ __device__ __forceinline__ uint64_t trans_hash(uint64_t lo, uint64_t hi
   return cache_hash(lo ^ (c * 0xD6E8FEB86659FD93ull), hi + c);
 }
 
-// Transition slot (24 B) in buckets of kTransBucket slots, two-choice
-// hashing: a key sits in one of the 8 slots of its bucket A or of its bucket B
-// (k_trans_insert fills the emptier of the two; a key finding both full is
-// left out and takes the descent).  A bucket is 192 B (64-B aligned: two 128-B
-// lines), so a probe reads the same 16 slots / 384 B / 4 lines as a 16-slot
-// linear-probing run did, while the table runs at load 0.85 with about as few
-// left-out keys as linear probing had at 0.57 (0.15 % vs 0.12 % simulated;
-// C3: 45.2 -> 30.4 GiB).
-//   w0 = plo | c << 34                       (empty: ~0)
-//   w1 = phi | (clo & (2^30 - 1)) << 34
-//   w2 = clo >> 30 | cw << 4 | aux << 38      aux: 0, cache id + 1 of the child,
-//                                             or kTransOne | the child's only symbol
-constexpr uint32_t kTransSymShift = 34;
-constexpr uint64_t kMask34 = (1ull << 34) - 1;
-constexpr uint64_t kTransOne = 1ull << 25;
+// Transition slot (16 B) in buckets of kTransBucket = 8 slots -- 128 B, one line -- with two-choice
+// hashing: a key sits in one of the 8 slots of its bucket A or of its bucket B (k_trans_insert fills
+// the emptier of the two; a key finding both full is left out and takes the descent), so a probe
+// reads 16 slots in two 128-B lines.  The key is (the parent's CACHE ID, symbol): every parent is a
+// cached range, and a probe reads the parent's range-cache run in the same round trip, so its id is
+// there to compare with (the round-5 slot kept the parent's (lo, hi) itself: 24 B).
+//   w0 = pid | c << 20 | kind << 38 | (clo & (2^24 - 1)) << 40        (empty slot: ~0)
+//   w1 = clo >> 24 | cw << 10 | aux << 44
+// kind 0: the child range [clo, clo + cw) alone; 1: aux = its only symbol (a one-row child);
+// 2: aux = its cache id (a cached child: its bitmap).  pid < 2^20 - 1 (kTPidNone is the empty
+// slot's), c < 2^18, aux < 2^20: keys outside these are left out (the descent).
+constexpr uint32_t kTSymShift = 20;
+constexpr uint64_t kTPidNone = (1ull << 20) - 1;
+constexpr uint64_t kTSymLimit = 1ull << 18;
+constexpr uint64_t kTKeyMask = (1ull << 38) - 1;
+constexpr uint32_t kTKindOne = 1, kTKindCached = 2;
+constexpr uint64_t kTAuxLimit = 1ull << 20;
 constexpr uint32_t kTransBucket = 8;
 constexpr uint32_t kTransProbe = 2 * kTransBucket;   // a key's candidate slots: bucket A's, then bucket B's
 constexpr uint64_t kTransEmpty = ~0ull;
+constexpr uint64_t kTransSlotBytes = 16;
+constexpr uint64_t kMask34 = (1ull << 34) - 1;
+
+__host__ __device__ __forceinline__ uint64_t trans_key(uint64_t pid, uint64_t c) { return pid | (c << kTSymShift); }
+__host__ __device__ __forceinline__ bool trans_match(uint64_t w0, uint64_t key) { return (w0 & kTKeyMask) == key; }
+__host__ __device__ __forceinline__ uint64_t trans_clo(uint64_t w0, uint64_t w1) {
+  return (w0 >> 40) | ((w1 & 0x3FFull) << 24);
+}
+__host__ __device__ __forceinline__ uint64_t trans_cw(uint64_t w1) { return (w1 >> 10) & kMask34; }
+__host__ __device__ __forceinline__ uint32_t trans_kind(uint64_t w0) { return (uint32_t)((w0 >> 38) & 3u); }
+__host__ __device__ __forceinline__ uint64_t trans_aux(uint64_t w1) { return w1 >> 44; }
 
 __host__ __device__ __forceinline__ uint64_t mul_hi64(uint64_t a, uint64_t b) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -582,46 +595,52 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   const uint32_t q = lane & 31u;
   const bool side = lane >= 32;
   const uint64_t c = (uint64_t)sym;
-  // (1) transition probe of a cached range: its 16 candidate slots x 3 words,
-  // one word per lane 0-47; lanes 48-63 read the parent's own home run in the range cache
-  // (8 slots x 2 words), in the same round trip
+  // (1) transition probe of a cached range: its 16 candidate slots x 2 words, one word per lane
+  // 0-31; lanes 32-63 read the parent's own home run in the range cache (16 slots x 2 words) in
+  // the same round trip -- the parent's cache id, which the slots' keys hold
   const bool probe = v.trans_cap && hi - lo >= v.cache_min;
-  const uint64_t key0 = lo | (c << kTransSymShift);
   uint64_t tw = kTransEmpty;
-  if (probe && lane < 3 * kTransProbe) {
-    const uint64_t slot = trans_slot(trans_home(lo, hi, c, v.trans_cap), lane / 3);
-    tw = v.trans_tab[3 * slot + lane % 3];
+  if (probe && lane < 2 * kTransProbe) {
+    const uint64_t slot = trans_slot(trans_home(lo, hi, c, v.trans_cap), lane / 2);
+    tw = v.trans_tab[2 * slot + (lane & 1u)];
   } else if (probe && v.cache_mask) {
-    const uint32_t k = lane - 3 * kTransProbe;
+    const uint32_t k = lane - 2 * kTransProbe;
     tw = v.cache_tab[2 * ((cache_hash(lo, hi) + k / 2) & v.cache_mask) + (k & 1)];
   }
+  // the parent's cache id (kTPidNone: not in the run read -- no key can match, the descent serves)
+  auto parent_id = [&](uint64_t w1n) -> uint64_t {
+    const uint64_t bc = __ballot(lane >= 2 * kTransProbe && (lane & 1u) == 0 && tw == lo && (w1n & kMask34) == hi);
+    return bc ? __shfl(w1n, __ffsll((long long)bc) - 1, 64) >> kCacheIdShift : kTPidNone;
+  };
+  // a hit: the child's range, and its bitmap (cached) or only symbol
+  auto take_hit = [&](uint64_t bh) {
+    const int src = __ffsll((long long)bh) - 1;
+    const uint64_t w0 = __shfl(tw, src, 64), w1 = __shfl(tw, src + 1, 64);
+    const uint64_t clo = trans_clo(w0, w1);
+    lo = clo;
+    hi = clo + trans_cw(w1);
+    const uint32_t kind = trans_kind(w0);
+    if (kind == kTKindOne)
+      one = (int64_t)trans_aux(w1);
+    else if (kind == kTKindCached)
+      cbm = v.cache_bm + trans_aux(w1) * v.bm_words;
+  };
   // A probe miss is a symbol the parent lacks -- or one of the few keys the
   // table left out.  The parent's cached bitmap tells which: its word for c
   // is loaded with the descent's first level, and an absent c ends the step
   // there (one round trip after the probe instead of the whole descent).
   uint32_t pword = ~0u;
-  if (probe && v.probe_first) {   // the probe alone: one round trip of 384 B for a hit
+  if (probe && v.probe_first) {   // the probe alone: one round trip of 256 B + the run for a hit
     const uint64_t w1n = __shfl_down(tw, 1, 64);
-    const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
+    const uint64_t pid = parent_id(w1n);
+    const uint64_t key = trans_key(pid, c);
+    const uint64_t bh = __ballot(lane < 2 * kTransProbe && (lane & 1u) == 0 && pid != kTPidNone &&
+                                 trans_match(tw, key));
     if (bh) {
-      const int src = __ffsll((long long)bh) - 1;
-      const uint64_t w1 = __shfl(tw, src + 1, 64), w2 = __shfl(tw, src + 2, 64);
-      const uint64_t clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
-      const uint64_t aux = w2 >> 38;
-      lo = clo;
-      hi = clo + ((w2 >> 4) & kMask34);
-      if (aux & kTransOne)
-        one = (int64_t)(aux & (kTransOne - 1));
-      else if (aux)
-        cbm = v.cache_bm + (aux - 1) * v.bm_words;
+      take_hit(bh);
       return;
     }
-    const uint64_t bc = __ballot(lane >= 3 * kTransProbe && ((lane - 3 * kTransProbe) & 1u) == 0 && tw == lo &&
-                                 (w1n & kMask34) == hi);
-    if (bc) {
-      const uint64_t pid = __shfl(w1n, __ffsll((long long)bc) - 1, 64) >> kCacheIdShift;
-      pword = v.cache_bm[pid * v.bm_words + (c32 >> 5)];
-    }
+    if (pid != kTPidNone) pword = v.cache_bm[pid * v.bm_words + (c32 >> 5)];
   }
   // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
@@ -641,18 +660,12 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
     }
     if (l == 0 && probe && !v.probe_first) {   // the probe's loads were issued before this level's
       const uint64_t w1n = __shfl_down(tw, 1, 64);
-      const uint64_t bh = __ballot(lane < 3 * kTransProbe && lane % 3 == 0 && tw == key0 && (w1n & kMask34) == hi);
+      const uint64_t pid = parent_id(w1n);
+      const uint64_t key = trans_key(pid, c);
+      const uint64_t bh = __ballot(lane < 2 * kTransProbe && (lane & 1u) == 0 && pid != kTPidNone &&
+                                   trans_match(tw, key));
       if (bh) {
-        const int src = __ffsll((long long)bh) - 1;
-        const uint64_t w1 = __shfl(tw, src + 1, 64), w2 = __shfl(tw, src + 2, 64);
-        const uint64_t clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
-        const uint64_t aux = w2 >> 38;
-        lo = clo;
-        hi = clo + ((w2 >> 4) & kMask34);
-        if (aux & kTransOne)
-          one = (int64_t)(aux & (kTransOne - 1));
-        else if (aux)
-          cbm = v.cache_bm + (aux - 1) * v.bm_words;
+        take_hit(bh);
         return;
       }
     }

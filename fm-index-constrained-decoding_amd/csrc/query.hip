@@ -90,32 +90,27 @@ __global__ void __launch_bounds__(kLfThreads) k_search(DevView v, const int64_t*
 // wave-packed scan of group_step (one load per entry actually needed).
 constexpr uint64_t kPackMax = 128;
 
-// Transition probe of a wave's cached rows eight at a time (8 lanes per row):
-// the row's two 192-B buckets as three 16-B loads per lane (128 B contiguous
-// per row and instruction) staged through LDS, and (CE) the range's own
-// range-cache run alongside.  Used by get_range (group_step<P8>) and the
-// opt-in LF sweep (k_lf_sweep).
+// Transition probe of a wave's cached rows eight at a time (8 lanes per row): lane sl of a row's
+// segment loads slot sl of its bucket A and slot sl of its bucket B (16-B slots: the two 128-B
+// lines) and (CE) slot sl of the range's own range-cache run -- the parent's cache id, which the
+// slots' keys hold.  Used by get_range (group_step<P8>) and the LF sweep (sweep_head).
 constexpr uint32_t kProbeLanes = 8;
 constexpr uint32_t kProbeRows = 64 / kProbeLanes;
-constexpr uint32_t kProbeChunks = 24;   // 16-B chunks staged per probe row (two buckets of 12)
 
 // Transition probe of up to eight rows (8 lanes each; row k of the batch =
 // the wave's lane src[k], src < 0: none) -- loads only; probe_finish consumes.
 struct ProbeLoads {
-  uint4 c0, c1, c2;       // 16-B chunks sl, sl + 8, sl + 16 of the row's 24 (bucket A's 12, then B's)
+  uint4 ca, cb;           // slot sl of bucket A, slot sl of bucket B
   uint4 ce;               // the range's own range-cache slot sl
 };
 template <bool CE = true>
 __device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, uint64_t h, uint64_t c) {
   const uint32_t sl = (threadIdx.x & 63u) % kProbeLanes;
   const TransHome th = trans_home(l, h, c, v.trans_cap);
-  // chunk i < 12 of bucket A at 24 a / 16 + i, chunk i >= 12 of bucket B
   const uint4* tt = reinterpret_cast<const uint4*>(v.trans_tab);
-  const uint64_t ca = (24 * th.a) >> 4, cb = ((24 * th.b) >> 4) - 12;
   ProbeLoads p;
-  p.c0 = tt[ca + sl];                                                        // chunks 0 .. 7
-  p.c1 = tt[sl < 4 ? ca + 8 + sl : cb + 8 + sl];                             // 8 .. 15
-  p.c2 = tt[cb + 16 + sl];                                                   // 16 .. 23
+  p.ca = tt[th.a + sl];
+  p.cb = tt[th.b + sl];
   // the range's own range-cache run (8 slots, one per lane)
   if (CE) {
     const uint64_t cs = (cache_hash(l, h) + sl) & v.cache_mask;
@@ -127,45 +122,33 @@ __device__ __forceinline__ ProbeLoads probe_issue(const DevView& v, uint64_t l, 
 }
 
 // -> per lane: hit (and the child range on the row's first lane), or the
-// range's cache id + 1 (0: not found) for the tail entry of a miss
+// range's cache id + 1 (0: not found) for the tail entry of a miss.  Without
+// the range's cache id among the 8 run slots read no key can match: a miss.
 template <bool CE = true>
 __device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint64_t h, uint64_t c, bool act,
-                                            const ProbeLoads& p, uint4* s_run, bool& hit_row, uint64_t& clo,
+                                            const ProbeLoads& p, uint4* /*s_run*/, bool& hit_row, uint64_t& clo,
                                             uint64_t& chi, uint64_t& pid1) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t seg = lane / kProbeLanes, sl = lane % kProbeLanes;
-  uint4* sr = s_run + seg * kProbeChunks + sl;
-  sr[0] = p.c0;
-  sr[kProbeLanes] = p.c1;
-  sr[2 * kProbeLanes] = p.c2;
-  __builtin_amdgcn_wave_barrier();
-  const uint64_t* run = reinterpret_cast<const uint64_t*>(&s_run[seg * kProbeChunks]);   // the 16 candidates
-  const uint64_t key0 = l | (c << kTransSymShift);
-  bool hit = false;
-  uint64_t w1 = 0, w2 = 0;
-#pragma unroll
-  for (uint32_t u = 0; u < 2; ++u) {
-    const uint32_t slot = 2 * sl + u;
-    const uint64_t x0 = run[3 * slot], x1 = run[3 * slot + 1], x2 = run[3 * slot + 2];
-    const bool mt = x0 == key0 && (x1 & kMask34) == h;
-    hit |= mt;
-    w1 = mt ? x1 : w1;
-    w2 = mt ? x2 : w2;
-  }
-  __builtin_amdgcn_wave_barrier();   // a later batch's staging overwrites s_run
+  const uint32_t seg = lane / kProbeLanes;
   const uint64_t klo = (uint64_t)p.ce.x | ((uint64_t)p.ce.y << 32);
   const uint64_t khi = (uint64_t)p.ce.z | ((uint64_t)p.ce.w << 32);
   const bool pc = CE && v.cache_mask && klo == l && (khi & kMask34) == h;
   const uint64_t segm = 0xFFull << (kProbeLanes * seg);
-  const uint64_t hb = __ballot(act && hit) & segm, pb = __ballot(act && pc) & segm;
-  const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
-  const uint64_t hw1 = __shfl(w1, hl, 64), hw2 = __shfl(w2, hl, 64);
+  const uint64_t pb = __ballot(act && pc) & segm;
   const int pl = pb ? __ffsll((long long)pb) - 1 : (int)lane;
-  const uint64_t pk = __shfl(khi, pl, 64);
+  const uint64_t pid = pb ? (__shfl(khi, pl, 64) >> kCacheIdShift) : kTPidNone;
+  const uint64_t key = trans_key(pid, c);
+  const uint64_t a0 = (uint64_t)p.ca.x | ((uint64_t)p.ca.y << 32), a1 = (uint64_t)p.ca.z | ((uint64_t)p.ca.w << 32);
+  const uint64_t b0 = (uint64_t)p.cb.x | ((uint64_t)p.cb.y << 32), b1 = (uint64_t)p.cb.z | ((uint64_t)p.cb.w << 32);
+  const bool ma = pid != kTPidNone && trans_match(a0, key), mb = pid != kTPidNone && trans_match(b0, key);
+  const uint64_t w0 = ma ? a0 : b0, w1 = ma ? a1 : b1;
+  const uint64_t hb = __ballot(act && (ma || mb)) & segm;
+  const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
+  const uint64_t hw0 = __shfl(w0, hl, 64), hw1 = __shfl(w1, hl, 64);
   hit_row = hb != 0;
-  clo = (hw1 >> kTransSymShift) | ((hw2 & 0xFu) << 30);
-  chi = clo + ((hw2 >> 4) & kMask34);
-  pid1 = pb ? (pk >> kCacheIdShift) + 1 : 0;
+  clo = trans_clo(hw0, hw1);
+  chi = clo + trans_cw(hw1);
+  pid1 = pb ? pid + 1 : 0;
 }
 
 
@@ -228,19 +211,27 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
   // C lookup (full-range rows only) and (GP) the group's transition probe, issued together
   const uint64_t cf = full ? c : 0;
   const uint64_t ca = v.C[cf], cb = v.C[cf + 1];
-  uint64_t pw[GP ? 3 * (16 / G) : 1];
-  const bool probe = GP && wide && v.trans_cap && h - l >= v.cache_min;
+  uint64_t pw[GP ? 2 * (16 / G) : 1];
+  uint64_t pe[GP ? 2 * (16 / G) : 1];
+  const bool probe = GP && wide && v.trans_cap && v.cache_mask && h - l >= v.cache_min;
   if (GP) {
-    // the 16-slot probe of lf_step_decode, 16 / G slots (3 words each) per lane;
-    // unconditional loads (slot 0 for rows that do not probe; C[0..2] when
-    // the index has no transition table)
-    const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;
+    // the 16-slot probe of lf_step_decode, 16 / G slots (2 words each) per lane, and as many slots
+    // of the range's own range-cache run (the parent's cache id, which the keys hold);
+    // unconditional loads (slot 0 for rows that do not probe; C[0..1] when the index has no
+    // transition table or cache)
+    const uint64_t* tt = probe ? v.trans_tab : v.C;
+    const uint64_t* ct = probe ? v.cache_tab : v.C;
     const TransHome th = probe ? trans_home(l, h, c, v.trans_cap) : TransHome{0, 0};
+    const uint64_t ch = probe ? cache_hash(l, h) : 0;
 #pragma unroll
     for (int k = 0; k < 16 / G; ++k) {
       const uint64_t slot_k = probe ? trans_slot(th, j * (16 / G) + k) : 0;
+      const uint64_t cs_k = probe ? ((ch + j * (16 / G) + k) & v.cache_mask) : 0;
 #pragma unroll
-      for (int w = 0; w < 3; ++w) pw[3 * k + w] = tt[3 * slot_k + w];
+      for (int w = 0; w < 2; ++w) {
+        pw[2 * k + w] = tt[2 * slot_k + w];
+        pe[2 * k + w] = ct[2 * cs_k + w];
+      }
     }
   }
   // ---- the wave-packed E scan of the narrow rows
@@ -310,7 +301,6 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
   if (P8) {
     // cached wide rows eight per round trip; a hit settles the row, a miss (a
     // symbol the range lacks, or a key the table left out) stays wide
-    __shared__ uint4 s_run8[kLfThreads / 64][kProbeRows * kProbeChunks];
     const uint32_t seg = lane / kProbeLanes;
     uint64_t pm = __ballot(wide && j == 0 && v.trans_cap && h - l >= v.cache_min);
     while (pm) {   // wave-uniform
@@ -323,10 +313,10 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
       const bool act = src >= 0;
       const int ps = act ? src : 0;
       const uint64_t pl = __shfl(l, ps, 64), ph = __shfl(h, ps, 64), pc = __shfl(c, ps, 64);
-      const ProbeLoads pld = probe_issue<false>(v, pl, ph, pc);
+      const ProbeLoads pld = probe_issue<true>(v, pl, ph, pc);
       bool hit;
       uint64_t clo, chi, p1;
-      probe_finish<false>(v, pl, ph, pc, act, pld, s_run8[wv], hit, clo, chi, p1);
+      probe_finish<true>(v, pl, ph, pc, act, pld, nullptr, hit, clo, chi, p1);
 #pragma unroll
       for (uint32_t k = 0; k < kProbeRows; ++k) {
         const int sk = __shfl(src, (int)(k * kProbeLanes), 64);
@@ -341,14 +331,21 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     }
   }
   if (GP) {   // a probe hit (at most one slot of the group holds the key) ends a wide row's step
-    const uint64_t key0 = l | (c << kTransSymShift);
+    // the parent's cache id from the group's run slots (id + 1; 0: not among them -- no hit)
+    uint64_t pid1 = 0;
+#pragma unroll
+    for (int k = 0; k < 16 / G; ++k)
+      pid1 |= (probe && pe[2 * k] == l && (pe[2 * k + 1] & kMask34) == h) ? (pe[2 * k + 1] >> kCacheIdShift) + 1 : 0;
+#pragma unroll
+    for (int d = 1; d < G; d <<= 1) pid1 |= __shfl_xor(pid1, d, 64);
+    const uint64_t key = trans_key(pid1 ? pid1 - 1 : kTPidNone, c);
     uint64_t hit = 0, clo = 0, cw = 0;
 #pragma unroll
     for (int k = 0; k < 16 / G; ++k) {
-      const bool m = probe && pw[3 * k] == key0 && (pw[3 * k + 1] & kMask34) == h;
+      const bool m = probe && pid1 && trans_match(pw[2 * k], key);
       hit |= m ? 1u : 0u;
-      clo |= m ? ((pw[3 * k + 1] >> kTransSymShift) | ((pw[3 * k + 2] & 0xFu) << 30)) : 0;
-      cw |= m ? ((pw[3 * k + 2] >> 4) & kMask34) : 0;
+      clo |= m ? trans_clo(pw[2 * k], pw[2 * k + 1]) : 0;
+      cw |= m ? trans_cw(pw[2 * k + 1]) : 0;
     }
 #pragma unroll
     for (int d = 1; d < G; d <<= 1) {
@@ -372,7 +369,8 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     const bool elig = wide && ((v.E && h - l <= 128) || (v.trans_cap && h - l >= v.cache_min));
     uint64_t qb = __ballot(elig && j == 0);
     uint64_t keep = __ballot(wide && !elig && j == 0);
-    const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;   // C[0..2]: a valid dummy address
+    const uint64_t* tt = v.trans_cap ? v.trans_tab : v.C;   // C[0..1]: a valid dummy address
+    const uint64_t* ct = v.cache_mask ? v.cache_tab : v.C;
     while (qb) {
       int sv[4];
 #pragma unroll
@@ -389,7 +387,10 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
       const bool qscan = act && v.E && qh - ql <= 128;
       const bool qprobe = act && !qscan && v.trans_cap && qh - ql >= v.cache_min;
       const uint64_t slot = qprobe ? trans_slot(trans_home(ql, qh, qc, v.trans_cap), sl) : 0;
-      const uint64_t p0 = tt[3 * slot], p1 = tt[3 * slot + 1], p2 = tt[3 * slot + 2];
+      const uint64_t p0 = tt[2 * slot], p1 = tt[2 * slot + 1];
+      // slot sl of the range's own range-cache run: the parent's cache id
+      const uint64_t cslot = (qprobe && v.cache_mask) ? ((cache_hash(ql, qh) + sl) & v.cache_mask) : 0;
+      const uint64_t e0 = ct[2 * cslot], e1 = ct[2 * cslot + 1];
       uint64_t qe[8];
 #pragma unroll
       for (uint32_t k = 0; k < 8; ++k) {
@@ -423,10 +424,12 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
           lmx = xl;
         }
       }
-      const uint64_t key0 = ql | (qc << kTransSymShift);
-      const uint64_t hb = __ballot(qprobe && p0 == key0 && (p1 & kMask34) == qh) & (0xFFFFull << (16 * seg));
+      const uint64_t segm = 0xFFFFull << (16 * seg);
+      const uint64_t pb = __ballot(qprobe && v.cache_mask && e0 == ql && (e1 & kMask34) == qh) & segm;
+      const uint64_t qpid = pb ? (__shfl(e1, __ffsll((long long)pb) - 1, 64) >> kCacheIdShift) : kTPidNone;
+      const uint64_t hb = __ballot(qprobe && pb && trans_match(p0, trans_key(qpid, qc))) & segm;
       const int hl = hb ? __ffsll((long long)hb) - 1 : 0;
-      const uint64_t w1 = __shfl(p1, hl, 64), w2 = __shfl(p2, hl, 64);
+      const uint64_t w0 = __shfl(p0, hl, 64), w1 = __shfl(p1, hl, 64);
       uint64_t rlo = 0, rhi = 0;
       int done = 0;
       if (qscan) {
@@ -434,8 +437,8 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
         rhi = fmx ? lmx + 1 : 0;
         done = 1;
       } else if (qprobe && hb) {
-        rlo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
-        rhi = rlo + ((w2 >> 4) & kMask34);
+        rlo = trans_clo(w0, w1);
+        rhi = rlo + trans_cw(w1);
         done = 1;
       }
       // hand each row's result to its group (the loop and sv[] are wave-uniform)
@@ -992,7 +995,6 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
                                                         const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                                                         uint64_t m, LfWork* lt, uint32_t* cnt, uint64_t cap) {
   __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
-  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
   __shared__ uint32_t s_n[kLfThreads / 64 + 1];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = threadIdx.x >> 6;
@@ -1000,7 +1002,7 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
   // (no early return: every wave of the workgroup reaches the append's barriers)
   const bool valid = i < m;
   SweepRow r;
-  sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], s_run[wv], r);
+  sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], nullptr, r);
   if (INLINE) {
 #if FMIDX_SWEEP_TAIL_BATCH
     sweep_tails(v, s_mm[wv], r);
@@ -1107,7 +1109,6 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
                                                           const uint64_t* hi_in, uint64_t* lo_out, uint64_t* hi_out,
                                                           uint64_t m, PersistWs ws, uint32_t qcap, uint32_t epoch) {
   __shared__ unsigned long long s_mm[kLfThreads / 64][2][64];
-  __shared__ uint4 s_run[kLfThreads / 64][kProbeRows * kProbeChunks];
   typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = threadIdx.x >> 6;
@@ -1124,7 +1125,7 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
     const uint64_t i = chunk * 64 + lane;
     const bool valid = i < m;
     SweepRow r;
-    sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], s_run[wv], r);
+    sweep_head(v, tok, shift, reset_below, lo_in, hi_in, m, i, valid, s_mm[wv], nullptr, r);
     const bool tail = valid && r.tail;
     if (valid && !tail) {
       lo_out[i] = r.nl;
@@ -1556,17 +1557,16 @@ constexpr uint32_t kDcWords = 256;
 
 // the child of (lo, hi) by symbol c: a scan of its candidate slots from
 // candidate d0 on (the caller has checked the others)
-__device__ __forceinline__ void child_of(const DevView& v, uint64_t lo, uint64_t hi, uint32_t c, uint32_t d0,
-                                         uint64_t& clo, uint64_t& cnt) {
-  const uint64_t key0 = lo | ((uint64_t)c << kTransSymShift);
+__device__ __forceinline__ void child_of(const DevView& v, uint64_t pid, uint64_t lo, uint64_t hi, uint32_t c,
+                                         uint32_t d0, uint64_t& clo, uint64_t& cnt) {
+  const uint64_t key = trans_key(pid, c);
   const TransHome th = trans_home(lo, hi, c, v.trans_cap);
-  for (uint32_t d = d0; d < kTransProbe; ++d) {
+  for (uint32_t d = d0; d < kTransProbe && pid < kTPidNone && c < kTSymLimit; ++d) {
     const uint64_t slot = trans_slot(th, d);
-    const uint64_t w0 = v.trans_tab[3 * slot], w1 = v.trans_tab[3 * slot + 1];
-    if (w0 == key0 && (w1 & kMask34) == hi) {
-      const uint64_t w2 = v.trans_tab[3 * slot + 2];
-      clo = (w1 >> kTransSymShift) | ((w2 & 0xFu) << 30);
-      cnt = (w2 >> 4) & kMask34;
+    const uint64_t w0 = v.trans_tab[2 * slot], w1 = v.trans_tab[2 * slot + 1];
+    if (trans_match(w0, key)) {
+      clo = trans_clo(w0, w1);
+      cnt = trans_cw(w1);
       return;
     }
     // a bucket fills from its first slot and is never emptied: an empty slot ends it
@@ -1600,6 +1600,8 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
   const bool fullr = lo == 0 && hi == v.n;
   const uint32_t* bm = fullr ? v.bm_full : cache_find(v, lo, hi);
   if (!bm) return;
+  // the range's cache id: the key of its transition slots
+  const uint64_t pid = fullr ? kTPidNone : (uint64_t)(bm - v.cache_bm) / v.bm_words;
   const uint64_t base = cap_off[row];
   const uint64_t cap = cap_off[row + 1] - base;
   const uint32_t W = v.bm_words;
@@ -1639,17 +1641,17 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
       }
     }
     // the first slot of both buckets of every symbol, issued together
-    uint64_t q[4][6];
+    uint64_t q[4][4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool pr = !fullr && u < nb;
       const TransHome th = pr ? trans_home(lo, hi, cs[u], v.trans_cap) : TransHome{0, 0};
       const uint64_t a = th.a, b = th.b;
-      const uint64_t* tt = pr ? v.trans_tab : v.C;   // C[0..2]: a valid dummy address
+      const uint64_t* tt = pr ? v.trans_tab : v.C;   // C[0..1]: a valid dummy address
 #pragma unroll
-      for (int w = 0; w < 3; ++w) {
-        q[u][w] = tt[3 * a + w];
-        q[u][3 + w] = tt[3 * b + w];
+      for (int w = 0; w < 2; ++w) {
+        q[u][w] = tt[2 * a + w];
+        q[u][2 + w] = tt[2 * b + w];
       }
     }
 #pragma unroll
@@ -1660,20 +1662,21 @@ __global__ void __launch_bounds__(256) k_distinct_cached(DevView v, const uint64
           clo = v.C[cs[u]];
           cnt = v.C[cs[u] + 1] - clo;
         } else {
-          const uint64_t key0 = lo | ((uint64_t)cs[u] << kTransSymShift);
-          if (q[u][0] == key0 && (q[u][1] & kMask34) == hi) {
-            clo = (q[u][1] >> kTransSymShift) | ((q[u][2] & 0xFu) << 30);
-            cnt = (q[u][2] >> 4) & kMask34;
-          } else if (q[u][3] == key0 && (q[u][4] & kMask34) == hi) {
-            clo = (q[u][4] >> kTransSymShift) | ((q[u][5] & 0xFu) << 30);
-            cnt = (q[u][5] >> 4) & kMask34;
-          } else if (q[u][0] == kTransEmpty && q[u][3] == kTransEmpty) {
+          const bool keyed = pid < kTPidNone && cs[u] < kTSymLimit;
+          const uint64_t key = trans_key(pid, cs[u]);
+          if (keyed && trans_match(q[u][0], key)) {
+            clo = trans_clo(q[u][0], q[u][1]);
+            cnt = trans_cw(q[u][1]);
+          } else if (keyed && trans_match(q[u][2], key)) {
+            clo = trans_clo(q[u][2], q[u][3]);
+            cnt = trans_cw(q[u][3]);
+          } else if (!keyed || (q[u][0] == kTransEmpty && q[u][2] == kTransEmpty)) {
             uint64_t pl = lo, pr2 = hi;    // not in the table (left out): the descent
             descend_w2_thread(v, cs[u], pl, pr2);
             clo = pl;
             cnt = pr2 - pl;
           } else {
-            child_of(v, lo, hi, cs[u], 0, clo, cnt);
+            child_of(v, pid, lo, hi, cs[u], 0, clo, cnt);
           }
         }
         if (pos - base < cap) {

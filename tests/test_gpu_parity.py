@@ -968,32 +968,15 @@ def _device_u8(ptr, nbytes, owner):
     return torch.as_tensor(_V(), device=torch.device("cuda", 0))
 
 
-def _trans_home(lo, hi, c, cap):
-    """trans_home (csrc/fmidx_internal.h) in Python integers: the first slots of
-    a key's two buckets."""
-    M = (1 << 64) - 1
-
-    def cache_hash(a, b):
-        x = ((a * 0x9E3779B97F4A7C15) & M) ^ (((b + 0x632BE59BD9B4E019) & M) * 0xC2B2AE3D27D4EB4F & M)
-        x ^= x >> 29
-        x = (x * 0xBF58476D1CE4E5B9) & M
-        return x ^ (x >> 32)
-
-    h = cache_hash(lo ^ ((c * 0xD6E8FEB86659FD93) & M), (hi + c) & M)
-    g = ((h ^ (h >> 31)) * 0x94D049BB133111EB) & M
-    g ^= g >> 29
-    nb = cap // 8
-    return ((h * nb) >> 64) * 8, ((g * nb) >> 64) * 8
-
-
 def test_device_structs(dev):
     """fm_device_struct (the bench's gather ceilings over the index's own
     allocations) reports each structure's pointer and size, and the structures
     are what the kernels assume: E[i] = LF(i) | BWT[i] << 36 with LF the
     stable order of the BWT by symbol (LF(i) = C[BWT[i]] + rank), and the
-    transition table is 8-slot buckets of 24-B slots, each filled from its
-    first slot, with every key in one of its two buckets (trans_home,
-    csrc/fmidx_internal.h)."""
+    transition table is 8-slot buckets of 16-B slots (trans_key,
+    csrc/fmidx_internal.h), each filled from its first slot, whose entries are
+    children LF_c(P): a range inside c's C-block, with a one-row child's only
+    symbol or a cached child's bitmap (exactly its symbols) beside it."""
     import torch
 
     docs = markov_docs(11, 300, 200, 120)
@@ -1012,19 +995,34 @@ def test_device_structs(dev):
     order = torch.argsort(bwt, stable=True)
     assert torch.equal(lf[order], torch.arange(n, device=dev))
     p2, b2 = ours.device_struct(2)
-    assert p2 and b2 > 0 and b2 % 192 == 0
-    tab = _device_u8(p2, b2, ours).view(torch.int64).cpu().numpy().view(np.uint64).reshape(-1, 8, 3)
-    nb = tab.shape[0]
+    assert p2 and b2 > 0 and b2 % 128 == 0
+    tab = _device_u8(p2, b2, ours).view(torch.int64).cpu().numpy().view(np.uint64).reshape(-1, 8, 2)
     empty = tab[:, :, 0] == np.uint64(2**64 - 1)
     assert not (empty[:, :-1] & ~empty[:, 1:]).any()          # filled from the first slot
-    m34 = (1 << 34) - 1
-    keys = 0
+    st = ours.stats()
+    assert int((~empty).sum()) == st["trans_entries"] > 0
+    bw = bwt.cpu().numpy()
+    C = np.concatenate([[0], np.cumsum(np.bincount(bw))])
+    p3, b3 = ours.device_struct(3)
+    bm_words = b3 // (4 * st["cache_nodes"])
+    bm = _device_u8(p3, b3, ours).view(torch.int32).cpu().numpy().view(np.uint32).reshape(-1, bm_words)
+    kinds = [0, 0, 0]
     for b, k in zip(*np.nonzero(~empty)):
         w0, w1 = int(tab[b, k, 0]), int(tab[b, k, 1])
-        ha, hb = _trans_home(w0 & m34, w1 & m34, w0 >> 34, 8 * nb)
-        assert 8 * b in (ha, hb)
-        keys += 1
-    assert keys == ours.stats()["trans_entries"]
+        pid, c, kind = w0 & (2**20 - 1), (w0 >> 20) & (2**18 - 1), (w0 >> 38) & 3
+        clo = (w0 >> 40) | ((w1 & 0x3FF) << 24)
+        cw, aux = (w1 >> 10) & (2**34 - 1), w1 >> 44
+        assert pid < st["cache_nodes"] and cw > 0
+        assert C[c] <= clo and clo + cw <= C[c + 1]            # LF_c(P) lies in c's C-block
+        kinds[kind] += 1
+        if kind == 1:
+            assert cw == 1 and aux == bw[clo]
+        elif kind == 2:
+            syms = np.unique(bw[clo:clo + cw])
+            syms = syms[syms < 32 * bm_words]
+            bits = np.unpackbits(bm[aux].view(np.uint8), bitorder="little")
+            assert np.array_equal(np.nonzero(bits)[0], syms)
+    assert kinds[2] > 0
     for w in (3, 4):
         p, b = ours.device_struct(w)
         assert p and b > 0
