@@ -1063,35 +1063,34 @@ __global__ void __launch_bounds__(kLfThreads) FMIDX_SWEEP_ATTR k_lf_sweep(DevVie
 // The in-wave sweep above lives its rows' longest chain: a wave whose 64 rows hold a descent or a
 // wide E scan lives 16-27 us where one without lives 10 (round 5's stamps), and a 2^19-pair launch
 // is 1.6 residency rounds of such waves, so its last waves start late and end later.  Here the grid
-// is the resident wave count, and every wave
-//   heads  runs the head (sweep_head) of chunks w, w + W, w + 2W, ... (64 rows each; W = the
-//          grid's waves), stores the settled rows and APPENDS the tail rows to the tail queue of
-//          partition w mod 16 (one atomic per chunk reserves the slots; each entry is then written
-//          write-through and, after it is performed, its 4-B tag = the launch's epoch);
-//   drain  then claims queued tail rows up to four at a time (a compare-and-swap that claims only
-//          reserved slots) from every queue in turn, starting with its own, waits for their tags,
-//          and steps them together (sweep_tails: the E scans packed, the descents one per
-//          quarter-wave) -- tails are stepped four at a time by whichever wave is free, not one or
-//          two per wave by the wave that met them.
-// A wave leaves a queue when it holds no unclaimed reserved slot; a row appended later is drained
-// by the wave that appended it, which drains every queue after its heads.  So no wave waits for
-// another to finish anything but the few stores after a reservation (nothing waits on a wave that
-// is not resident), and the poll for a tag is bounded all the same (kPersistSpins; on expiry the
-// error word is set and the wave leaves).  Counters: two sets (the epoch's parity), each counter
-// on its own 128-B line; a launch zeroes the other set for the next launch on the stream.  Not
-// captured into graphs (the API launches it only on a stream that is not capturing).
-#ifndef FMIDX_PERSIST_ONE
-#define FMIDX_PERSIST_ONE 0
-#endif
-#ifndef FMIDX_PERSIST_ALLQ
-#define FMIDX_PERSIST_ALLQ 0
-#endif
-constexpr uint32_t kPParts = 16;                  // tail queues
+// is the resident wave count W (a multiple of kPParts), and every wave
+//   heads  runs the head (sweep_head) of chunks w, w + W, w + 2W, ... (64 rows each), stores the
+//          settled rows and APPENDS the tail rows to the tail queue q = chunk mod kPParts (= w mod
+//          kPParts: one atomic per chunk reserves the slots; each entry is written write-through
+//          and, once performed, its 4-B tag = the launch's epoch); then it counts the chunk in
+//          the queue's head count (after its tags are performed);
+//   drain  then takes kPClaim slots of its own queue at a time with ONE fetch-and-add on the
+//          queue's claim counter (no compare-and-swap: round 6's first two versions claimed only
+//          reserved slots by CAS, and 4096 waves retrying CAS on 16 counters made the launch
+//          9-15x slower than the in-wave sweep), waits for each slot's tag -- or, once the head
+//          count says every chunk of the queue is done, for the slot to lie past the final tail
+//          (an empty slot) -- and steps the ready rows together (sweep_tails: E scans packed, the
+//          descents one per quarter-wave).  A wave leaves when its claim lies wholly past the
+//          final tail.
+// A claimed slot may not be reserved yet, so a drainer can wait on another wave's heads: every
+// wave of the grid must be resident (the grid is the occupancy x CUs; a launch beside other work
+// that keeps waves off the chip can only end by the bounded poll, kPersistSpins, which sets the
+// error word -- fm_lf_persist_status reports it).  Counters: two sets (the epoch's parity), each
+// counter on its own 128-B line; a launch zeroes the other set for the next launch on the stream.
+// Not captured into graphs (the API launches it only on a stream that is not capturing).
+constexpr uint32_t kPParts = 64;                  // tail queues
+constexpr uint32_t kPClaim = 8;                   // slots per claim
 constexpr uint32_t kPStride = 32;                 // words between counters
-constexpr uint32_t kPCounters = 2 * kPParts;      // qtail[16] (reserved), qhead[16] (claimed)
+constexpr uint32_t kPCounters = 3 * kPParts;      // qtail (reserved), qhead (claimed), hdone (chunks done)
 constexpr uint32_t kPSetWords = kPCounters * kPStride;
 constexpr uint32_t kPersistSpins = 1u << 22;
 constexpr int kPSysAux = 16;                      // sc1: entries written through, read past the L1
+static_assert(kPCounters <= kLfThreads, "one thread zeroes each counter of the next set");
 
 struct PersistWs {
   uint32_t* ctr;     // 2 x kPSetWords
@@ -1117,9 +1116,12 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
     ws.ctr[((epoch + 1u) & 1u) * kPSetWords + threadIdx.x * kPStride] = 0u;
   const uint64_t nchunks = (m + 63) / 64;
   const uint64_t gw = (uint64_t)blockIdx.x * (kLfThreads / 64) + wv;
-  const uint64_t nw = (uint64_t)gridDim.x * (kLfThreads / 64);
-  const uint32_t p0 = (uint32_t)(gw % kPParts);
-  const __amdgpu_buffer_rsrc_t rq = make_rsrc(ws.tq + (uint64_t)p0 * qcap, qcap * (uint32_t)sizeof(LfWork));
+  const uint64_t nw = (uint64_t)gridDim.x * (kLfThreads / 64);   // a multiple of kPParts
+  const uint32_t q = (uint32_t)(gw % kPParts);
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(ws.tq + (uint64_t)q * qcap, qcap * (uint32_t)sizeof(LfWork));
+  uint32_t* qt = pctr(set, 0, q);
+  uint32_t* qh = pctr(set, 1, q);
+  uint32_t* hd = pctr(set, 2, q);
   // ---- heads: chunks gw, gw + nw, ...
   for (uint64_t chunk = gw; chunk < nchunks; chunk += nw) {   // wave-uniform
     const uint64_t i = chunk * 64 + lane;
@@ -1135,11 +1137,10 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
     if (tb) {   // wave-uniform
       uint32_t base = 0;
       if (lane == 0)
-        base = __hip_atomic_fetch_add(pctr(set, 0, p0), (uint32_t)__popcll(tb), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+        base = __hip_atomic_fetch_add(qt, (uint32_t)__popcll(tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       base = __shfl(base, 0, 64);
       const uint32_t pos = base + (uint32_t)__popcll(tb & ((1ull << lane) - 1));
-      if (tail) {   // pos < qcap: a queue holds every row of its waves' chunks
+      if (tail) {   // pos < qcap: a queue holds every row of its chunks
         const uint64_t sp = r.c | (r.pid1 << 32);
         const v4u_ a = {(uint32_t)r.l, (uint32_t)(r.l >> 32), (uint32_t)r.h, (uint32_t)(r.h >> 32)};
         const v4u_ b = {(uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)i, (uint32_t)(i >> 32)};
@@ -1148,69 +1149,63 @@ __global__ void __launch_bounds__(kLfThreads) k_lf_persist(DevView v, const int6
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every entry performed before its tag
       if (tail)
-        __hip_atomic_store(ws.tag + (uint64_t)p0 * qcap + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ws.tag + (uint64_t)q * qcap + pos, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every tag performed before the chunk counts
     }
+    if (lane == 0) __hip_atomic_fetch_add(hd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // ---- drain: this wave's own queue (FMIDX_PERSIST_ALLQ: every queue, from its own)
-  for (uint32_t k = 0; k < (FMIDX_PERSIST_ALLQ ? kPParts : 1u); ++k) {   // wave-uniform
-    const uint32_t q = (p0 + k) % kPParts;
-    uint32_t* qt = pctr(set, 0, q);
-    uint32_t* qh = pctr(set, 1, q);
-    for (;;) {
-      // claim up to four reserved slots: [j0, j0 + n)
-      uint32_t j0 = 0, n = 0;
+  // ---- drain: this wave's queue, kPClaim slots per claim
+  const uint32_t qchunks = nchunks > q ? (uint32_t)((nchunks - 1 - q) / kPParts + 1) : 0u;
+  const bool mine = lane < kPClaim;
+  for (;;) {
+    uint32_t j0 = 0;
+    if (lane == 0) j0 = __hip_atomic_fetch_add(qh, kPClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    j0 = __shfl(j0, 0, 64);
+    const uint32_t j = j0 + lane;
+    // per slot: 1 ready (tagged), 2 empty (past the final tail), 0 not yet known
+    uint32_t st = mine ? 0u : 2u;
+    uint32_t spin = 0;
+    for (; spin < kPersistSpins; ++spin) {
+      if (st == 0 && j < qcap &&
+          __hip_atomic_load(ws.tag + (uint64_t)q * qcap + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch)
+        st = 1;
+      if (__all(st != 0)) break;
+      uint32_t fin = 0, t = 0;
       if (lane == 0) {
-        uint32_t h = __hip_atomic_load(qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t t = __hip_atomic_load(qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (h < t) {
-          const uint32_t want = min(4u, t - h);
-          const uint32_t old = atomicCAS(qh, h, h + want);   // device scope
-          if (old == h) {
-            j0 = h;
-            n = want;
-            break;
-          }
-          h = old;   // another wave claimed first
-        }
+        fin = __hip_atomic_load(hd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == qchunks;
+        if (fin) t = __hip_atomic_load(qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      j0 = __shfl(j0, 0, 64);
-      n = __shfl(n, 0, 64);
-      if (!n) break;   // nothing reserved and unclaimed here now: the next queue
-      const bool mine = lane < n;
-      const uint32_t j = j0 + lane;
-      const uint64_t slot = (uint64_t)q * qcap + (mine ? j : j0);
-      // the slots are reserved: their tags follow within a few stores (bounded poll regardless)
-      bool ok = !mine;
-      for (uint32_t spin = 0; spin < kPersistSpins; ++spin) {
-        if (!ok) ok = __hip_atomic_load(ws.tag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!__all(ok)) {
-        if (lane == 0) __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
-      SweepRow r;
-      r.tail = mine;
-      r.nl = r.nh = 0;
-      const __amdgpu_buffer_rsrc_t re = make_rsrc(ws.tq + (uint64_t)q * qcap, qcap * (uint32_t)sizeof(LfWork));
-      const uint32_t jj = mine ? j : j0;
-      const v4u_ a = __builtin_amdgcn_raw_buffer_load_b128(re, jj * (uint32_t)sizeof(LfWork), 0, kPSysAux);
-      const v4u_ b = __builtin_amdgcn_raw_buffer_load_b128(re, jj * (uint32_t)sizeof(LfWork) + 16u, 0, kPSysAux);
-      r.l = (uint64_t)a.x | ((uint64_t)a.y << 32);
-      r.h = (uint64_t)a.z | ((uint64_t)a.w << 32);
-      const uint64_t sp = (uint64_t)b.x | ((uint64_t)b.y << 32);
-      r.c = sp & 0xFFFFFFFFull;
-      r.pid1 = sp >> 32;
-      const uint64_t row = (uint64_t)b.z | ((uint64_t)b.w << 32);
-      s_mm[wv][0][lane] = ~0ull;
-      s_mm[wv][1][lane] = 0;
-      __builtin_amdgcn_wave_barrier();
-      sweep_tails(v, s_mm[wv], r);
-      if (mine) {
-        lo_out[row] = r.nl;
-        hi_out[row] = r.nh;
-      }
+      fin = __shfl(fin, 0, 64);
+      t = __shfl(t, 0, 64);
+      if (fin && st == 0 && j >= t) st = 2;   // below the final tail, the tag is performed: re-read
+      if (__all(st != 0)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (spin == kPersistSpins) {
+      if (lane == 0) __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    const bool ready = st == 1;
+    if (!__ballot(ready)) break;   // the claim lies past the final tail: the queue is drained
+    SweepRow r;
+    r.tail = ready;
+    r.nl = r.nh = 0;
+    const uint32_t jj = ready ? j : j0;
+    const v4u_ a = __builtin_amdgcn_raw_buffer_load_b128(rq, jj * (uint32_t)sizeof(LfWork), 0, kPSysAux);
+    const v4u_ b = __builtin_amdgcn_raw_buffer_load_b128(rq, jj * (uint32_t)sizeof(LfWork) + 16u, 0, kPSysAux);
+    r.l = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    r.h = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    const uint64_t sp = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    r.c = sp & 0xFFFFFFFFull;
+    r.pid1 = sp >> 32;
+    const uint64_t row = (uint64_t)b.z | ((uint64_t)b.w << 32);
+    s_mm[wv][0][lane] = ~0ull;
+    s_mm[wv][1][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    sweep_tails(v, s_mm[wv], r);
+    if (ready) {
+      lo_out[row] = r.nl;
+      hi_out[row] = r.nh;
     }
   }
 }
@@ -1908,8 +1903,9 @@ static unsigned lf_persist_grid(int dev) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lf_persist, kLfThreads, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-  unsigned g = (unsigned)per_cu * (unsigned)cus;
-  g = std::max(4u, g / 4 * 4);   // waves a multiple of 16: wave w's chunks all in queue w mod 16
+  constexpr unsigned kBlk = kPParts / (kLfThreads / 64);   // waves a multiple of kPParts: wave w's chunks
+  unsigned g = (unsigned)per_cu * (unsigned)cus;          // all in queue w mod kPParts
+  g = std::max(kBlk, g / kBlk * kBlk);
   if (dev >= 0 && dev < 64) cached[dev] = g;
   return g;
 }
@@ -1931,11 +1927,9 @@ int launch_lf_persist(const DevView& v, const int64_t* tok, int64_t shift, int64
   w.tq = reinterpret_cast<LfWork*>(b + 2 * kPSetWords * 4 + 128);
   w.tag = reinterpret_cast<uint32_t*>(w.tq + kPParts * qcap);
   const uint64_t nchunks = (m + 63) / 64;
-  // FMIDX_PERSIST_ONE (measurement variant): one chunk per wave -- the heads dispatched as the in-wave
-  // sweep's are, only the tail rows shared
-  const unsigned g = FMIDX_PERSIST_ONE ? (unsigned)((nchunks + 3) / 4 * 4)
-                                       : (unsigned)std::min<uint64_t>(lf_persist_grid(dev), (nchunks + 3) / 4 * 4);
-  k_lf_persist<<<std::max(4u, g / 4 * 4), kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, w,
+  constexpr uint64_t kBlk = kPParts / (kLfThreads / 64);
+  const unsigned g = (unsigned)std::min<uint64_t>(lf_persist_grid(dev), (nchunks + 4 * kBlk - 1) / (4 * kBlk) * kBlk);
+  k_lf_persist<<<g, kLfThreads, 0, s>>>(v, tok, shift, reset_below, lo, hi, lo_out, hi_out, m, w,
                                                                (uint32_t)qcap, epoch);
   FM_HIP(hipGetLastError());
   return 0;
