@@ -427,7 +427,9 @@ int fm_shard_or_rows_peers(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_
 int fm_peer_signal(const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_step, void* stream);
 /* The persistent LF sweep (fm_tuning lf_work = 4, fm_lf_step_batch from lf_sweep_min rows on a stream
  * that is not capturing): after a synchronisation with its last launch, *err != 0 if a launch gave up
- * a wait (never on a sound run; its rows are then not all stepped). */
+ * a wait (its rows are then not all stepped).  Its grid is the resident wave count and a drainer may
+ * wait on another wave's heads, so a launch beside other work that keeps its waves off the chip can
+ * end this way; the in-wave sweep (lf_work -1, the default) has no such wait. */
 int fm_lf_persist_status(fm_index* h, uint32_t* err);
 int fm_shard_or_rows_peers_wait(const uint64_t* d_part_ptrs, uint64_t nparts, uint64_t cap_words, uint64_t B,
                                 uint64_t vocab, int64_t shift, void* d_out, uint64_t ld_out, int unpack,
