@@ -8,7 +8,8 @@ library's (saved masks), and prints one JSON line per library.
 usage: python tools/ab_decode.py [--tokens 4.5e9] [--reps 7] lib_a.so lib_b.so ...
 A library argument may carry build options for its process:
 lib.so@trans_min=2,lf_e=0 (FMIDX_BUILD_OPTIONS); the line then reports the
-index's device bytes and transition-table counts too.
+index's device bytes and transition-table counts too.  A %-suffix sets the
+process's FMIDX_TUNING: lib.so%dec_threads=512 (or lib.so@opts%tuning).
 """
 import argparse
 import json
@@ -77,7 +78,7 @@ def child(args):
         st = fm.stats()
     except AttributeError:     # a library older than the stats it asks for
         st = {"device_bytes": 0, "trans_bytes": 0, "trans_entries": -1, "trans_dropped": -1}
-    print(json.dumps({"lib": os.environ.get("FMIDX_LIB"), "build_options": os.environ.get("FMIDX_BUILD_OPTIONS", ""),
+    print(json.dumps({"lib": os.environ.get("FMIDX_LIB"), "build_options": os.environ.get("FMIDX_BUILD_OPTIONS", ""), "tuning": os.environ.get("FMIDX_TUNING", ""),
                       "device_gib": st["device_bytes"] / 2**30, "trans_gib": st["trans_bytes"] / 2**30,
                       "trans_entries": st["trans_entries"], "trans_dropped": st["trans_dropped"], "cold_us": sorted(cold), "warm_us": sorted(warm),
                       "cold_median": float(np.median(cold)), "warm_median": float(np.median(warm)),
@@ -102,10 +103,13 @@ def main():
         os.remove(ref)
     rc = 0
     for lib in args.libs:
+        lib, _, tun = lib.partition("%")
         lib, _, opts = lib.partition("@")
         env = dict(os.environ, FMIDX_LIB=os.path.abspath(lib))
         if opts:
             env["FMIDX_BUILD_OPTIONS"] = opts
+        if tun:
+            env["FMIDX_TUNING"] = tun
         r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--child", "--tokens", str(args.tokens),
                             "--batch", str(args.batch), "--reps", str(args.reps), "--out", args.out], env=env)
         rc = rc or r.returncode
