@@ -1457,8 +1457,8 @@ def main():
                          f"start from the prefix (force_decoding_from), V={V}, incremental ranges; timed replay "
                          f"cold (caches evicted)" if args.corpus == "paq" else
                          f"decode step (LF + allowed-token mask) over a synthetic Markov/Zipf corpus "
-                         f"of n={n} tokens ({'C3 enwiki' if n > 2e9 else ('C5 PAQ' if n > 1e9 else 'C2 simplewiki')} "
-                         f"scale), B={B} rows, V={V}, incremental ranges; timed replay cold (caches evicted)"),
+                         f"of n={n} tokens ({'C3 enwiki scale' if n > 2e9 else ('C2 simplewiki scale' if n <= 3.5e8 else 'Markov corpus between the C2 and C3 scales; C5 is --corpus paq')}"
+                         f"), B={B} rows, V={V}, incremental ranges; timed replay cold (caches evicted)"),
             "corpus": args.corpus,
             "corpus_tokens": n,
             "global_batch": world * B,
