@@ -588,17 +588,16 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
             checked = mode == "peer_flags_checked"
             packed_out = mode == "peer_flags_packed"
             tok_static = torch.empty_like(tokens[0])
-            ev_chk = torch.cuda.Event()
 
             def step(i, tok=None):
                 nonlocal payload
                 src, dst = bufs[i % 2], bufs[(i + 1) % 2]
                 if flags:            # state in place, the buffer and the step number on the device
+                    # one C call (fm_peer_flags_step, as ShardedDecoder makes it); checked: it also
+                    # synchronises the stream, then the error word is read -- exact or absent
                     peer.flags_step(ix, tokens[i] if tok is None else tok, lo, hi, V, SHIFT,
-                                    outw if packed_out else out, unpack=not packed_out)
-                    if checked:      # exact or absent (ShardedDecoder's default): wait, read the error word
-                        ev_chk.record()
-                        ev_chk.synchronize()
+                                    outw if packed_out else out, unpack=not packed_out, sync=checked)
+                    if checked:
                         peer.check()
                     return
                 if mode == "peer":   # the decode kernel writes the payload itself
@@ -684,11 +683,12 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
             ms_pf, exact_pf, to_pf = run("peer_flags")
             modes["peer_flags"] = {"ms_per_step": ms_pf, "value": B / (ms_pf / 1e3),
                                    "masks_equal_unsharded": exact_pf, "flag_timeouts": to_pf,
-                                   "step": "as peer, with the flag barrier: fm_peer_signal (the device step counter "
-                                           "advanced, a system-scope release, stores into every rank's flag array) "
-                                           "+ fm_shard_or_rows_peers_wait; state updated in place; eager launches; "
-                                           "the error word read only after the timed region (ShardedDecoder's "
-                                           "check='deferred')"}
+                                   "step": "as peer, with the flag barrier, one C call per step (fm_peer_flags_step): "
+                                           "the payload decode with the signal fused into its last workgroup (the "
+                                           "device step counter advanced, a system-scope release, stores into every "
+                                           "rank's flag array) + fm_shard_or_rows_peers_wait; state updated in place; "
+                                           "eager launches; the error word read only after the timed region "
+                                           "(ShardedDecoder's check='deferred')"}
             ms_pp, exact_pp, to_pp = run("peer_flags_packed")
             modes["peer_flags_packed"] = {"ms_per_step": ms_pp, "value": B / (ms_pp / 1e3),
                                           "masks_equal_unsharded": exact_pp, "flag_timeouts": to_pp,
@@ -701,8 +701,9 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
                                            "masks_equal_unsharded": exact_pc, "flag_timeouts": to_pc,
                                            "wait_cost_us_per_step": (ms_pc - ms_pf) * 1e3,
                                            "step": "as peer_flags, plus the exact-or-absent check every step "
-                                                   "(ShardedDecoder's default check='sync'): an event after the "
-                                                   "OR pass, waited on, then the error word read"}
+                                                   "(ShardedDecoder's default check='sync'): the same C call "
+                                                   "synchronises the stream after the OR pass, then the error "
+                                                   "word is read"}
             try:
                 ms_pg, exact_pg, to_pg = run("peer_flags_graph")
                 modes["peer_flags_graph"] = {"ms_per_step": ms_pg, "value": B / (ms_pg / 1e3),

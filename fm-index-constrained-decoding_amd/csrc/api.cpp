@@ -1207,7 +1207,12 @@ int fm_lf_step_batch(fm_index* h, const int64_t* d_tokens, int64_t shift, int64_
     } else if (h->lfp_ev_pending) {
       FM_HIP(hipStreamWaitEvent(s, h->lfp_ev, 0));
     }
-    if (++h->lfp_epoch == 0) h->lfp_epoch = 1;
+    if (++h->lfp_epoch == 0) {
+      // the epoch wrapped: tags of an old launch could equal a new epoch, and the counter sets
+      // alternate by the epoch's parity -- start over from a zeroed workspace at an even epoch
+      FM_HIP(hipMemsetAsync(h->lfp_ws, 0, h->lfp_bytes, s));
+      h->lfp_epoch = 2;
+    }
     const int rc = fmidx::launch_lf_persist(h->idx.view, d_tokens, shift, reset_below, d_lo, d_hi, d_lo_out, d_hi_out,
                                             m, s, h->lfp_ws, h->lfp_bytes, h->lfp_epoch, h->idx.device);
     FM_HIP(hipEventRecord(h->lfp_ev, s));
@@ -1586,6 +1591,30 @@ int fm_shard_or_rows_peers_facts(const uint64_t* d_part_ptrs, uint64_t nparts, u
   return fmidx::launch_shard_or_rows_peers(d_part_ptrs, nparts, cap_words, B, vocab, shift, d_out, ld_out, unpack,
                                            d_flags, d_step, spins, err, d_facts_out,
                                            reinterpret_cast<hipStream_t>(stream));
+  FM_API_END
+}
+
+static_assert(sizeof(fm_peer_step) == 168 && offsetof(fm_peer_step, reset_below) == 160,
+              "fm_peer_step: fmidx/sharding.py's FmPeerStep mirrors this layout");
+int fm_peer_flags_step(fm_index* h, const fm_peer_step* p, const int64_t* d_tokens, int sync, void* stream) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  FM_GUARD(h);
+  if (!p || !p->d_step || !p->d_done || !p->d_payload_alt || !p->d_flags || !p->d_part_ptrs) {
+    set_error("peer_flags_step: the step counter, the done counter, both payload buffers, the flags and the parts");
+    return -1;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (fmidx::launch_decode_payload(h->idx.view, d_tokens, p->shift, p->reset_below, p->d_lo, p->d_hi, p->d_lo, p->d_hi,
+                                   p->m, p->d_payload, p->cap_words, p->vocab, p->d_payload_alt, p->d_step, s,
+                                   p->d_flag_ptrs, p->world, p->d_done))
+    return -1;
+  if (fmidx::launch_shard_or_rows_peers(p->d_part_ptrs, p->nparts, p->cap_words, p->m, p->vocab, p->shift, p->d_out,
+                                        p->ld_out, p->unpack, p->d_flags, p->d_step, p->spins, p->err, nullptr, s))
+    return -1;
+  if (!sync || capturing(s)) return 0;
+  FM_HIP(hipStreamSynchronize(s));
+  return (p->err && *reinterpret_cast<volatile uint32_t*>(p->err)) ? 1 : 0;
   FM_API_END
 }
 

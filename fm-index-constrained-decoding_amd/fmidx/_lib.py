@@ -95,6 +95,7 @@ SIGNATURES = {
     "fm_shard_or_rows_peers_facts": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint64, c_int64, c_void_p,
                                              c_uint64, c_int, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p,
                                              c_void_p]),
+    "fm_peer_flags_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "fm_host_mapped_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
     "fm_host_mapped_free": (c_int, [c_void_p]),
     "fm_ipc_handle": (c_int, [c_void_p, c_void_p, u64p]),

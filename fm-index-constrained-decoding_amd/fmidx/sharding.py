@@ -298,12 +298,17 @@ class ShardedDecoder:
         if self.peer_barrier == "flags":
             px = self._peer
 
-            def launch(tok):
+            def launch(tok, sync=False):
                 px.flags_step(self.index, tok, self.lo, self.hi, self.vocab, self.shift, self._out,
-                              unpack=self.unpack)
+                              unpack=self.unpack, sync=sync)
 
             if not self.graph:
-                launch(tokens)
+                # one C call; with check="sync" it also waits for the step and reads the error word
+                launch(tokens, sync=self.check == "sync")
+                px.step += 1
+                if self.check == "sync":
+                    px.check()
+                return self._out
             else:
                 if self._g is None:
                     self._g_tok = torch.empty_like(tokens)
@@ -715,6 +720,20 @@ class PeerBarrierTimeout(RuntimeError):
     synchronisation, at the next call and at close())."""
 
 
+class FmPeerStep(ctypes.Structure):
+    """fm_peer_step (include/fmidx.h): one flag-barrier step's fixed buffers."""
+    _fields_ = [("d_lo", ctypes.c_void_p), ("d_hi", ctypes.c_void_p), ("m", ctypes.c_uint64),
+                ("d_payload", ctypes.c_void_p), ("d_payload_alt", ctypes.c_void_p), ("cap_words", ctypes.c_uint64),
+                ("d_step", ctypes.c_void_p), ("d_flag_ptrs", ctypes.c_void_p), ("world", ctypes.c_uint64),
+                ("d_done", ctypes.c_void_p), ("d_part_ptrs", ctypes.c_void_p), ("nparts", ctypes.c_uint64),
+                ("d_flags", ctypes.c_void_p), ("spins", ctypes.c_uint32), ("err", ctypes.c_void_p),
+                ("d_out", ctypes.c_void_p), ("ld_out", ctypes.c_uint64), ("unpack", ctypes.c_int32),
+                ("vocab", ctypes.c_uint64), ("shift", ctypes.c_int64), ("reset_below", ctypes.c_int64)]
+
+
+assert ctypes.sizeof(FmPeerStep) == 168 and FmPeerStep.reset_below.offset == 160   # api.cpp asserts the same
+
+
 class PeerExchange:
     """The sparse exchange with no gather and no host read: every rank packs
     into one of two payload buffers of its own (double-buffered by step
@@ -778,6 +797,7 @@ class PeerExchange:
         self._err_word = ctypes.c_int32.from_address(self._err_ptr)
         self._failed = 0
         self._skip_signal = 0        # tests: steps whose signal posts nothing (a rank that falls behind)
+        self._step_key = None        # fm_peer_flags_step's struct, per (index, state, output)
         torch.cuda.synchronize(self.device)
         mine = []
         for b in self.bufs + [self.flags]:
@@ -852,8 +872,44 @@ class PeerExchange:
         check(lib().fm_peer_signal(c_void_p(self.signal_to.data_ptr()), world, c_void_p(self.ctr.data_ptr()),
                                    c_void_p(stream)), "peer_signal")
 
+    def _fused_step(self, index, tokens, lo, hi, vocab, shift, out, unpack, reset_below, sync):
+        """fm_peer_flags_step: the struct of this step's fixed buffers is built
+        once per (index, state, output) and reused; per call only the tokens,
+        the signal's world (the test hook) and the stream travel."""
+        import torch
+        from ctypes import addressof, c_void_p
+
+        from ._lib import check, lib
+
+        B = lo.numel()
+        ld = out.stride(0) * out.element_size()
+        key = (index._h.value if hasattr(index._h, "value") else index._h, lo.data_ptr(), hi.data_ptr(), B,
+               out.data_ptr(), ld, bool(unpack), int(vocab), int(shift), int(reset_below))
+        if self._step_key != key:
+            assert out.stride(1) == 1 and out.device == self.device
+            st = FmPeerStep(d_lo=lo.data_ptr(), d_hi=hi.data_ptr(), m=B, d_payload=self.bufs[0].data_ptr(),
+                            d_payload_alt=self.bufs[1].data_ptr(), cap_words=self.cap, d_step=self.ctr.data_ptr(),
+                            d_flag_ptrs=self.signal_to.data_ptr(), world=self.world, d_done=self.done.data_ptr(),
+                            d_part_ptrs=self.ptab.data_ptr(), nparts=self.ptab.shape[-1],
+                            d_flags=self.flags.data_ptr(), spins=self.spins, err=self._err_ptr or None,
+                            d_out=out.data_ptr(), ld_out=ld, unpack=1 if unpack else 0, vocab=int(vocab),
+                            shift=int(shift), reset_below=int(reset_below))
+            self._step_struct, self._step_key = st, key
+            self._step_arg = c_void_p(addressof(st))
+        st = self._step_struct
+        st.world = self.world
+        if self._skip_signal:
+            self._skip_signal -= 1
+            st.world = 0
+        stream = torch._C._cuda_getCurrentRawStream(self.device.index)
+        rc = lib().fm_peer_flags_step(index._h, self._step_arg, c_void_p(tokens.data_ptr()), 1 if sync else 0,
+                                      c_void_p(stream))
+        if rc < 0:
+            check(rc, "peer_flags_step")
+        return out
+
     def flags_step(self, index, tokens, lo, hi, vocab: int, shift: int, out, unpack: bool = True,
-                   reset_below: int = 0):
+                   reset_below: int = 0, sync=None):
         """One decode step with the flag barrier, as two stream-ordered
         launches and nothing else (capturable; a captured call replays for
         every step): the payload decode of ``index`` -- the state (lo, hi)
@@ -861,12 +917,18 @@ class PeerExchange:
         the signal fused into its last workgroup -- then the OR pass into
         ``out`` (an index without the fused form: three launches, the signal
         its own).  The caller counts executed steps
-        in ``self.step`` (host parity = device parity, for payload())."""
+        in ``self.step`` (host parity = device parity, for payload()).  ``sync``
+        (True / False; None = the separate launches): one C call
+        (fm_peer_flags_step) for both launches, with True also the stream's
+        synchronisation -- the error word is then current for check()."""
         if self.barrier_mode != "flags":
             raise ValueError("flags_step: the exchange's barrier is not the flag barrier")
         B = lo.numel()
         if B > self.rows or vocab != self.vocab:
             raise ValueError(f"PeerExchange holds {self.rows} rows of vocab {self.vocab}")
+        if sync is not None and hasattr(index, "_h"):
+            # both launches (and, with sync, the wait and the error word) in one C call
+            return self._fused_step(index, tokens, lo, hi, vocab, shift, out, unpack, reset_below, sync)
         if hasattr(index, "decode_step_payload_signal"):
             # the signal fused into the decode kernel (its last workgroup posts the step): two launches
             world = self.world

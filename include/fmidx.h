@@ -372,6 +372,35 @@ int fm_decode_step_payload_signal(fm_index* h, const int64_t* d_tokens, int64_t 
                                   uint64_t* d_hi_out, uint64_t m, uint32_t* d_payload, uint64_t cap_words,
                                   uint64_t vocab, uint32_t* d_payload_alt, uint32_t* d_step,
                                   const uint64_t* d_flag_ptrs, uint64_t world, uint32_t* d_done, void* stream);
+/* One flag-barrier step in one call (the per-step host work of ShardedDecoder's flag path: no
+ * Python between the launches): fm_decode_step_payload_signal on the state in place, then
+ * fm_shard_or_rows_peers_wait into d_out; with sync != 0 the stream is then synchronised and the
+ * host-mapped error word read, and a step whose barrier timed out returns 1 (its output is not
+ * exact: exact or absent).  The step's buffers, fixed across steps, travel in one struct. */
+typedef struct fm_peer_step {
+  uint64_t* d_lo;              /* the rows' state, updated in place */
+  uint64_t* d_hi;
+  uint64_t m;
+  uint32_t* d_payload;         /* the double-buffered payload (the counter's parity picks) */
+  uint32_t* d_payload_alt;
+  uint64_t cap_words;
+  uint32_t* d_step;            /* the device step counter */
+  const uint64_t* d_flag_ptrs; /* this rank's word in every rank's flag array */
+  uint64_t world;
+  uint32_t* d_done;            /* 288 words, zero (the fused signal's arrival counts) */
+  const uint64_t* d_part_ptrs; /* [2, nparts]: every rank's two payload buffers */
+  uint64_t nparts;
+  const uint32_t* d_flags;     /* this rank's flag array */
+  uint32_t spins;
+  uint32_t* err;               /* host-mapped error word (fm_host_mapped_alloc) */
+  void* d_out;
+  uint64_t ld_out;
+  int32_t unpack;
+  uint64_t vocab;
+  int64_t shift;
+  int64_t reset_below;
+} fm_peer_step;
+int fm_peer_flags_step(fm_index* h, const fm_peer_step* p, const int64_t* d_tokens, int sync, void* stream);
 int fm_shard_pack(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t B, const uint32_t* d_bits,
                   uint64_t ldw, uint64_t vocab, uint32_t* d_payload, uint64_t cap_words, void* stream);
 int fm_shard_or_rows(const uint32_t* d_parts, uint64_t nparts, uint64_t part_stride, uint64_t B, uint64_t vocab,

@@ -97,10 +97,13 @@ def _header_struct_fields(name):
 
 
 def test_ctypes_structs_match_header():
-    """The ctypes mirrors of fm_prep_config / fm_processor_args list the
+    """The ctypes mirrors of fm_prep_config / fm_processor_args / fm_peer_step list the
     header's fields in the header's order (their sizes are asserted at import
     and in api.cpp)."""
     import fmidx.processors as P
 
     assert [f[0] for f in P._PrepConfig._fields_] == _header_struct_fields("fm_prep_config")
     assert [f[0] for f in P._ProcessorArgs._fields_] == _header_struct_fields("fm_processor_args")
+    from fmidx.sharding import FmPeerStep
+
+    assert [f[0] for f in FmPeerStep._fields_] == _header_struct_fields("fm_peer_step")
