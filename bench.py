@@ -1571,8 +1571,10 @@ def main():
             if t.get("lib_sha16") != lib_hash:
                 big = []
             if big:
-                result["standalone_kernels"]["k_lf"]["at_scale"]["pmc_bytes_per_launch"] = float(
-                    np.median([a + b for a, b in big]))
+                at = result["standalone_kernels"]["k_lf"]["at_scale"]
+                at["pmc_bytes_per_launch"] = float(np.median([a + b for a, b in big]))
+                if at.get("alg_bytes_per_launch"):   # HBM bytes moved per byte of LF plan
+                    at["pmc_over_plan_bytes"] = at["pmc_bytes_per_launch"] / at["alg_bytes_per_launch"]
         except Exception:
             pass
     # Memory-side read requests by size (tools/pmc_req.sh, committed under profiles/ with the
