@@ -886,7 +886,15 @@ class PeerExchange:
         key = (index._h.value if hasattr(index._h, "value") else index._h, lo.data_ptr(), hi.data_ptr(), B,
                out.data_ptr(), ld, bool(unpack), int(vocab), int(shift), int(reset_below))
         if self._step_key != key:
-            assert out.stride(1) == 1 and out.device == self.device
+            W = (int(vocab) + 31) // 32
+            want = (torch.uint8, int(vocab)) if unpack else (torch.int32, W)
+            if not (out.dim() == 2 and out.stride(1) == 1 and out.device == self.device and out.dtype == want[0]
+                    and out.shape[0] >= B and out.shape[1] >= want[1]):
+                raise ValueError(f"flags_step: out must be a row-contiguous {want[0]} [>= {B}, >= {want[1]}] "
+                                 f"tensor on {self.device}")
+            if not (lo.dtype == hi.dtype == torch.int64 and lo.is_contiguous() and hi.is_contiguous()
+                    and hi.numel() == B and lo.device == hi.device == self.device):
+                raise ValueError("flags_step: lo / hi must be contiguous int64 tensors of one length on the device")
             st = FmPeerStep(d_lo=lo.data_ptr(), d_hi=hi.data_ptr(), m=B, d_payload=self.bufs[0].data_ptr(),
                             d_payload_alt=self.bufs[1].data_ptr(), cap_words=self.cap, d_step=self.ctr.data_ptr(),
                             d_flag_ptrs=self.signal_to.data_ptr(), world=self.world, d_done=self.done.data_ptr(),
@@ -896,6 +904,8 @@ class PeerExchange:
                             shift=int(shift), reset_below=int(reset_below))
             self._step_struct, self._step_key = st, key
             self._step_arg = c_void_p(addressof(st))
+        if tokens.dtype != torch.int64 or tokens.numel() < B or tokens.device != self.device:
+            raise ValueError(f"flags_step: tokens must be an int64 tensor of >= {B} ids on {self.device}")
         st = self._step_struct
         st.world = self.world
         if self._skip_signal:
