@@ -387,8 +387,21 @@ constexpr int kOrSymU = 8;   // per later round (32 K symbols)
 // range check returns zeros without a memory request), the (part, round) pairs eight at a time,
 // instead of over one flat index space searched per load.  In PEERS mode these are 16-B
 // system-scope loads where the flat space needs pairs of 8-B ones.
-template <bool PEERS, bool PP>
-__global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __restrict__ parts,
+// The flag wait's acquire.  Every read of a peer's payload below is a system-scope load (sc0 sc1:
+// part_word / part_quad are system-scope atomic loads, the buffer loads carry kSysLoadAux), each
+// coherent for its location at the system's coherence point, and each issued only after wave 0's
+// poll has returned the step (the loop's exit depends on the polled values; the other waves pass
+// the workgroup barrier after it).  The peers' payload stores were write-through and acknowledged
+// before their release and flag store.  So the data is read from where the peer put
+// it, and an acquire fence adds only its cache maintenance -- a system-scope `buffer_inv sc0 sc1`
+// in every workgroup, invalidating the XCD's L2 each time: 12 µs of a B = 2048 world-1 step
+// (69.8 -> 57.8 µs; B = 256 20.2 -> 18.6; profiles/r06_or/).  FMIDX_OR_ACQUIRE=1 restores the fence
+// (measurement variant).
+#ifndef FMIDX_OR_ACQUIRE
+#define FMIDX_OR_ACQUIRE 0
+#endif
+template <bool PEERS, bool PP, int T>
+__global__ void __launch_bounds__(T) k_or_rows(const uint32_t* __restrict__ parts,
                                                             const uint64_t* __restrict__ ptrs, uint32_t nparts,
                                                             uint64_t stride, uint64_t B, uint32_t W, uint64_t vocab,
                                                             int64_t shift, void* __restrict__ out, uint64_t ld,
@@ -408,7 +421,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     else return parts + (uint64_t)p * stride;
   };
   const uint32_t W4 = (W + 3) / 4;
-  for (uint32_t w4 = t; w4 < W4; w4 += kOrRowThreads) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
+  for (uint32_t w4 = t; w4 < W4; w4 += T) reinterpret_cast<uint4*>(s_bits)[w4] = make_uint4(0, 0, 0, 0);
   if (t < 64) {
     const uint64_t* tab = ptrs;
     if (PEERS && flags) {
@@ -429,9 +442,9 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
         if (!__all(ok)) __builtin_amdgcn_s_sleep(4);
       }
       if (!__all(ok) && t == 0) __hip_atomic_store(err, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      // acquire: the peers' payload stores, released before their flag stores (k_peer_signal),
-      // are visible to every load below (they are system-scope loads as well)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      // the peers' payload stores, released before their flag stores, are read below by
+      // system-scope loads only, issued after this poll (see FMIDX_OR_ACQUIRE)
+      if (FMIDX_OR_ACQUIRE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     // wave 0 stages every part's (desc, off) and scans them in registers (nparts <= 64).  A row
     // whose data lies past the part's end (a gather shorter than the payload: the speculative
@@ -481,7 +494,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     if (t == 0) {
       s_pre[nparts] = tot;
       s_nd = (uint32_t)__popcll(dm);
-      s_nq = (mq + kOrRowThreads - 1) / kOrRowThreads;
+      s_nq = (mq + T - 1) / T;
     }
   }
   or_lds_barrier();
@@ -510,19 +523,19 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     const uint32_t k = j / nparts, p = j - k * nparts;
     const uint32_t bytes = j < npairs ? 4u * ((s_cnt[p] + 3u) & ~3u) : 0u;   // dense parts: 0, no request
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(base_of(p) + s_off[p], bytes);
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (t + k * kOrRowThreads), 0, PEERS ? kSysLoadAux : 0);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (t + k * T), 0, PEERS ? kSysLoadAux : 0);
   };
   auto pair_set = [&](uint32_t j, const or_v4u& x) {
     if (j >= npairs) return;                             // workgroup-uniform
     const uint32_t k = j / nparts, p = j - k * nparts;
-    const uint32_t i0 = 4 * (t + k * kOrRowThreads), cnt = s_cnt[p];
+    const uint32_t i0 = 4 * (t + k * T), cnt = s_cnt[p];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int64_t tok = (int64_t)x[e] - shift;
       if (i0 + e < cnt && tok >= 0 && (uint64_t)tok < vocab) atomicOr(&s_bits[tok >> 5], 1u << (tok & 31));
     }
   };
-  constexpr int kPP = 8;                                 // (part, round) pairs per round trip
+  constexpr int kPP = T >= 1024 ? 8 : 4;                 // (part, round) pairs per round trip
   or_v4u pq0[PP ? kPP : 1];
   if constexpr (PP) {
 #pragma unroll
@@ -535,15 +548,15 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
 #pragma unroll
     for (int u = 0; u < kOrSym0; ++u) {
       sp0[u] = 0;
-      sq0[u] = total4 ? quad_at(min(u * kOrRowThreads + t, total4 - 1), sp0[u]) : make_uint4(0, 0, 0, 0);
+      sq0[u] = total4 ? quad_at(min(u * T + t, total4 - 1), sp0[u]) : make_uint4(0, 0, 0, 0);
     }
   }
-  constexpr int kSlots4 = kOrRowMaxWords / (4 * kOrRowThreads);   // W <= 8192 words
-  const uint32_t slots = (W4 + kOrRowThreads - 1) / kOrRowThreads;
+  constexpr int kSlots4 = kOrRowMaxWords / (4 * T);   // W <= 8192 words
+  const uint32_t slots = (W4 + T - 1) / T;
   uint4 acc[kSlots4];
 #pragma unroll
   for (int k = 0; k < kSlots4; ++k) acc[k] = make_uint4(0u, 0u, 0u, 0u);
-  constexpr int kPB = 8;
+  constexpr int kPB = T >= 1024 ? 8 : 1;                // dense parts per round trip (registers: kPB x kSlots4)
   for (uint32_t j0 = 0; j0 < nd; j0 += kPB) {
     uint4 x[kPB][kSlots4];
 #pragma unroll
@@ -556,7 +569,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
 #pragma unroll
         for (int k = 0; k < kSlots4; ++k) {
           if ((uint32_t)k < slots) {
-            const or_v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * min(t + k * kOrRowThreads, W4 - 1), 0,
+            const or_v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * min(t + k * T, W4 - 1), 0,
                                                                    kSysLoadAux);
             x[q][k] = make_uint4(v.x, v.y, v.z, v.w);
           } else {
@@ -567,7 +580,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
         const uint4* s4 = reinterpret_cast<const uint4*>(src);
 #pragma unroll
         for (int k = 0; k < kSlots4; ++k)
-          x[q][k] = (uint32_t)k < slots ? s4[min(t + k * kOrRowThreads, W4 - 1)] : make_uint4(0, 0, 0, 0);
+          x[q][k] = (uint32_t)k < slots ? s4[min(t + k * T, W4 - 1)] : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -583,7 +596,7 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
   if (nd) {
 #pragma unroll
     for (int k = 0; k < kSlots4; ++k) {
-      const uint32_t w4 = t + k * kOrRowThreads;
+      const uint32_t w4 = t + k * T;
       if (w4 < W4) reinterpret_cast<uint4*>(s_bits)[w4] = acc[k];
     }
   }
@@ -602,27 +615,27 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < kOrSym0; ++u) set_quad(u * kOrRowThreads + t, sp0[u], sq0[u]);
-    for (uint32_t j0 = kOrSym0 * kOrRowThreads; j0 < total4; j0 += kOrSymU * kOrRowThreads) {   // long lists
+    for (int u = 0; u < kOrSym0; ++u) set_quad(u * T + t, sp0[u], sq0[u]);
+    for (uint32_t j0 = kOrSym0 * T; j0 < total4; j0 += kOrSymU * T) {   // long lists
       uint4 sq[kOrSymU];
       uint32_t sp[kOrSymU];
 #pragma unroll
-      for (int u = 0; u < kOrSymU; ++u) sq[u] = quad_at(min(j0 + u * kOrRowThreads + t, total4 - 1), sp[u]);
+      for (int u = 0; u < kOrSymU; ++u) sq[u] = quad_at(min(j0 + u * T + t, total4 - 1), sp[u]);
 #pragma unroll
-      for (int u = 0; u < kOrSymU; ++u) set_quad(j0 + u * kOrRowThreads + t, sp[u], sq[u]);
+      for (int u = 0; u < kOrSymU; ++u) set_quad(j0 + u * T + t, sp[u], sq[u]);
     }
   }
   or_lds_barrier();
   if (!unpack) {
     uint32_t* o = static_cast<uint32_t*>(out) + b * (ld / 4);
-    for (uint32_t w = t; w < W; w += kOrRowThreads) o[w] = s_bits[w];
+    for (uint32_t w = t; w < W; w += T) o[w] = s_bits[w];
     return;
   }
   uint8_t* row = static_cast<uint8_t*>(out) + b * ld;
   const __amdgpu_buffer_rsrc_t r = make_rsrc(row, (uint32_t)vocab);
   const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
   const uint32_t nch = (uint32_t)((vocab + 15) / 16);
-  for (uint32_t c = t; c < nch; c += kOrRowThreads) {
+  for (uint32_t c = t; c < nch; c += T) {
     const uint64_t t0 = 16ull * c;
     const uint32_t bits16 = (s_bits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
     uint32_t q[4];
@@ -645,6 +658,19 @@ __global__ void __launch_bounds__(kOrRowThreads) k_or_rows(const uint32_t* __res
 #define FMIDX_OR_PERPART 1
 #endif
 static bool or_per_part() { return FMIDX_OR_PERPART != 0; }
+
+// Workgroup size of the OR pass by batch, as the decode kernel's (decode_threads): one 1024-thread
+// workgroup per row while the rows fit one per CU (the 128-KB uint8 row wants all 16 waves' store
+// issue); beyond that 256 threads, so that several rows' round-trip chains -- flag poll, header,
+// payload data -- overlap on each CU instead of running one row per CU per round.
+// FMIDX_OR_THREADS (measurement variant): 1024 or 256 for every batch.
+#ifndef FMIDX_OR_THREADS
+#define FMIDX_OR_THREADS 0
+#endif
+static uint32_t or_threads(uint64_t B) {
+  if (FMIDX_OR_THREADS == 1024 || FMIDX_OR_THREADS == 256) return FMIDX_OR_THREADS;
+  return B <= 256 ? 1024u : 256u;
+}
 
 uint64_t shard_payload_capacity(uint64_t B, uint64_t vocab) {
   const uint64_t W = (vocab + 31) / 32;
@@ -687,14 +713,18 @@ int launch_shard_or_rows(const uint32_t* parts, uint64_t nparts, uint64_t stride
     set_error("shard_or_rows: the payloads must start on 16-B boundaries (stride a multiple of 4 words)");
     return -1;
   }
-  if (or_per_part())
-    k_or_rows<false, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr,
-        facts_out);
-  else
-    k_or_rows<false, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        parts, nullptr, (uint32_t)nparts, stride, B, (uint32_t)W, vocab, shift, out, ld, unpack, nullptr, nullptr, 0, nullptr,
-        facts_out);
+#define FM_OR_LAUNCH(PP, TT)                                                                                  \
+  k_or_rows<false, PP, TT><<<(unsigned)B, TT, (W + 3) / 4 * 16, s>>>(parts, nullptr, (uint32_t)nparts, stride, B,     \
+                                                                     (uint32_t)W, vocab, shift, out, ld, unpack,       \
+                                                                     nullptr, nullptr, 0, nullptr, facts_out)
+  if (or_threads(B) == 1024) {
+    if (or_per_part()) FM_OR_LAUNCH(true, 1024);
+    else FM_OR_LAUNCH(false, 1024);
+  } else {
+    if (or_per_part()) FM_OR_LAUNCH(true, 256);
+    else FM_OR_LAUNCH(false, 256);
+  }
+#undef FM_OR_LAUNCH
   FM_HIP(hipGetLastError());
   return 0;
 }
@@ -718,14 +748,18 @@ int launch_shard_or_rows_peers(const uint64_t* ptrs, uint64_t nparts, uint64_t c
     return -1;
   }
   if (!spins) spins = kFlagSpins;
-  if (or_per_part())
-    k_or_rows<true, true><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err,
-        facts_out);
-  else
-    k_or_rows<true, false><<<(unsigned)B, kOrRowThreads, (W + 3) / 4 * 16, s>>>(
-        nullptr, ptrs, (uint32_t)nparts, cap, B, (uint32_t)W, vocab, shift, out, ld, unpack, flags, ctr, spins, err,
-        facts_out);
+#define FM_OR_LAUNCH(PP, TT)                                                                                  \
+  k_or_rows<true, PP, TT><<<(unsigned)B, TT, (W + 3) / 4 * 16, s>>>(nullptr, ptrs, (uint32_t)nparts, cap, B,           \
+                                                                    (uint32_t)W, vocab, shift, out, ld, unpack, flags, \
+                                                                    ctr, spins, err, facts_out)
+  if (or_threads(B) == 1024) {
+    if (or_per_part()) FM_OR_LAUNCH(true, 1024);
+    else FM_OR_LAUNCH(false, 1024);
+  } else {
+    if (or_per_part()) FM_OR_LAUNCH(true, 256);
+    else FM_OR_LAUNCH(false, 256);
+  }
+#undef FM_OR_LAUNCH
   FM_HIP(hipGetLastError());
   return 0;
 }

@@ -70,14 +70,15 @@ def test_or_bits_rejects_short_rows(dev):
     np.testing.assert_array_equal(or_bits(parts, 100).cpu().numpy(), np.zeros((3, 100), np.uint8))
 
 
-@pytest.mark.parametrize("V", [100, 128256, 151936])
+@pytest.mark.parametrize("V,B", [(100, 64), (128256, 64), (151936, 64), (128256, 320)])
 @pytest.mark.parametrize("world", [2, 5])
-def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
+def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, B, world):
     """fm_shard_pack + fm_shard_or_rows (the sparse C4 exchange) against the
     dense exchange (fm_or_bits over every shard's packed rows) and the
     unsharded index's mask, over doc-range shards with a halo: rows from
     empty to the full range, so both payload kinds (BWT slice, bitmap) occur;
-    the gathered payloads are padded to the largest, as the all_gather does."""
+    the gathered payloads are padded to the largest, as the all_gather does.
+    B > 256 takes the OR pass's 256-thread workgroups (or_threads)."""
     import torch
 
     from fmidx.index import FMIndex
@@ -90,7 +91,6 @@ def test_sparse_exchange_equals_dense_or_and_unsharded(dev, V, world):
     for d in docs[::3]:
         d[:4] = [1, 2, 3, 4]
     F = [t for d in reversed(docs) for t in d]
-    B = 64
     pats = [[]] + [[1, 2]] + [[1]] + [F[s:s + int(rng.integers(1, 5))] for s in rng.integers(0, len(F) - 8, B - 4)]
     pats.append([vocab_used + 7])                 # never in the corpus: empty everywhere
     full = FMIndex()
