@@ -1401,6 +1401,14 @@ int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint
   FM_API_END
 }
 
+int fm_stats_trans_complete(const fm_index* h, uint32_t* complete) {
+  FM_API_BEGIN
+  FM_CHECK_BUILT(h);
+  if (complete) *complete = (h->idx.view.probe_first & fmidx::kProbeComplete) ? 1u : 0u;
+  return 0;
+  FM_API_END
+}
+
 int fm_cache_lookup_batch(fm_index* h, const uint64_t* d_lo, const uint64_t* d_hi, uint64_t m, uint8_t* d_out,
                           void* stream) {
   FM_API_BEGIN

@@ -93,7 +93,10 @@ __global__ void __launch_bounds__(256) k_trans_insert(DevView v, const uint64_t*
   const uint64_t r = blockIdx.x;
   if (r >= m) return;
   const uint64_t kr = k[r];
-  if (kr == ~0ull) return;
+  if (kr == ~0ull) {   // a parent whose children were not listed: the table is not complete
+    if (threadIdx.x == 0) atomicAdd(&stats[2], 1ull);
+    return;
+  }
   const uint64_t lo = plo[r], hi = phi[r], base = off[r];
   if (threadIdx.x == 0) s_pid = cache_id_thread(v, lo, hi);   // the parent's cache id + 1 (0: not cached)
   __syncthreads();
@@ -152,6 +155,7 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   DevView& v = h->view;
   v.trans_cap = 0;
   v.trans_tab = nullptr;
+  v.probe_first &= ~kProbeComplete;
   if (h->trans_tab) (void)hipFree(h->trans_tab);
   h->trans_tab = nullptr;
   h->trans_entries = h->trans_dropped = h->trans_bytes = 0;
@@ -237,11 +241,11 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   FM_HIP(hipMemsetAsync(tab, 0xFF, cap * kTransSlotBytes, s));
   DBuf<unsigned long long> d_stats;
   DBuf<uint32_t> d_fill;   // per-bucket fill counts, for the insert only
-  if (d_stats.alloc(2) || d_fill.alloc(cap / kTransBucket)) {
+  if (d_stats.alloc(3) || d_fill.alloc(cap / kTransBucket)) {
     (void)hipFree(tab);
     return -1;
   }
-  FM_HIP(hipMemsetAsync(d_stats.p, 0, 16, s));
+  FM_HIP(hipMemsetAsync(d_stats.p, 0, 24, s));
   FM_HIP(hipMemsetAsync(d_fill.p, 0, cap / kTransBucket * 4, s));
   uint64_t dummy = 0;
   t = build_clock();
@@ -250,8 +254,8 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
     return -1;
   }
   build_phase("transitions: insert pass", t, s);
-  unsigned long long st[2] = {0, 0};
-  FM_HIP(hipMemcpy(st, d_stats.p, 16, hipMemcpyDeviceToHost));
+  unsigned long long st[3] = {0, 0, 0};
+  FM_HIP(hipMemcpy(st, d_stats.p, 24, hipMemcpyDeviceToHost));
   FM_HIP(hipStreamSynchronize(s));
   h->trans_tab = tab;
   h->trans_entries = st[0];
@@ -260,6 +264,10 @@ int build_transitions(Index* h, const std::vector<std::pair<uint64_t, uint64_t>>
   h->cache_bytes += cap * kTransSlotBytes;
   v.trans_tab = tab;
   v.trans_cap = cap;
+  // every child of every cached parent offered to the table (kProbeComplete, fmidx_internal.h);
+  // FMIDX_PROBE_COMPLETE=0 turns the absent-symbol shortcut off (measurement)
+  const char* pc_env = getenv("FMIDX_PROBE_COMPLETE");
+  if (min_count == 1 && st[2] == 0 && !(pc_env && pc_env[0] == '0')) v.probe_first |= kProbeComplete;
   return 0;
 }
 

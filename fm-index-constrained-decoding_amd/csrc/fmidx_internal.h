@@ -87,8 +87,10 @@ struct DevView {
   uint32_t bm_words;          // uint32 words per bitmap (multiple of 4)
   uint32_t bm_levels;         // number of bitmap levels (0 = none)
   uint32_t bm_log2;           // log2(B0)
-  uint32_t probe_first;       // 1: a cached range's LF step waits for its transition probe before
-                              //    issuing the descent (a hit needs no rank loads); 0: issued together
+  uint32_t probe_first;       // bit 0: a cached range's LF step waits for its transition probe before
+                              //    issuing the descent (a hit needs no rank loads); else issued together
+                              // bit 1 (kProbeComplete): the table holds every child of every cached
+                              //    parent, so a miss beside a free slot proves the symbol absent
 #ifdef FMIDX_STAMPS
   uint64_t* stamps;           // diagnostic build only: per-workgroup phase timestamps
 #endif
@@ -511,6 +513,12 @@ constexpr uint32_t kTKindOne = 1, kTKindCached = 2;
 constexpr uint64_t kTAuxLimit = 1ull << 20;
 constexpr uint32_t kTransBucket = 8;
 constexpr uint32_t kTransProbe = 2 * kTransBucket;   // a key's candidate slots: bucket A's, then bucket B's
+// DevView::probe_first bit 1.  The insert leaves a key out only when both of its buckets are
+// full, and a bucket's fill never shrinks; so when the table was built with every child of every
+// cached parent (transitions = 2, trans_min = 1, no parent skipped), a probe that finds the
+// parent's id, no matching key and a free slot among its 16 has proved the symbol absent from the
+// parent's range -- the step ends after the probe, without the parent's bitmap word.
+constexpr uint32_t kProbeComplete = 2;
 constexpr uint64_t kTransEmpty = ~0ull;
 constexpr uint64_t kTransSlotBytes = 16;
 constexpr uint64_t kMask34 = (1ull << 34) - 1;
@@ -630,17 +638,24 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
   // is loaded with the descent's first level, and an absent c ends the step
   // there (one round trip after the probe instead of the whole descent).
   uint32_t pword = ~0u;
-  if (probe && v.probe_first) {   // the probe alone: one round trip of 256 B + the run for a hit
+  if (probe && (v.probe_first & 1u)) {   // the probe alone: one round trip of 256 B + the run for a hit
     const uint64_t w1n = __shfl_down(tw, 1, 64);
     const uint64_t pid = parent_id(w1n);
     const uint64_t key = trans_key(pid, c);
-    const uint64_t bh = __ballot(lane < 2 * kTransProbe && (lane & 1u) == 0 && pid != kTPidNone &&
-                                 trans_match(tw, key));
+    // (a parent id of 2^20 - 1 or more is never a key: trans_key would spill into the symbol bits)
+    const bool keyed = pid < kTPidNone && c < kTSymLimit;
+    const bool even = lane < 2 * kTransProbe && (lane & 1u) == 0;
+    const uint64_t bh = __ballot(even && keyed && trans_match(tw, key));
     if (bh) {
       take_hit(bh);
       return;
     }
-    if (pid != kTPidNone) pword = v.cache_bm[pid * v.bm_words + (c32 >> 5)];
+    if (keyed && (v.probe_first & kProbeComplete) && __ballot(even && tw == kTransEmpty)) {
+      lo = 0;   // c is absent from the parent's range (kProbeComplete)
+      hi = 0;
+      return;
+    }
+    if (pid < kTPidNone) pword = v.cache_bm[pid * v.bm_words + (c32 >> 5)];
   }
   // (2) level-independent loads, then the descent
   const int64_t dd = v.D2[c32];
@@ -658,12 +673,12 @@ __device__ __forceinline__ void lf_step_decode(const DevView& v, int64_t sym, ui
       hi = 0;
       return;
     }
-    if (l == 0 && probe && !v.probe_first) {   // the probe's loads were issued before this level's
+    if (l == 0 && probe && !(v.probe_first & 1u)) {   // the probe's loads were issued before this level's
       const uint64_t w1n = __shfl_down(tw, 1, 64);
       const uint64_t pid = parent_id(w1n);
       const uint64_t key = trans_key(pid, c);
-      const uint64_t bh = __ballot(lane < 2 * kTransProbe && (lane & 1u) == 0 && pid != kTPidNone &&
-                                   trans_match(tw, key));
+      const uint64_t bh = __ballot(lane < 2 * kTransProbe && (lane & 1u) == 0 && pid < kTPidNone &&
+                                   c < kTSymLimit && trans_match(tw, key));
       if (bh) {
         take_hit(bh);
         return;

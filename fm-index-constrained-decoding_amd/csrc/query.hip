@@ -140,14 +140,20 @@ __device__ __forceinline__ void probe_finish(const DevView& v, uint64_t l, uint6
   const uint64_t key = trans_key(pid, c);
   const uint64_t a0 = (uint64_t)p.ca.x | ((uint64_t)p.ca.y << 32), a1 = (uint64_t)p.ca.z | ((uint64_t)p.ca.w << 32);
   const uint64_t b0 = (uint64_t)p.cb.x | ((uint64_t)p.cb.y << 32), b1 = (uint64_t)p.cb.z | ((uint64_t)p.cb.w << 32);
-  const bool ma = pid != kTPidNone && trans_match(a0, key), mb = pid != kTPidNone && trans_match(b0, key);
+  // (a parent id of 2^20 - 1 or more is never a key: trans_key would spill into the symbol bits)
+  const bool keyed = pid < kTPidNone && c < kTSymLimit;
+  const bool ma = keyed && trans_match(a0, key), mb = keyed && trans_match(b0, key);
   const uint64_t w0 = ma ? a0 : b0, w1 = ma ? a1 : b1;
   const uint64_t hb = __ballot(act && (ma || mb)) & segm;
   const int hl = hb ? __ffsll((long long)hb) - 1 : (int)lane;
   const uint64_t hw0 = __shfl(w0, hl, 64), hw1 = __shfl(w1, hl, 64);
-  hit_row = hb != 0;
-  clo = trans_clo(hw0, hw1);
-  chi = clo + trans_cw(hw1);
+  // a miss beside a free slot of either bucket: c is absent from the range (kProbeComplete) --
+  // settled here as the empty range, not handed to the tail
+  const uint64_t eb = __ballot(act && keyed && (a0 == kTransEmpty || b0 == kTransEmpty)) & segm;
+  const bool absent = !hb && eb && (v.probe_first & kProbeComplete);
+  hit_row = hb != 0 || absent;
+  clo = absent ? 0 : trans_clo(hw0, hw1);
+  chi = absent ? 0 : clo + trans_cw(hw1);
   pid1 = pb ? pid + 1 : 0;
 }
 
@@ -342,7 +348,7 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
     uint64_t hit = 0, clo = 0, cw = 0;
 #pragma unroll
     for (int k = 0; k < 16 / G; ++k) {
-      const bool m = probe && pid1 && trans_match(pw[2 * k], key);
+      const bool m = probe && pid1 && pid1 - 1 < kTPidNone && c < kTSymLimit && trans_match(pw[2 * k], key);
       hit |= m ? 1u : 0u;
       clo |= m ? trans_clo(pw[2 * k], pw[2 * k + 1]) : 0;
       cw |= m ? trans_cw(pw[2 * k + 1]) : 0;
@@ -427,7 +433,8 @@ __device__ __forceinline__ void group_step(const DevView& v, bool live, int64_t 
       const uint64_t segm = 0xFFFFull << (16 * seg);
       const uint64_t pb = __ballot(qprobe && v.cache_mask && e0 == ql && (e1 & kMask34) == qh) & segm;
       const uint64_t qpid = pb ? (__shfl(e1, __ffsll((long long)pb) - 1, 64) >> kCacheIdShift) : kTPidNone;
-      const uint64_t hb = __ballot(qprobe && pb && trans_match(p0, trans_key(qpid, qc))) & segm;
+      const uint64_t hb = __ballot(qprobe && pb && qpid < kTPidNone && qc < kTSymLimit &&
+                                   trans_match(p0, trans_key(qpid, qc))) & segm;
       const int hl = hb ? __ffsll((long long)hb) - 1 : 0;
       const uint64_t w0 = __shfl(p0, hl, 64), w1 = __shfl(p1, hl, 64);
       uint64_t rlo = 0, rhi = 0;

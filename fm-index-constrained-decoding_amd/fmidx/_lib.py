@@ -63,6 +63,7 @@ SIGNATURES = {
     "fm_stats": (c_int, [c_void_p, u64p, u64p, u64p, u64p, u64p]),
     "fm_stats_ex": (c_int, [c_void_p, u64p, u64p, u64p, u64p, u64p]),
     "fm_stats_trans": (c_int, [c_void_p, u64p, u64p, u64p]),
+    "fm_stats_trans_complete": (c_int, [c_void_p, POINTER(c_uint32)]),
     "fm_stats_mem": (c_int, [c_void_p, u64p, u64p, u64p]),
     "fm_locate_batch": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
     "fm_extract_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),

@@ -13,7 +13,7 @@ from __future__ import annotations
 import ctypes
 import itertools
 import os
-from ctypes import byref, c_uint64, c_void_p
+from ctypes import byref, c_uint32, c_uint64, c_void_p
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -277,6 +277,9 @@ class FMIndex:
         check(lib().fm_stats_trans(self._h, *[byref(v) for v in tr]), "stats_trans")
         for k, v in zip(["trans_entries", "trans_dropped", "trans_bytes"], tr):
             out[k] = int(v.value)
+        tc = c_uint32()
+        check(lib().fm_stats_trans_complete(self._h, byref(tc)), "stats_trans_complete")
+        out["trans_complete"] = int(tc.value)
         mem = [c_uint64() for _ in range(3)]
         check(lib().fm_stats_mem(self._h, *[byref(v) for v in mem]), "stats_mem")
         for k, v in zip(["lf_e_bytes", "sample_bytes", "device_bytes"], mem):

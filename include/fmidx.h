@@ -622,6 +622,12 @@ int fm_stats_ex(const fm_index* h, uint64_t* w2_levels, uint64_t* w2_bytes, uint
  * wavelet-matrix descent) and bytes in HBM. */
 int fm_stats_trans(const fm_index* h, uint64_t* entries, uint64_t* dropped, uint64_t* bytes);
 
+/* 1 when the transition table holds every child of every cached parent (transitions = 2,
+ * trans_min = 1, nothing skipped): a probe that finds no key beside a free slot then proves
+ * the symbol absent and the LF step ends after the probe; 0 otherwise (or with
+ * FMIDX_PROBE_COMPLETE=0 at build time). */
+int fm_stats_trans_complete(const fm_index* h, uint32_t* complete);
+
 /* Device memory of the index: the E array, the SA/ISA samples and the total
  * of every device structure (bytes). */
 int fm_stats_mem(const fm_index* h, uint64_t* e_bytes, uint64_t* sample_bytes, uint64_t* total_bytes);

@@ -6,8 +6,11 @@
     the flag barrier's serving form -- equals the same steps decoded with
     ping-pong state buffers, eagerly: states and payload rows, every step;
   * fm_set_build_options on an index that is already built is refused, and
-    the options reported stay the ones the index was built with."""
+    the options reported stay the ones the index was built with;
+  * round-6 kernels: the static split emit, the persistent LF sweep, and the
+    absent-symbol probe shortcut (kProbeComplete), each against the oracle."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -248,3 +251,82 @@ def test_lf_persist_vs_oracle(dev):
             assert not bad, (opts, rep, [(i, nxt[i], li[i], hv[i], got[i], want_lf[i]) for i in bad[:5]])
         err = ctypes.c_uint32(7)
         assert lib().fm_lf_persist_status(ours._h, ctypes.byref(err)) == 0 and err.value == 0, opts
+
+
+def test_probe_complete_absent_vs_oracle(dev):
+    """The absent-symbol probe shortcut (kProbeComplete, fmidx_internal.h): with
+    a transition table that holds every child of every cached parent, a probe
+    finding no key beside a free slot ends the LF step as the empty range.  An
+    index built with FMIDX_PROBE_COMPLETE=0 (the parent's bitmap word decides
+    instead) and the default one both equal the oracle -- decode steps (uint8
+    mask + state) and the in-wave LF sweep -- on cached parents stepped with
+    symbols they lack, symbols they hold, and past-vocabulary ids."""
+    import torch
+
+    from fmidx.index import FMIndex
+    from fmidx.options import tuning
+    from oracle.fm_oracle import OracleIndex, allowed_mask
+
+    rng = np.random.default_rng(61)
+    V = 128256
+    common = rng.choice(40, 20, replace=False)
+    docs = []
+    for _ in range(600):
+        ln = int(rng.integers(20, 120))
+        docs.append([int(common[rng.integers(0, 20)]) if rng.random() < 0.85 else int(rng.integers(0, V))
+                     for _ in range(ln)])
+    ora = OracleIndex()
+    ora.initialize(docs, in_memory=True)
+    F = [t for d in reversed(docs) for t in d]
+    # patterns of 0-2 common tokens: wide parents (cached at cache_min 4; single tokens ~2400
+    # rows, past the decode kernel's E scans, so the decode step probes them)
+    B = 256
+    pats = [[]] + [[int(x) for x in rng.choice(common, int(rng.integers(1, 3)))] for _ in range(B - 1)]
+    want0 = [ora.get_range(p) if p else (0, len(F) + 1) for p in pats]
+    completes = []
+    for pc in ("0", "1"):
+        old = os.environ.get("FMIDX_PROBE_COMPLETE")
+        os.environ["FMIDX_PROBE_COMPLETE"] = pc
+        try:
+            ours = FMIndex(device=0, options={"cache_min": 4})
+            ours.initialize(docs, in_memory=True)
+        finally:
+            if old is None:
+                os.environ.pop("FMIDX_PROBE_COMPLETE")
+            else:
+                os.environ["FMIDX_PROBE_COMPLETE"] = old
+        st = ours.stats()
+        completes.append(st["trans_complete"])
+        n = ours.size()
+        lo, hi = ours.get_range_batch(pats, 10)
+        assert [(int(a), int(b)) for a, b in zip(lo, hi)][1:] == [tuple(w) for w in want0][1:]
+        # tokens: 50 % a symbol the parent lacks (a random id), 35 % a common token, 15 % past the vocabulary
+        r = rng.random(B)
+        tok = np.where(r < 0.5, rng.integers(0, V, B), np.where(r < 0.85, rng.choice(common, B), V + 5))
+        want = []
+        for b in range(B):
+            a_, b_ = (0, n) if not pats[b] else want0[b]
+            t = int(tok[b])
+            want.append((0, 0) if a_ >= b_ else ora.backward_search_step(t + 10, a_, b_ - 1))
+        want = [(a, b) if b > a else (0, 0) for a, b in want]
+        lo_t = torch.tensor(np.asarray(lo, dtype=np.int64), device=dev)
+        hi_t = torch.tensor(np.asarray(hi, dtype=np.int64), device=dev)
+        lo_t[0], hi_t[0] = 0, n
+        tk = torch.tensor(tok.astype(np.int64), device=dev)
+        # the in-wave LF sweep
+        lo2, hi2 = torch.empty_like(lo_t), torch.empty_like(hi_t)
+        with tuning(lf_work=-1, lf_sweep_min=1):
+            ours.lf_step_batch(tk, lo_t, hi_t, 10, lo_out=lo2, hi_out=hi2, reset_below=-1)
+        got = [(a, b) if b > a else (0, 0) for a, b in zip(lo2.cpu().tolist(), hi2.cpu().tolist())]
+        assert got == want, (pc, [(i, tok[i], want0[i], got[i], want[i]) for i in range(B) if got[i] != want[i]][:5])
+        # the fused decode step
+        mask = torch.empty((B, V), dtype=torch.uint8, device=dev)
+        lo3, hi3 = torch.empty_like(lo_t), torch.empty_like(hi_t)
+        ours.decode_step(tk, lo_t, hi_t, mask, V, 10, reset_below=-1, lo_out=lo3, hi_out=hi3)
+        got = [(a, b) if b > a else (0, 0) for a, b in zip(lo3.cpu().tolist(), hi3.cpu().tolist())]
+        assert got == want, pc
+        ref = allowed_mask(ora, [w[0] for w in want], [w[1] for w in want], V, 10)
+        assert np.array_equal(mask.cpu().numpy(), ref), pc
+        absent_wide = sum(1 for b in range(B) if want[b] == (0, 0) and want0[b][1] - want0[b][0] >= 4)
+        assert absent_wide > 50, absent_wide
+    assert completes == [0, 1]
