@@ -714,7 +714,8 @@ def sharded_leg(holder, text_seed, n_tokens, V, K, W, world, rank, dev, shs, hal
             except Exception as e:   # capture refused: the eager figures stand
                 modes["peer_flags_graph"] = {"value": None, "error": repr(e)}
         else:
-            modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0)"}
+            modes["peer"] = {"value": None, "error": peer_err or "disabled (FMIDX_BENCH_PEER=0, or the "
+                                                                      "peer preflight was not exact on every rank)"}
         # the headline sharded figure is a uint8 mask like the replica's; the packed-output mode is reported beside it
         exact_modes = [m for m, r in modes.items() if r.get("masks_equal_unsharded") and m != "peer_flags_packed"]
         best = min(exact_modes, key=lambda m: modes[m]["ms_per_step"]) if exact_modes else "sparse"
@@ -1035,6 +1036,93 @@ def after_replica_legs(holder, text_seed, n_tokens, V, B, K, W, dev, main_trace,
 
 
 # ---------------------------------------------------------------------------
+# The peer exchange's cross-device preflight (N > 1).  The sharded leg's peer modes are the first
+# code here to map another GPU's memory (hipIpc), store flag words over xGMI and read payloads in
+# place with system-scope loads; a GPU fault there would end the rank's process before its
+# measured line is printed.  So each rank first runs those mechanics in a CHILD process on a tiny
+# corpus: a fault ends the child only, and the ranks then skip the peer modes (dense and sparse
+# still run) with the reason in the line.
+PREFLIGHT_PORT_OFFSET = 101   # the children's gloo rendezvous: MASTER_PORT + this
+PREFLIGHT_TIMEOUT_S = 180.0
+
+
+def peer_preflight_child() -> int:
+    """``bench.py --peer-preflight``: ShardedDecoder(reduce="peer", the flag barrier, check="sync")
+    over 6 steps of a 400-doc corpus sharded WORLD_SIZE ways, against the unsharded decoder, on
+    device LOCAL_RANK (FMIDX_PREFLIGHT_DEVICE overrides it: the one-GPU test runs both ranks on
+    device 0).  The group is gloo on 127.0.0.1:FMIDX_PREFLIGHT_PORT (the IPC handles' exchange;
+    no RCCL communicator).  Returns the exit status: 0 exact, 1 inexact or an exception."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from fmidx.index import FMIndex as DocIndex
+    from fmidx.sharding import ShardedDecoder, shard_corpus
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    d = int(os.environ.get("FMIDX_PREFLIGHT_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(d)
+    dev = torch.device("cuda", d)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{int(os.environ['FMIDX_PREFLIGHT_PORT'])}",
+                            world_size=world, rank=rank, timeout=datetime.timedelta(seconds=120))
+    ok = False
+    try:
+        V, halo, B = 128256, 32, 64
+        rng = np.random.default_rng(17)
+        docs = [rng.integers(0, 900, size=int(rng.integers(5, 300))).tolist() for _ in range(400)]
+        full = DocIndex(device=d)
+        full.initialize(docs, in_memory=True)
+        sd, _ = shard_corpus(docs, world, rank, halo)
+        ix = DocIndex(device=d)
+        ix.initialize(sd, in_memory=True)
+        F = [t for doc in reversed(docs) for t in doc]
+        starts = np.random.default_rng(5).integers(0, len(F) - 20, size=B)
+        pats = [F[a:a + 2] for a in starts]
+        dec = ShardedDecoder(ix, V, 10, group=dist.group.WORLD, reduce="peer", halo=halo, peer_barrier="flags")
+        ref = ShardedDecoder(full, V, 10)
+        dec.start(pats, dev)
+        ref.start(pats, dev)
+        srng = np.random.default_rng(9)
+        bad = []
+        for step in range(6):
+            tok = [F[a + 2 + step] if srng.random() < 0.85 else int(srng.integers(-1, 900)) for a in starts]
+            if step == 3:
+                tok = [-1] * B   # every row restarts: every payload row a bitmap
+            t = torch.tensor(tok, dtype=torch.int64, device=dev)
+            if not torch.equal(dec.step(t), ref.step(t)):
+                bad.append(step)
+        dec.close()
+        ok = not bad
+        if bad:
+            log(f"peer preflight rank {rank}: masks differ from the unsharded index at steps {bad}")
+    except Exception as e:  # reported through the exit status; the parent records it
+        log(f"peer preflight rank {rank}: {e!r}")
+    finally:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+def peer_preflight(timeout_s: float = PREFLIGHT_TIMEOUT_S, cmd: list | None = None) -> tuple[bool, str]:
+    """Run this rank's preflight child (``cmd``: tests substitute a stub) and wait for it, at most
+    ``timeout_s`` (then it is killed).  -> (exact, what happened)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env["FMIDX_PREFLIGHT_PORT"] = str(int(os.environ.get("MASTER_PORT", "29500")) + PREFLIGHT_PORT_OFFSET)
+    cmd = cmd or [sys.executable, os.path.abspath(__file__), "--peer-preflight"]
+    t0 = time.time()
+    try:
+        # the child's stdout goes to stderr: stdout carries only the JSON line
+        rc = subprocess.run(cmd, env=env, stdout=sys.stderr, stderr=sys.stderr, timeout=timeout_s).returncode
+    except subprocess.TimeoutExpired:
+        return False, f"timed out after {timeout_s:g} s"
+    dt = time.time() - t0
+    if rc == 0:
+        return True, f"exact ({dt:.1f} s)"
+    return False, (f"exit status {rc}" if rc > 0 else f"killed by signal {-rc}") + f" ({dt:.1f} s)"
+
+
+# ---------------------------------------------------------------------------
 WATCHDOG_EXIT = 3   # a leg that hung: the line is printed, the run still fails
 
 
@@ -1075,6 +1163,8 @@ class LegWatchdog:
 
 
 def main():
+    if sys.argv[1:] == ["--peer-preflight"]:
+        sys.exit(peer_preflight_child())
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -1650,6 +1740,17 @@ def main():
                                                   args.cpu_window, args.cpu_reps, dev)
         except Exception as e:  # the GPU line must still print
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if want_sharded and world > 1 and os.environ.get("FMIDX_BENCH_PEER", "1") != "0":
+        # the peer modes' cross-device mechanics, first in a child process (see peer_preflight)
+        import torch.distributed as dist
+
+        pf_ok, pf_note = peer_preflight()
+        log(f"peer preflight: {pf_note}")
+        agree = torch.tensor([1 if pf_ok else 0], device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+        result["peer_preflight"] = {"exact_every_rank": bool(agree.item()), "rank0": pf_note}
+        if not int(agree.item()):
+            os.environ["FMIDX_BENCH_PEER"] = "0"   # the sharded leg's dense and sparse modes still run
     if want_sharded:
         if world == 1:
             import torch.distributed as dist

@@ -174,3 +174,39 @@ def test_leg_watchdog_finish_cancels(tmp_path):
     """)
     assert p.returncode == 0, p.stderr
     assert p.stdout.split() == ["line"]
+
+
+def test_peer_preflight_outcomes(tmp_path, monkeypatch):
+    """bench.peer_preflight (the N > 1 sharded leg's cross-device check, run in a child so a GPU
+    fault ends only the child): an exact child, a failing child, a crashed child and a hung
+    child (killed at the limit) give (True, ...), (False, "exit status 1"), (False, "killed by
+    signal ..."), (False, "timed out ..."); the child's rendezvous port is MASTER_PORT + 101 and
+    its stdout never reaches the parent's stdout (the JSON line's channel)."""
+    import subprocess
+
+    monkeypatch.setenv("MASTER_PORT", "29611")
+    ok = _stub(tmp_path, f"""
+        import os, sys
+        print("chatter on stdout")
+        open(os.path.join({str(tmp_path)!r}, "port"), "w").write(os.environ["FMIDX_PREFLIGHT_PORT"])
+    """)
+    p = subprocess.run([sys.executable, "-c", textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {REPO!r})
+        import bench
+        print(repr(bench.peer_preflight(cmd={ok!r})))
+    """)], capture_output=True, text=True, timeout=120, env=dict(os.environ))
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip().startswith("(True, 'exact"), p.stdout
+    assert "chatter on stdout" in p.stderr and "chatter" not in p.stdout
+    assert (tmp_path / "port").read_text() == str(29611 + bench.PREFLIGHT_PORT_OFFSET)
+    fail = _stub(tmp_path, "import sys; sys.exit(1)")
+    assert bench.peer_preflight(cmd=fail)[0] is False
+    assert bench.peer_preflight(cmd=fail)[1].startswith("exit status 1")
+    crash = _stub(tmp_path, "import os, signal; os.kill(os.getpid(), signal.SIGABRT)")
+    r = bench.peer_preflight(cmd=crash)
+    assert r[0] is False and r[1].startswith("killed by signal 6"), r
+    hang = _stub(tmp_path, "import time; time.sleep(60)")
+    t0 = time.time()
+    r = bench.peer_preflight(timeout_s=1.0, cmd=hang)
+    assert r == (False, "timed out after 1 s") and time.time() - t0 < 20

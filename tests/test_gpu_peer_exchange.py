@@ -282,3 +282,33 @@ def _spawn(fn, tmp_path, arg, limit):
                 p.kill()
     for r in range(WORLD):
         assert (tmp_path / f"r{r}.txt").read_text() == "ok", (r, (tmp_path / f"r{r}.txt").read_text())
+
+
+def test_bench_peer_preflight_two_processes(tmp_path):
+    """bench.py --peer-preflight, the child each rank runs before the N > 1 sharded leg's peer
+    modes: two children (RANK 0 / 1 of WORLD_SIZE 2) on this box's one GPU
+    (FMIDX_PREFLIGHT_DEVICE=0) map each other's buffers, decode 6 steps with the flag barrier
+    and check="sync", and both exit 0 (exact against the unsharded index)."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), FMIDX_PREFLIGHT_DEVICE="0",
+                   FMIDX_PREFLIGHT_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(repo, "bench.py"), "--peer-preflight"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=200)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert [p.returncode for p in procs] == [0, 0], outs
