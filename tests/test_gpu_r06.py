@@ -258,7 +258,8 @@ def test_probe_complete_absent_vs_oracle(dev):
     a transition table that holds every child of every cached parent, a probe
     finding no key beside a free slot ends the LF step as the empty range.  An
     index built with FMIDX_PROBE_COMPLETE=0 (the parent's bitmap word decides
-    instead) and the default one both equal the oracle -- decode steps (uint8
+    instead), the default one and one built with trans_min = 2 (an incomplete
+    table: the flag stays off) all equal the oracle -- decode steps (uint8
     mask + state) and the in-wave LF sweep -- on cached parents stepped with
     symbols they lack, symbols they hold, and past-vocabulary ids."""
     import torch
@@ -284,11 +285,12 @@ def test_probe_complete_absent_vs_oracle(dev):
     pats = [[]] + [[int(x) for x in rng.choice(common, int(rng.integers(1, 3)))] for _ in range(B - 1)]
     want0 = [ora.get_range(p) if p else (0, len(F) + 1) for p in pats]
     completes = []
-    for pc in ("0", "1"):
+    # (flag off, on, and a table built without the one-occurrence children: incomplete, so off)
+    for pc, extra in (("0", {}), ("1", {}), ("1", {"trans_min": 2})):
         old = os.environ.get("FMIDX_PROBE_COMPLETE")
         os.environ["FMIDX_PROBE_COMPLETE"] = pc
         try:
-            ours = FMIndex(device=0, options={"cache_min": 4})
+            ours = FMIndex(device=0, options={"cache_min": 4, **extra})
             ours.initialize(docs, in_memory=True)
         finally:
             if old is None:
@@ -329,4 +331,4 @@ def test_probe_complete_absent_vs_oracle(dev):
         assert np.array_equal(mask.cpu().numpy(), ref), pc
         absent_wide = sum(1 for b in range(B) if want[b] == (0, 0) and want0[b][1] - want0[b][0] >= 4)
         assert absent_wide > 50, absent_wide
-    assert completes == [0, 1]
+    assert completes == [0, 1, 0]
